@@ -1,0 +1,555 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Runs only in the development container (the reference is mounted read-only
+at /root/reference and never travels to the GPU box).  The reference is
+imported unmodified from a scratch cwd; its global ``random`` module is
+replaced by ``gzero.rng.StreamSet`` (the counter-based sub-streams the HIP
+engine and the C oracle use), and three methods are wrapped purely to select
+the sub-stream (game, ply, sim) and to observe results:
+
+* ``AlphaZeroGomokuAI.get_move``      -> main stream of (game, ply)
+* ``AlphaZeroGomokuAI._mcts_search``  -> resets the simulation counter
+* ``AlphaZeroGomokuAI._mcts_simulation`` -> stream ``sim = k`` while simulation k runs
+* ``MCTSNode.__init__`` / ``GomokuModel.predict`` -> capture the root, count forwards
+
+Usage:  python tests/golden/make_golden.py [part ...]   (parts: board pattern
+policy rollout mcts games tables; default = all)
+
+Each part writes ``tests/golden/<part>.json.gz``.
+"""
+import gzip
+import json
+import math
+import os
+import sys
+import tempfile
+import time
+import zlib
+from multiprocessing import Pool
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "alphazero-gomoku_amd"))
+from gzero.rng import StreamSet  # noqa: E402
+
+REF = "/root/reference"
+N = 15
+SEED = 20251003
+
+_ref = None
+
+
+def ref():
+    """Import the reference once per process, from a scratch cwd."""
+    global _ref
+    if _ref is not None:
+        return _ref
+    sys.dont_write_bytecode = True
+    os.chdir(tempfile.mkdtemp(prefix="gz_ref_"))
+    sys.path.insert(0, REF)
+    import torch
+    torch.set_num_threads(1)
+    import gomoku_board
+    import neural_network
+    import bg_planner
+    import ai_agent
+    import training
+
+    class H:
+        pass
+
+    h = H()
+    h.gb, h.nn, h.bg, h.ai, h.tr = gomoku_board, neural_network, bg_planner, ai_agent, training
+    h.rs = StreamSet(SEED)
+    for m in (ai_agent, bg_planner, training):
+        m.random = h.rs
+    h.last_root = None
+    h.predicts = 0
+    h.sim_counter = 0
+
+    A = ai_agent.AlphaZeroGomokuAI
+    orig_get_move = A.get_move
+    orig_search = A._mcts_search
+    orig_sim = A._mcts_simulation
+
+    def get_move(self, board):
+        h.rs.set(ply=board.get_move_count(), sim=0)
+        return orig_get_move(self, board)
+
+    def mcts_search(self, board, valid):
+        h.sim_counter = 0
+        return orig_search(self, board, valid)
+
+    def mcts_sim(self, root):
+        h.sim_counter += 1
+        h.rs.set(sim=h.sim_counter)
+        try:
+            return orig_sim(self, root)
+        finally:
+            h.rs.set(sim=0)
+
+    A.get_move = get_move
+    A._mcts_search = mcts_search
+    A._mcts_simulation = mcts_sim
+
+    orig_node_init = ai_agent.MCTSNode.__init__
+
+    def node_init(self, board, parent, *a, **k):
+        orig_node_init(self, board, parent, *a, **k)
+        if parent is None:
+            h.last_root = self
+
+    ai_agent.MCTSNode.__init__ = node_init
+
+    orig_predict = neural_network.GomokuModel.predict
+
+    def predict(self, state):
+        h.predicts += 1
+        return orig_predict(self, state)
+
+    neural_network.GomokuModel.predict = predict
+    _ref = h
+    return h
+
+
+# ---------------------------------------------------------------------------
+# position generation (own code, replayed through the reference board)
+# ---------------------------------------------------------------------------
+
+def _wins(cells, r, c, p):
+    for dr, dc in ((0, 1), (1, 0), (1, 1), (1, -1)):
+        cnt = 1
+        for s in (1, -1):
+            rr, cc = r + s * dr, c + s * dc
+            while 0 <= rr < N and 0 <= cc < N and cells[rr * N + cc] == p:
+                cnt += 1
+                rr += s * dr
+                cc += s * dc
+        if cnt >= 5:
+            return True
+    return False
+
+
+def gen_moves(rng, length, avoid_five=True, near=False):
+    """A move sequence of ``length`` plies that (if avoid_five) never completes five."""
+    for _ in range(100):
+        cells = [0] * (N * N)
+        nearby = set()
+        moves = []
+        p = 1
+        ok = True
+        for _ply in range(length):
+            empty = [i for i in range(N * N) if cells[i] == 0]
+            if near and moves:
+                cand = [i for i in empty if i in nearby]
+                if cand and rng.random() < 0.85:
+                    empty = cand
+            rng.shuffle(empty)
+            mv = None
+            for i in empty:
+                if not avoid_five or not _wins(cells, i // N, i % N, p):
+                    mv = i
+                    break
+            if mv is None:
+                ok = False
+                break
+            if not avoid_five and _wins(cells, mv // N, mv % N, p):
+                moves.append(mv)  # the game ends here; stop the sequence
+                return moves
+            cells[mv] = p
+            r0, c0 = divmod(mv, N)
+            for rr in range(max(0, r0 - 2), min(N, r0 + 3)):
+                for cc in range(max(0, c0 - 2), min(N, c0 + 3)):
+                    nearby.add(rr * N + cc)
+            moves.append(mv)
+            p = 3 - p
+        if ok:
+            return moves
+    raise RuntimeError("could not generate position")
+
+
+def replay(h, moves):
+    b = h.gb.GomokuBoard()
+    for m in moves:
+        assert b.make_move(m // N, m % N), moves
+    return b
+
+
+def board_str(b):
+    return "".join(str(int(v)) for v in b.board.reshape(-1))
+
+
+def legal_hex(b):
+    x = 0
+    for r, c in b.get_valid_moves():
+        x |= 1 << (r * N + c)
+    return format(x, "057x")
+
+
+def dump(name, obj):
+    path = os.path.join(HERE, name + ".json.gz")
+    with gzip.open(path, "wt") as f:
+        json.dump(obj, f, separators=(",", ":"))
+    print(f"wrote {path} ({os.path.getsize(path)} bytes)", flush=True)
+
+
+# ---------------------------------------------------------------------------
+# G1 board
+# ---------------------------------------------------------------------------
+
+def part_board():
+    import random as pyrandom
+    h = ref()
+    rng = pyrandom.Random(1)
+    games = []
+    for g in range(240):
+        b = h.gb.GomokuBoard()
+        moves, oks, overs, winners, players, masks = [], [], [], [], [], []
+        avoid = g % 3 == 0
+        cells = [0] * 225
+        while True:
+            empty = [i for i in range(225) if cells[i] == 0]
+            if not empty:
+                break
+            rng.shuffle(empty)
+            mv = empty[0]
+            if avoid:
+                for i in empty:
+                    if not _wins(cells, i // N, i % N, b.current_player):
+                        mv = i
+                        break
+            # occasionally try an illegal move (occupied / off-board / after game over)
+            if rng.random() < 0.05 and any(cells):
+                occ = [i for i in range(225) if cells[i]]
+                bad = rng.choice(occ)
+                ok = b.make_move(bad // N, bad % N)
+                moves.append(bad)
+                oks.append(bool(ok))
+                overs.append(bool(b.game_over))
+                winners.append(b.winner if b.winner is not None else 0)
+                players.append(b.current_player)
+                masks.append(legal_hex(b))
+            ok = b.make_move(mv // N, mv % N)
+            if ok:
+                cells[mv] = 3 - b.current_player
+            moves.append(mv)
+            oks.append(bool(ok))
+            overs.append(bool(b.game_over))
+            winners.append(b.winner if b.winner is not None else 0)
+            players.append(b.current_player)
+            masks.append(legal_hex(b))
+            if b.game_over:
+                # one extra attempt after game over must fail
+                extra = [i for i in range(225) if cells[i] == 0]
+                if extra:
+                    e = extra[0]
+                    ok = b.make_move(e // N, e % N)
+                    moves.append(e)
+                    oks.append(bool(ok))
+                    overs.append(bool(b.game_over))
+                    winners.append(b.winner if b.winner is not None else 0)
+                    players.append(b.current_player)
+                    masks.append(legal_hex(b))
+                break
+        crc = zlib.crc32("".join(masks).encode())
+        games.append({"moves": moves, "ok": oks, "over": overs, "winner": winners,
+                      "player": players, "mask_crc32": crc,
+                      "masks": masks if g < 16 else None,
+                      "n_history": len(b.move_history)})
+    # off-board attempts
+    b = h.gb.GomokuBoard()
+    offboard = [[r, c, bool(b.make_move(r, c))] for r, c in ((-1, 0), (0, -1), (15, 0), (0, 15), (15, 15), (-1, -1))]
+    # crafted: overline of six, each direction through edges
+    crafted = []
+    lines = {
+        "row_edge": [(0, c) for c in range(5)],
+        "col_edge": [(r, 14) for r in range(10, 15)],
+        "diag_corner": [(i, i) for i in range(10, 15)],
+        "anti_corner": [(i, 14 - i) for i in range(0, 5)],
+        "anti_bottom": [(14 - i, i) for i in range(0, 5)],
+    }
+    for name, cells5 in lines.items():
+        for order in (list(range(5)), [0, 1, 3, 4, 2], [4, 3, 2, 1, 0]):
+            bb = h.gb.GomokuBoard()
+            seq = []
+            fillers = [(r, c) for r in range(N) for c in range(N)
+                       if (r, c) not in cells5 and all(abs(r - x) + abs(c - y) > 2 for x, y in cells5)]
+            for k, idx in enumerate(order):
+                r, c = cells5[idx]
+                seq.append(r * N + c)
+                bb.make_move(r, c)
+                if k < 4:
+                    fr, fc = fillers[k * 7 % len(fillers)]
+                    seq.append(fr * N + fc)
+                    bb.make_move(fr, fc)
+            crafted.append({"name": name, "moves": seq, "over": bool(bb.game_over),
+                            "winner": bb.winner or 0})
+    # overline: XX.XXX -> filling the gap makes six
+    bb = h.gb.GomokuBoard()
+    seq = []
+    for c, f in zip((0, 1, 3, 4, 5), ((10, 0), (10, 2), (10, 4), (10, 6), (10, 8))):
+        seq += [7 * N + c, f[0] * N + f[1]]
+        bb.make_move(7, c)
+        bb.make_move(*f)
+    pre_over = bool(bb.game_over)
+    seq.append(7 * N + 2)
+    bb.make_move(7, 2)
+    crafted.append({"name": "overline6", "moves": seq, "over": bool(bb.game_over),
+                    "winner": bb.winner or 0, "pre_over": pre_over})
+    # 200-ply draw
+    mv = gen_moves(rng, 200, avoid_five=True)
+    bb = replay(h, mv[:199])
+    o199 = bool(bb.game_over)
+    bb.make_move(mv[199] // N, mv[199] % N)
+    crafted.append({"name": "draw200", "moves": mv, "over": bool(bb.game_over),
+                    "winner": bb.winner or 0, "over_at_199": o199})
+    dump("board", {"games": games, "offboard": offboard, "crafted": crafted})
+
+
+# ---------------------------------------------------------------------------
+# G3 pattern score
+# ---------------------------------------------------------------------------
+
+def part_pattern():
+    import numpy as np
+    import random as pyrandom
+    h = ref()
+    ks = h.bg.KnowledgeSearch(15)
+    scores = {'FIVE': 100000.0, 'LIVE_FOUR': 10000.0, 'RUSH_FOUR': 5000.0,
+              'DOUBLE_LIVE_THREE': 3000.0, 'LIVE_THREE': 1000.0, 'RUSH_THREE': 300.0,
+              'LIVE_TWO': 50.0}
+    # LUT over the 8 non-centre cells (0 = me, 1 = empty, 2 = other)
+    lut = []
+    for code in range(3 ** 8):
+        digits = []
+        x = code
+        for _ in range(8):
+            digits.append(x % 3)
+            x //= 3
+        vals = {}
+        for player in (1, 2):
+            for blocked in (-1, 3 - player):
+                seg = []
+                for j in range(9):
+                    if j == 4:
+                        seg.append(player)
+                        continue
+                    d = digits[j if j < 4 else j - 1]
+                    seg.append(player if d == 0 else (0 if d == 1 else blocked))
+                vals[(player, blocked)] = ks._eval_segment(seg, scores, player)
+        vs = set(vals.values())
+        assert len(vs) == 1, (code, vals)
+        lut.append(int(vs.pop()))
+    rng = pyrandom.Random(3)
+    positions = []
+    ai = h.ai.AlphaZeroGomokuAI(1, "medium", device="cpu", time_limit=float("inf"))
+    for i in range(1500):
+        L = rng.randint(0, 160)
+        mv = gen_moves(rng, L, avoid_five=rng.random() < 0.8, near=rng.random() < 0.6)
+        b = replay(h, mv)
+        s1 = ks._pattern_score(b, 1)
+        s2 = ks._pattern_score(b, 2)
+        positions.append({"moves": mv, "s1": s1, "s2": s2,
+                          "bg1": ai._bg_score(b, 1), "bg2": ai._bg_score(b, 2)})
+    dump("pattern", {"lut": lut, "positions": positions})
+
+
+# ---------------------------------------------------------------------------
+# G2 rollout policy (one step) and full rollouts
+# ---------------------------------------------------------------------------
+
+def _policy_task(args):
+    idx, moves = args
+    h = ref()
+    if not hasattr(h, "policy_ai"):
+        h.policy_ai = h.ai.AlphaZeroGomokuAI(1, "medium", device="cpu", time_limit=float("inf"))
+    b = replay(h, moves)
+    h.rs.set(game_id=idx, ply=len(moves), sim=1)
+    mv = h.policy_ai._select_offensive_move(b, b.get_valid_moves())
+    return {"moves": moves, "move": mv[0] * N + mv[1], "draws": h.rs.count(idx, len(moves), 1)}
+
+
+def part_policy():
+    import random as pyrandom
+    rng = pyrandom.Random(5)
+    tasks = []
+    for i in range(3000):
+        kind = i % 4
+        if kind == 0:
+            L = rng.randint(0, 12)
+            mv = gen_moves(rng, L, avoid_five=True, near=False)
+        elif kind == 1:
+            L = rng.randint(4, 60)
+            mv = gen_moves(rng, L, avoid_five=True, near=True)
+        elif kind == 2:
+            L = rng.randint(20, 198)
+            mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.5)
+        else:
+            L = rng.randint(1, 30)
+            mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.3)
+        tasks.append((i, mv))
+    with Pool(8) as pool:
+        out = pool.map(_policy_task, tasks, chunksize=20)
+    dump("policy", {"seed": SEED, "cases": out})
+
+
+def _rollout_task(args):
+    idx, moves, player = args
+    h = ref()
+    key = ("rollout_ai", player)
+    if not hasattr(h, "ais"):
+        h.ais = {}
+    if key not in h.ais:
+        h.ais[key] = h.ai.AlphaZeroGomokuAI(player, "medium", device="cpu", planner_steps=0,
+                                            time_limit=float("inf"))
+    ai = h.ais[key]
+    b = replay(h, moves)
+    node = h.ai.MCTSNode(b, None, None, ai.model, ai.params, bg_beta=ai.beta,
+                         bg_scorer=ai._bg_score, current_player=ai.player)
+    captured = {}
+    orig = ai._get_terminal_value
+
+    def gtv(board):
+        captured["b"] = board
+        return orig(board)
+
+    ai._get_terminal_value = gtv
+    h.rs.set(game_id=idx, ply=len(moves), sim=1)
+    v = ai._simulate(node)
+    del ai._get_terminal_value
+    fb = captured["b"]
+    return {"moves": moves, "player": player, "value": v, "final": board_str(fb),
+            "final_n": len(fb.move_history), "over": bool(fb.game_over),
+            "winner": fb.winner or 0, "draws": h.rs.count(idx, len(moves), 1)}
+
+
+def part_rollout():
+    import random as pyrandom
+    rng = pyrandom.Random(7)
+    tasks = []
+    for i in range(320):
+        L = [6, 10, 20, 40, 80, 120, 160, 185][i % 8] + rng.randint(0, 4)
+        mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.6)
+        player = 1 + (len(mv) % 2) if i % 5 else 2 - (len(mv) % 2)
+        tasks.append((i, mv, player))
+    with Pool(8) as pool:
+        out = pool.map(_rollout_task, tasks, chunksize=2)
+    dump("rollout", {"seed": SEED, "cases": out})
+
+
+# ---------------------------------------------------------------------------
+# G6 MCTS get_move
+# ---------------------------------------------------------------------------
+
+def _mcts_task(args):
+    idx, moves, sims, beta, difficulty = args
+    h = ref()
+    b = replay(h, moves)
+    player = b.current_player
+    ai = h.ai.AlphaZeroGomokuAI(player, difficulty, device="cpu", beta=beta, planner_steps=0,
+                                time_limit=float("inf"))
+    ai.params["num_simulations"] = sims
+    h.rs.set(game_id=idx)
+    h.last_root = None
+    h.predicts = 0
+    t0 = time.time()
+    mv = ai.get_move(b)
+    dt = time.time() - t0
+    root = h.last_root
+    ply = len(moves)
+    res = {"moves": moves, "sims": sims, "beta": beta, "difficulty": difficulty,
+           "game_id": idx, "move": None if mv is None else mv[0] * N + mv[1],
+           "predicts": h.predicts, "main_draws": h.rs.count(idx, ply, 0),
+           "sim_draws": [h.rs.count(idx, ply, k) for k in range(1, sims + 1)], "seconds": dt}
+    if root is not None and len(moves) >= 6:
+        res["root_visits"] = root.visits
+        res["root_value"] = root.value
+        res["children"] = [[c.move[0] * N + c.move[1], c.visits, c.value] for c in root.children]
+        # second level (children of children) for the sequential phase
+        res["grand"] = [[ci, c2.move[0] * N + c2.move[1], c2.visits, c2.value]
+                        for ci, c in enumerate(root.children) for c2 in c.children]
+    return res
+
+
+def part_mcts():
+    import random as pyrandom
+    rng = pyrandom.Random(11)
+    tasks = []
+    i = 0
+    # opening plies and tiny searches
+    for L in range(0, 6):
+        for sims in (1, 3):
+            tasks.append((i, gen_moves(rng, L, avoid_five=True, near=False), sims, 0.2, "medium")); i += 1
+    for _ in range(8):
+        L = rng.randint(6, 14)
+        sims = rng.choice([1, 2, 5, 8])
+        tasks.append((i, gen_moves(rng, L, True, True), sims, rng.choice([0.0, 0.2]), "medium")); i += 1
+    # sequential phase (sims > legal + 1): late positions, short rollouts
+    for k in range(24):
+        L = rng.randint(150, 190)
+        legal = 225 - L
+        sims = legal + 1 + rng.randint(5, 40)
+        tasks.append((i, gen_moves(rng, L, True, rng.random() < 0.5), sims,
+                      [0.0, 0.2][k % 2], ["medium", "easy", "hard"][k % 3])); i += 1
+    # mid-game, parallel + some sequential
+    for k in range(8):
+        L = rng.randint(110, 140)
+        legal = 225 - L
+        sims = legal + 1 + rng.randint(3, 12)
+        tasks.append((i, gen_moves(rng, L, True, True), sims, [0.0, 0.2][k % 2], "medium")); i += 1
+    # the metric's setting: 200 sims, early-mid game (parallel phase only / a few sequential)
+    for k in range(4):
+        L = [6, 12, 30, 40][k]
+        tasks.append((i, gen_moves(rng, L, True, True), 200, [0.0, 0.2][k % 2], "medium")); i += 1
+    tasks.sort(key=lambda t: -t[2] * (1 if len(t[1]) < 100 else 0.2))
+    with Pool(8) as pool:
+        out = pool.map(_mcts_task, tasks, chunksize=1)
+    out.sort(key=lambda r: r["game_id"])
+    dump("mcts", {"seed": SEED, "cases": out})
+
+
+# ---------------------------------------------------------------------------
+# G7 full self-play games (training.play_one_game)
+# ---------------------------------------------------------------------------
+
+def _game_task(args):
+    gid, sims, beta, difficulty = args
+    h = ref()
+    inf = float("inf")
+    ab = h.ai.AlphaZeroGomokuAI(1, difficulty, device="cpu", beta=beta, planner_steps=0, time_limit=inf)
+    aw = h.ai.AlphaZeroGomokuAI(2, difficulty, device="cpu", beta=beta, planner_steps=0, time_limit=inf)
+    ab.params["num_simulations"] = sims
+    aw.params["num_simulations"] = sims
+    aw.model = ab.model
+    h.rs.set(game_id=gid)
+    h.predicts = 0
+    import io
+    import contextlib
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        buf, glen = h.tr.play_one_game(ab, aw, step_timeout=inf, game_timeout=inf)
+    dt = time.time() - t0
+    return {"game_id": gid, "sims": sims, "beta": beta, "difficulty": difficulty,
+            "moves": buf.move_indices, "players": buf.players, "outcomes": buf.outcomes,
+            "len": glen, "predicts": h.predicts, "seconds": dt,
+            "planes_crc32": zlib.crc32(b"".join(s.tobytes() for s in buf.states))}
+
+
+def part_games():
+    tasks = [(100 + g, 2, [0.0, 0.2][g % 2], "medium") for g in range(6)]
+    tasks += [(200 + g, 3, 0.2, ["easy", "hard"][g % 2]) for g in range(2)]
+    with Pool(8) as pool:
+        out = pool.map(_game_task, tasks, chunksize=1)
+    dump("games", {"seed": SEED, "games": out})
+
+
+PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
+         "rollout": part_rollout, "mcts": part_mcts, "games": part_games}
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(PARTS)
+    for n in names:
+        t = time.time()
+        PARTS[n]()
+        print(f"part {n} done in {time.time() - t:.1f}s", flush=True)
