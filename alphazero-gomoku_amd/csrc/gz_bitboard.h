@@ -17,10 +17,27 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 #if defined(__HIPCC__)
 #define GZ_HD __host__ __device__ inline
 #else
 #define GZ_HD static inline
+#endif
+
+// keep the scheduler from interleaving independent directions (bounds live registers)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GZ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define GZ_SCHED_FENCE() ((void)0)
+#endif
+
+// materialise a value in a VGPR here: stops the compiler from re-associating an
+// OR-accumulation across directions (which keeps every partial result live)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GZ_PIN(x) asm volatile("" : "+v"(x))
+#else
+#define GZ_PIN(x) ((void)0)
 #endif
 
 #define GZ_N 15
@@ -84,7 +101,15 @@ GZ_HD BB bb_valid() {
     return r;
 }
 
-GZ_HD bool bb_test(const BB& x, int bit) { return (x.w[bit >> 5] >> (bit & 31)) & 1u; }
+// word selected by compare/select (no dynamic register indexing -> no scratch)
+GZ_HD uint32_t bb_word(const BB& x, int wi) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < GZ_W; i++) w = (i == wi) ? x.w[i] : w;
+    return w;
+}
+
+GZ_HD bool bb_test(const BB& x, int bit) { return (bb_word(x, bit >> 5) >> (bit & 31)) & 1u; }
 
 GZ_HD int bb_count(const BB& x) {
     int n = 0;
@@ -102,42 +127,63 @@ GZ_HD bool bb_any(const BB& x) {
 
 // (hi:lo) >> s for 0 < s < 32 (v_alignbit_b32 on gfx950)
 GZ_HD uint32_t funnel(uint32_t hi, uint32_t lo, int s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)s);
+#else
     return (uint32_t)((((uint64_t)hi << 32) | (uint64_t)lo) >> s);
+#endif
 }
 
-// X << S (bit b receives bit b - S), S compile time
+// compile-time loop over word indices (guarantees register-resident words)
+template <int I, int N, typename F>
+GZ_HD void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// word I of (X << S): bit b receives bit b - S
+template <int S, int I>
+GZ_HD uint32_t shl_w(const BB& x) {
+    constexpr int q = S >> 5, r = S & 31;
+    constexpr int ci = I - q, pi = I - q - 1;
+    uint32_t cur = 0, prev = 0;
+    if constexpr (ci >= 0 && ci < GZ_W) cur = x.w[ci];
+    if constexpr (r == 0) {
+        return cur;
+    } else {
+        if constexpr (pi >= 0 && pi < GZ_W) prev = x.w[pi];
+        return funnel(cur, prev, 32 - r);
+    }
+}
+
+// word I of (X >> S): bit b receives bit b + S
+template <int S, int I>
+GZ_HD uint32_t shr_w(const BB& x) {
+    constexpr int q = S >> 5, r = S & 31;
+    constexpr int ci = I + q, ni = I + q + 1;
+    uint32_t cur = 0, next = 0;
+    if constexpr (ci >= 0 && ci < GZ_W) cur = x.w[ci];
+    if constexpr (r == 0) {
+        return cur;
+    } else {
+        if constexpr (ni >= 0 && ni < GZ_W) next = x.w[ni];
+        return funnel(next, cur, r);
+    }
+}
+
 template <int S>
 GZ_HD BB shl(const BB& x) {
-    constexpr int q = S >> 5, r = S & 31;
     BB o;
-#pragma unroll
-    for (int i = 0; i < GZ_W; i++) {
-        uint32_t cur = (i - q >= 0) ? x.w[i - q] : 0u;
-        if (r == 0) {
-            o.w[i] = cur;
-        } else {
-            uint32_t prev = (i - q - 1 >= 0) ? x.w[i - q - 1] : 0u;
-            o.w[i] = funnel(cur, prev, 32 - r);
-        }
-    }
+    static_for<0, GZ_W>([&](auto ic) { o.w[decltype(ic)::value] = shl_w<S, decltype(ic)::value>(x); });
     return o;
 }
 
-// X >> S (bit b receives bit b + S)
 template <int S>
 GZ_HD BB shr(const BB& x) {
-    constexpr int q = S >> 5, r = S & 31;
     BB o;
-#pragma unroll
-    for (int i = 0; i < GZ_W; i++) {
-        uint32_t cur = (i + q < GZ_W) ? x.w[i + q] : 0u;
-        if (r == 0) {
-            o.w[i] = cur;
-        } else {
-            uint32_t next = (i + q + 1 < GZ_W) ? x.w[i + q + 1] : 0u;
-            o.w[i] = funnel(next, cur, r);
-        }
-    }
+    static_for<0, GZ_W>([&](auto ic) { o.w[decltype(ic)::value] = shr_w<S, decltype(ic)::value>(x); });
     return o;
 }
 
@@ -161,20 +207,14 @@ GZ_HD BB empties(const BB& a, const BB& b) {
     return o;
 }
 
-// Centre buckets of _select_offensive_move step 5 (ai_agent.py:339-361):
-// Manhattan distance to (7,7) <= 2, in (2, 4], > 4.
-GZ_HD BB centre_mask(int lo, int hi) {
-    BB o = bb_zero();
-    for (int r = 0; r < GZ_N; r++)
-        for (int c = 0; c < GZ_N; c++) {
-            int d = (r > 7 ? r - 7 : 7 - r) + (c > 7 ? c - 7 : 7 - c);
-            if (d >= lo && d <= hi) {
-                int b = r * 16 + c;
-                o.w[b >> 5] |= 1u << (b & 31);
-            }
-        }
-    return o;
-}
+// Constant masks.  Centre buckets of _select_offensive_move step 5
+// (ai_agent.py:339-361): Manhattan distance to (7,7) <= 2, in [3, 4], > 4.
+// Opening squares of _opening_move (ai_agent.py:152-163): Chebyshev <= 1, <= 2.
+#define GZ_MASK_C2 {{0x00000000u, 0x00000000u, 0x00800000u, 0x03E001C0u, 0x008001C0u, 0x00000000u, 0x00000000u, 0x00000000u}}
+#define GZ_MASK_C4 {{0x00000000u, 0x00800000u, 0x036001C0u, 0x0C180630u, 0x03600630u, 0x008001C0u, 0x00000000u, 0x00000000u}}
+#define GZ_MASK_CE {{0x7FFF7FFFu, 0x7F7F7FFFu, 0x7C1F7E3Fu, 0x7007780Fu, 0x7C1F780Fu, 0x7F7F7E3Fu, 0x7FFF7FFFu, 0x00007FFFu}}
+#define GZ_MASK_K3 {{0x00000000u, 0x00000000u, 0x00000000u, 0x01C001C0u, 0x000001C0u, 0x00000000u, 0x00000000u, 0x00000000u}}
+#define GZ_MASK_K5 {{0x00000000u, 0x00000000u, 0x03E00000u, 0x03E003E0u, 0x03E003E0u, 0x00000000u, 0x00000000u, 0x00000000u}}
 
 // ------------------------------------------------------------ threat analysis
 struct Threats {
@@ -183,41 +223,51 @@ struct Threats {
     bool has3;    // the player already has a run >= 3 somewhere
 };
 
+// One direction of the threat analysis, computed word by word so that only a
+// handful of shifted words are live at a time.
 template <int D>
-GZ_HD void threats_dir(const BB& m, Threats& t) {
-    BB a1 = shl<D>(m), a2 = shl<2 * D>(m), a3 = shl<3 * D>(m), a4 = shl<4 * D>(m);
-    BB b1 = shr<D>(m), b2 = shr<2 * D>(m), b3 = shr<3 * D>(m), b4 = shr<4 * D>(m);
-    BB l2 = a1 & a2, l3 = l2 & a3, l4 = l3 & a4;
-    BB r2 = b1 & b2, r3 = r2 & b3, r4 = r2 & b3 & b4;
-    uint32_t h = 0;
-#pragma unroll
-    for (int i = 0; i < GZ_W; i++) {
-        uint32_t w = l4.w[i] | r4.w[i] | (a1.w[i] & r3.w[i]) | (l2.w[i] & r2.w[i]) | (l3.w[i] & b1.w[i]);
-        t.win.w[i] |= w;
-        t.make3.w[i] |= l2.w[i] | r2.w[i] | (a1.w[i] & b1.w[i]);
-        h |= m.w[i] & l2.w[i];
-    }
-    t.has3 = t.has3 || (h != 0);
+GZ_HD void threats_dir(const BB& m, Threats& t, uint32_t& h) {
+    static_for<0, GZ_W>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t a1 = shl_w<D, i>(m), a2 = shl_w<2 * D, i>(m);
+        const uint32_t a3 = shl_w<3 * D, i>(m), a4 = shl_w<4 * D, i>(m);
+        const uint32_t b1 = shr_w<D, i>(m), b2 = shr_w<2 * D, i>(m);
+        const uint32_t b3 = shr_w<3 * D, i>(m), b4 = shr_w<4 * D, i>(m);
+        const uint32_t l2 = a1 & a2, l3 = l2 & a3, l4 = l3 & a4;
+        const uint32_t r2 = b1 & b2, r3 = r2 & b3, r4 = r3 & b4;
+        t.win.w[i] |= l4 | r4 | (a1 & r3) | (l2 & r2) | (l3 & b1);
+        t.make3.w[i] |= l2 | r2 | (a1 & b1);
+        h |= m.w[i] & l2;
+        GZ_PIN(t.win.w[i]);
+        GZ_PIN(t.make3.w[i]);
+    });
+    GZ_PIN(h);
 }
 
 GZ_HD Threats threats(const BB& m) {
     Threats t;
     t.win = bb_zero();
     t.make3 = bb_zero();
-    t.has3 = false;
-    threats_dir<1>(m, t);
-    threats_dir<16>(m, t);
-    threats_dir<17>(m, t);
-    threats_dir<15>(m, t);
+    uint32_t h = 0;
+    threats_dir<1>(m, t, h);
+    GZ_SCHED_FENCE();
+    threats_dir<16>(m, t, h);
+    GZ_SCHED_FENCE();
+    threats_dir<17>(m, t, h);
+    GZ_SCHED_FENCE();
+    threats_dir<15>(m, t, h);
+    GZ_SCHED_FENCE();
+    t.has3 = h != 0;
     return t;
 }
 
 template <int D>
 GZ_HD uint32_t run3_dir(const BB& m) {
-    BB a1 = shl<D>(m), a2 = shl<2 * D>(m);
     uint32_t h = 0;
-#pragma unroll
-    for (int i = 0; i < GZ_W; i++) h |= m.w[i] & a1.w[i] & a2.w[i];
+    static_for<0, GZ_W>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        h |= m.w[i] & shl_w<D, i>(m) & shl_w<2 * D, i>(m);
+    });
     return h;
 }
 
@@ -275,7 +325,12 @@ GZ_HD int select_bit(const BB& x, int k) {
     return base + pos;
 }
 
-GZ_HD void bb_set(BB& x, int bit) { x.w[bit >> 5] |= 1u << (bit & 31); }
+GZ_HD void bb_set(BB& x, int bit) {
+    const int wi = bit >> 5;
+    const uint32_t m = 1u << (bit & 31);
+#pragma unroll
+    for (int i = 0; i < GZ_W; i++) x.w[i] |= (i == wi) ? m : 0u;
+}
 
 // ---------------------------------------------------------------- rollout policy
 // One move of _select_offensive_move (ai_agent.py:306-361) for the side to move
@@ -286,10 +341,7 @@ struct Centre {
 };
 
 GZ_HD Centre centre_buckets() {
-    Centre c;
-    c.c2 = centre_mask(0, 2);
-    c.c4 = centre_mask(3, 4);
-    c.ce = centre_mask(5, 100);
+    Centre c = {GZ_MASK_C2, GZ_MASK_C4, GZ_MASK_CE};
     return c;
 }
 

@@ -1,0 +1,40 @@
+// gz_pvnet.h -- packed weight layout of AlphaZeroGomokuNet (neural_network.py:94-159)
+// for the fp32 MFMA forward.  Produced by gzero/weights.py:pack_pv_weights().
+//
+// Conv weights are stored K-major as the GEMM B operand W[k][n]:
+//   conv0:     k = tap*3 + cin   (27 rows + 1 zero row), n = out channel (128)
+//   res convs: k = tap*128 + cin (1152 rows),           n = out channel (128)
+// with tap = kh*3 + kw.  Bias and eval-mode BatchNorm are folded into a
+// per-channel affine epilogue: y = acc*S[n] + T[n],
+//   S = gamma / sqrt(running_var + eps), T = (bias - running_mean)*S + beta.
+// Head weights: 1x1 convs as [out][128]; FCs stored transposed ([in][out]) so a
+// thread per output reads coalesced rows.
+#pragma once
+
+namespace gzpv {
+constexpr int CH = 128;
+constexpr int POS = 225;
+constexpr int K0 = 28;          // 27 padded to a multiple of the MFMA K-step (2)
+constexpr int K = 9 * CH;       // 1152
+
+constexpr int C0_W = 0;
+constexpr int C0_S = C0_W + K0 * CH;
+constexpr int C0_T = C0_S + CH;
+constexpr int RES0 = C0_T + CH;
+constexpr int RES_STRIDE = K * CH + 2 * CH;  // W, S, T
+constexpr int RES_W = 0, RES_S = K * CH, RES_T = K * CH + CH;
+constexpr int P_W = RES0 + 4 * RES_STRIDE;   // [2][128]
+constexpr int P_B = P_W + 2 * CH;            // [2] (+2 pad)
+constexpr int PF_WT = P_B + 4;               // [450][225]
+constexpr int PF_B = PF_WT + 450 * 225;      // [225] (+3 pad)
+constexpr int V_W = PF_B + 228;              // [128]
+constexpr int V_B = V_W + CH;                // [1] (+3 pad)
+constexpr int V1_WT = V_B + 4;               // [225][64]
+constexpr int V1_B = V1_WT + 225 * 64;       // [64]
+constexpr int V2_W = V1_B + 64;              // [64]
+constexpr int V2_B = V2_W + 64;              // [1] (+3 pad)
+constexpr int TOTAL = V2_B + 4;
+
+// algorithmic work of one forward (neural_network.py:132-159), MACs
+constexpr long long MACS = 133690114LL;
+}  // namespace gzpv

@@ -1,0 +1,106 @@
+"""ctypes binding of libgzero.so (include/gzero.h).
+
+The shared library is built in-tree by ``csrc/Makefile`` (``gzero.build()``).
+There is no CPU fallback: if the library or a GPU is missing, every entry point
+raises ``GzeroUnavailable``.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgzero.so")
+
+GZ_OK = 0
+GZ_FLAG_GATHER_LEAVES = 1
+GZ_MAX_SIMULATIONS = 4095
+GZ_MAX_GAME_PLIES = 200
+
+
+class GzeroUnavailable(RuntimeError):
+    pass
+
+
+class GzeroError(RuntimeError):
+    pass
+
+
+class BoardState(ctypes.Structure):  # gz_board_state, 80 bytes
+    _fields_ = [("black", ctypes.c_uint32 * 8), ("white", ctypes.c_uint32 * 8),
+                ("n_moves", ctypes.c_int32), ("player", ctypes.c_int32),
+                ("over", ctypes.c_int32), ("winner", ctypes.c_int32)]
+
+
+class SearchParams(ctypes.Structure):  # gz_search_params
+    _fields_ = [("num_simulations", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("c_puct", ctypes.c_double), ("exploration", ctypes.c_double),
+                ("beta", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("planner_steps", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+class Record(ctypes.Structure):  # gz_record, 80 bytes
+    _fields_ = [("black", ctypes.c_uint32 * 8), ("white", ctypes.c_uint32 * 8),
+                ("game_id", ctypes.c_int64), ("ply", ctypes.c_int16), ("move", ctypes.c_int16),
+                ("player", ctypes.c_int8), ("z", ctypes.c_int8), ("pad", ctypes.c_int8 * 2)]
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("predicts", ctypes.c_int32),
+                ("main_draws", ctypes.c_int32), ("pad", ctypes.c_int32), ("sim_draws", ctypes.c_int64)]
+
+
+class SelfplayCounters(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_int32), ("leaves", ctypes.c_int32),
+                ("records_dropped", ctypes.c_int32), ("leaves_dropped", ctypes.c_int32),
+                ("moves", ctypes.c_int64), ("games", ctypes.c_int64)]
+
+
+assert ctypes.sizeof(BoardState) == 80 and ctypes.sizeof(Record) == 80
+assert ctypes.sizeof(SearchStats) == 24 and ctypes.sizeof(SelfplayCounters) == 32
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/gzero.h
+SIGNATURES = {
+    "gz_last_error": (ctypes.c_char_p, []),
+    "gz_version": (ctypes.c_int, []),
+    "gz_board_step": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P]),
+    "gz_policy_move": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P]),
+    "gz_rollout": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P]),
+    "gz_pattern_score": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P]),
+    "gz_tree_bytes": (_SZ, [_I32]),
+    "gz_search": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(SearchParams), _P, _P, _P, _P, _I32, _P, _P]),
+    "gz_slot_bytes": (_SZ, [_I32]),
+    "gz_selfplay_init": (ctypes.c_int, [_P, _I32, _I32, _I64, _I64, _P]),
+    "gz_selfplay_run": (ctypes.c_int, [_P, _I32, ctypes.POINTER(SearchParams), _I32, _P, _I32, _P, _I32, _P, _P]),
+    "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
+    "gz_pv_weight_floats": (_SZ, []),
+    "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libgzero.so (no GPU needed to load it); raises GzeroUnavailable if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GzeroUnavailable(
+            f"{path} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != GZ_OK:
+        msg = load().gz_last_error()
+        raise GzeroError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,187 @@
+"""Thin torch-owned-memory wrappers around the libgzero C-ABI.
+
+Every buffer is a torch tensor on the current CUDA(HIP) device; raw pointers
+and torch's current stream are handed to the library.  Nothing here runs on the
+CPU as a substitute: without a GPU or the library the calls raise.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .boards import RECORD_DTYPE, STATE_DTYPE
+
+
+def require_gpu():
+    lib = _lib.load()
+    if not torch.cuda.is_available():
+        raise _lib.GzeroUnavailable("no HIP device visible: the gzero engine has no CPU fallback")
+    return lib
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def to_dev(arr):
+    """numpy array (any dtype) -> uint8 device tensor holding the same bytes."""
+    a = np.ascontiguousarray(arr)
+    return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def from_dev(t, dtype, count=None):
+    a = t.cpu().numpy().view(dtype)
+    return a if count is None else a[:count]
+
+
+def search_params(num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2, seed=0, max_depth=100,
+                  planner_steps=0, gather_leaves=False):
+    return _lib.SearchParams(int(num_simulations), int(max_depth), float(c_puct), float(exploration),
+                             float(beta), int(seed) & ((1 << 64) - 1), int(planner_steps),
+                             _lib.GZ_FLAG_GATHER_LEAVES if gather_leaves else 0)
+
+
+# ---------------------------------------------------------------- K1 board step
+def board_step(states, moves):
+    """Batched GomokuBoard.make_move: returns (new states, ok[int32], legal[n,4] uint64)."""
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_moves = torch.as_tensor(np.asarray(moves, np.int32)).cuda()
+    d_ok = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_legal = torch.zeros(n * 4, dtype=torch.int64, device="cuda")
+    _lib.check(lib.gz_board_step(ptr(d_states), ptr(d_moves), n, ptr(d_ok), ptr(d_legal), stream()), "gz_board_step")
+    torch.cuda.synchronize()
+    return (from_dev(d_states, STATE_DTYPE), d_ok.cpu().numpy(),
+            d_legal.cpu().numpy().view(np.uint64).reshape(n, 4))
+
+
+# ---------------------------------------------------------------- rollout policy
+def policy_move(states, keys):
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_keys = torch.as_tensor(np.asarray(keys, np.uint64).view(np.int64)).cuda()
+    d_moves = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_draws = torch.zeros(n, dtype=torch.int32, device="cuda")
+    _lib.check(lib.gz_policy_move(ptr(d_states), ptr(d_keys), n, ptr(d_moves), ptr(d_draws), stream()),
+               "gz_policy_move")
+    torch.cuda.synchronize()
+    return d_moves.cpu().numpy(), d_draws.cpu().numpy()
+
+
+def rollout(states, ai, keys, max_depth=100):
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_ai = torch.as_tensor(np.asarray(ai, np.int32)).cuda()
+    d_keys = torch.as_tensor(np.asarray(keys, np.uint64).view(np.int64)).cuda()
+    d_vals = torch.zeros(n, dtype=torch.float64, device="cuda")
+    d_fin = torch.zeros(n * STATE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    d_draws = torch.zeros(n, dtype=torch.int32, device="cuda")
+    _lib.check(lib.gz_rollout(ptr(d_states), ptr(d_ai), ptr(d_keys), n, int(max_depth), ptr(d_vals), ptr(d_fin),
+                              ptr(d_draws), stream()), "gz_rollout")
+    torch.cuda.synchronize()
+    return d_vals.cpu().numpy(), from_dev(d_fin, STATE_DTYPE), d_draws.cpu().numpy()
+
+
+def pattern_score(states, players):
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_pl = torch.as_tensor(np.asarray(players, np.int32)).cuda()
+    d_s = torch.zeros(n, dtype=torch.int64, device="cuda")
+    d_bg = torch.zeros(n, dtype=torch.float64, device="cuda")
+    _lib.check(lib.gz_pattern_score(ptr(d_states), ptr(d_pl), n, ptr(d_s), ptr(d_bg), stream()), "gz_pattern_score")
+    torch.cuda.synchronize()
+    return d_s.cpu().numpy(), d_bg.cpu().numpy()
+
+
+# ---------------------------------------------------------------- MCTS get_move
+def parse_tree(raw, num_simulations, n_nodes):
+    """One exported search tree (LDS layout of gz_selfplay.hip) -> dict of arrays."""
+    mn = num_simulations + 1
+    b = np.asarray(raw, np.uint8)
+    return {
+        "value": b[0:8 * mn].view(np.float64)[:n_nodes],
+        "bg": b[8 * mn:16 * mn].view(np.float64)[:n_nodes],
+        "visits": b[16 * mn:20 * mn].view(np.int32)[:n_nodes],
+        "parent": b[20 * mn:22 * mn].view(np.int16)[:n_nodes],
+        "bound": b[22 * mn:24 * mn].view(np.int16)[:n_nodes],
+        "move": b[24 * mn:25 * mn][:n_nodes],
+        "term": b[25 * mn:26 * mn][:n_nodes],
+    }
+
+
+def search(states, game_ids, params, want_trees=False, leaf_cap=0):
+    """One AlphaZeroGomokuAI.get_move per state.  Returns (moves, stats, trees, leaves)."""
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_gids = torch.as_tensor(np.asarray(game_ids, np.int64)).cuda()
+    d_moves = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_stats = torch.zeros(n * ctypes.sizeof(_lib.SearchStats), dtype=torch.uint8, device="cuda")
+    tb = lib.gz_tree_bytes(params.num_simulations)
+    d_trees = torch.zeros(n * tb, dtype=torch.uint8, device="cuda") if want_trees else None
+    gather = (params.flags & _lib.GZ_FLAG_GATHER_LEAVES) != 0
+    d_leaves = torch.zeros(max(1, leaf_cap) * 16, dtype=torch.int32, device="cuda") if gather else None
+    d_lc = torch.zeros(1, dtype=torch.int32, device="cuda") if gather else None
+    _lib.check(lib.gz_search(ptr(d_states), ptr(d_gids), n, ctypes.byref(params), ptr(d_trees), ptr(d_moves),
+                             ptr(d_stats), ptr(d_leaves), int(leaf_cap), ptr(d_lc), stream()), "gz_search")
+    torch.cuda.synchronize()
+    st = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=np.dtype(
+        [("n_nodes", "<i4"), ("predicts", "<i4"), ("main_draws", "<i4"), ("pad", "<i4"), ("sim_draws", "<i8")]))
+    trees = None
+    if want_trees:
+        raw = d_trees.cpu().numpy().reshape(n, tb)
+        trees = [parse_tree(raw[i], params.num_simulations, int(st["n_nodes"][i])) for i in range(n)]
+    leaves = None
+    if gather:
+        cnt = int(d_lc.item())
+        leaves = d_leaves.cpu().numpy().view(np.uint32).reshape(-1, 16)[:min(cnt, leaf_cap)]
+    return d_moves.cpu().numpy(), st, trees, leaves
+
+
+# ---------------------------------------------------------------- PV forward
+class PVWeights:
+    """Packed weight blob resident on the device."""
+
+    def __init__(self, blob):
+        lib = require_gpu()
+        blob = np.ascontiguousarray(blob, np.float32)
+        if blob.size != lib.gz_pv_weight_floats():
+            raise ValueError(f"weight blob has {blob.size} floats, kernel expects {lib.gz_pv_weight_floats()}")
+        self.tensor = torch.from_numpy(blob).cuda()
+
+
+def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=None, d_probs=None):
+    """Device-resident forward: d_boards int32/uint32 tensor [n,16]; returns output tensors."""
+    lib = require_gpu()
+    if d_logits is None:
+        d_logits = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    if d_value is None:
+        d_value = torch.empty(n, dtype=torch.float32, device="cuda")
+    _lib.check(lib.gz_pv_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_logits),
+                                 ptr(d_value), ptr(d_probs), stream()), "gz_pv_forward")
+    return d_logits, d_value, d_probs
+
+
+def pv_forward(weights, leaf_rows):
+    """Host convenience: [n,16] uint32 leaf rows -> (logits [n,225], value [n], probs [n,225])."""
+    rows = np.ascontiguousarray(leaf_rows, np.uint32).reshape(-1, 16)
+    n = rows.shape[0]
+    d_b = torch.from_numpy(rows.view(np.int32).copy()).cuda()
+    d_probs = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    lg, v, pr = pv_forward_dev(weights, d_b, n, d_probs=d_probs)
+    torch.cuda.synchronize()
+    return lg.cpu().numpy().reshape(n, 225), v.cpu().numpy(), pr.cpu().numpy().reshape(n, 225)

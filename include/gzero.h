@@ -1,0 +1,148 @@
+/*
+ * gzero.h -- C-ABI of libgzero.so, the MI355X (gfx950) self-play engine that
+ * replaces the hot path of gitMasterLiujiahui/AlphaZero-Gomoku.
+ *
+ * The reference is pure Python with no FFI, so every entry point below
+ * replaces a Python call site; the binding a maintainer would add (ctypes,
+ * the same shape as cgo/JNI) is in INTEGRATION.md and in
+ * alphazero-gomoku_amd/gzero/_lib.py.
+ *
+ * Conventions
+ *  - All pointers named d_* are DEVICE pointers owned by the caller (torch
+ *    tensors in the Python host).  `stream` is a hipStream_t passed as void*.
+ *    Calls are stream-ordered and asynchronous; none allocates or synchronises.
+ *  - Return value: GZ_OK (0) or a negative GZ_ERR_*; gz_last_error() holds a
+ *    thread-local message.  Misuse (bad sizes) is rejected before any launch.
+ *  - Boards are bit planes: row r in word r>>1, bits (r&1)*16 + c (c < 15);
+ *    bit 15 of each row and row 15 are zero.  Cells are row-major r*15+c.
+ */
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GZ_OK 0
+#define GZ_ERR_ARG -1
+#define GZ_ERR_HIP -2
+#define GZ_ERR_UNSUPPORTED -3
+
+#define GZ_MAX_SIMULATIONS 4095
+#define GZ_MAX_GAME_PLIES 200
+
+/* GomokuBoard state (gomoku_board.py:40-53): stones, len(move_history),
+ * current_player (1/2), game_over, winner (0 = None). 80 bytes. */
+typedef struct gz_board_state {
+    uint32_t black[8];
+    uint32_t white[8];
+    int32_t n_moves;
+    int32_t player;
+    int32_t over;
+    int32_t winner;
+} gz_board_state;
+
+/* AlphaZeroGomokuAI search knobs (ai_agent.py:29-31,65-90); difficulty maps
+ * to num_simulations / c_puct / exploration exactly as the reference's table. */
+typedef struct gz_search_params {
+    int32_t num_simulations; /* params["num_simulations"] */
+    int32_t max_depth;       /* rollout cap, _simulate max_depth (100) */
+    double c_puct;           /* params["c_puct"] */
+    double exploration;      /* params["exploration"] */
+    double beta;             /* constructor beta: weight of tanh(pattern/1e4) in UCB */
+    uint64_t seed;           /* RNG streams (gzero/rng.py) */
+    int32_t planner_steps;   /* BG-planner plies per rollout: only 0 is implemented */
+    int32_t flags;           /* GZ_FLAG_* */
+} gz_search_params;
+
+#define GZ_FLAG_GATHER_LEAVES 1 /* append every non-terminal node's board for the PV forward */
+
+/* One (s, pi, z) training tuple (training.py:77-97,203-210). 80 bytes. */
+typedef struct gz_record {
+    uint32_t black[8]; /* planes before the move (absolute colours) */
+    uint32_t white[8];
+    int64_t game_id;
+    int16_t ply;    /* move number within the game */
+    int16_t move;   /* r*15+c */
+    int8_t player;  /* mover, 1/2 */
+    int8_t z;       /* +1 mover won, -1 lost, 0 draw */
+    int8_t pad[2];
+} gz_record;
+
+typedef struct gz_search_stats {
+    int32_t n_nodes;
+    int32_t predicts;   /* GomokuModel.predict calls the reference makes for this move */
+    int32_t main_draws; /* draws on the (game, ply, 0) stream */
+    int32_t pad;
+    int64_t sim_draws;  /* draws summed over simulation streams */
+} gz_search_stats;
+
+typedef struct gz_selfplay_counters {
+    int32_t records;         /* records written to d_records */
+    int32_t leaves;          /* boards appended to d_leaves */
+    int32_t records_dropped; /* records lost because d_records was full */
+    int32_t leaves_dropped;
+    int64_t moves;           /* plies played */
+    int64_t games;           /* games finished */
+} gz_selfplay_counters;
+
+const char* gz_last_error(void);
+int gz_version(void);
+
+/* ---- K1: board step / legal mask / five-in-a-row (gomoku_board.py:84-213) ----
+ * d_boards[i] <- make_move(d_moves[i]) (cell r*15+c, or any value outside
+ * [0,225) which fails like an off-board move).  d_ok[i] = make_move's return.
+ * d_legal (optional) = [n][4] uint64 row-major masks of empty cells after the
+ * step (get_valid_moves, which ignores game_over). */
+int gz_board_step(gz_board_state* d_boards, const int32_t* d_moves, int32_t n, int32_t* d_ok,
+                  uint64_t* d_legal, void* stream);
+
+/* ---- rollout policy and rollouts (ai_agent.py:251-430) ----
+ * Component entry points used by the parity tests. keys = RNG stream keys. */
+int gz_policy_move(const gz_board_state* d_boards, const uint64_t* d_keys, int32_t n, int32_t* d_moves,
+                   uint32_t* d_draws, void* stream);
+int gz_rollout(const gz_board_state* d_boards, const int32_t* d_ai, const uint64_t* d_keys, int32_t n,
+               int32_t max_depth, double* d_values, gz_board_state* d_final, uint32_t* d_draws,
+               void* stream);
+
+/* ---- pattern score / _bg_score (bg_planner.py:133-196, ai_agent.py:432-439) ---- */
+int gz_pattern_score(const gz_board_state* d_boards, const int32_t* d_player, int32_t n, int64_t* d_score,
+                     double* d_bg, void* stream);
+
+/* ---- K2+K3: one AlphaZeroGomokuAI.get_move per board (ai_agent.py:109-222) ----
+ * One wavefront per board.  d_trees: n * gz_tree_bytes(num_simulations)
+ * scratch holding each search tree (layout in DESIGN.md; readable by tests).
+ * d_moves[i] = chosen cell or -1 (None).  Leaves are appended to d_leaves
+ * ([leaf_cap][16] uint32: black[8], white[8]) when GZ_FLAG_GATHER_LEAVES. */
+size_t gz_tree_bytes(int32_t num_simulations);
+int gz_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
+              const gz_search_params* p, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
+              uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, void* stream);
+
+/* ---- self-play collector (training.py:141-218) over n_slots concurrent games ----
+ * Slot s plays games game_id_base + s + g*game_id_stride, g = 0,1,2,...  Each
+ * call advances every slot by n_plies plies; a finished game's tuples (with z)
+ * are appended to d_records and the slot restarts from the empty board. */
+size_t gz_slot_bytes(int32_t num_simulations);
+int gz_selfplay_init(void* d_slots, int32_t n_slots, int32_t num_simulations, int64_t game_id_base,
+                     int64_t game_id_stride, void* stream);
+int gz_selfplay_run(void* d_slots, int32_t n_slots, const gz_search_params* p, int32_t n_plies,
+                    gz_record* d_records, int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap,
+                    gz_selfplay_counters* d_counters, void* stream);
+/* current board of every slot (for inspection / tests) */
+int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations,
+                       gz_board_state* d_out, int64_t* d_game_ids, void* stream);
+
+/* ---- K6: AlphaZeroGomokuNet forward (neural_network.py:94-159,214-252) ----
+ * fp32 MFMA.  d_weights: packed blob of gz_pv_weight_floats() floats (layout in
+ * gzero/weights.py).  Boards [n][16] uint32 bit planes.  If d_count is not
+ * NULL it holds the number of valid boards on the device (n = capacity).
+ * Outputs: logits [n][225], value [n] (tanh), probs [n][225] (softmax) or NULL. */
+size_t gz_pv_weight_floats(void);
+int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
+                  float* d_logits, float* d_value, float* d_probs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif

@@ -169,6 +169,47 @@ def gen_moves(rng, length, avoid_five=True, near=False):
     raise RuntimeError("could not generate position")
 
 
+def gen_quiet(rng, length):
+    """A move sequence after which neither side can complete five in one move
+    (so rollouts and the UCB phase run for many plies)."""
+    for _ in range(200):
+        cells = [0] * (N * N)
+        wins = {1: set(), 2: set()}
+        moves = []
+        p = 1
+        ok = True
+        for _ply in range(length):
+            empty = [i for i in range(N * N) if cells[i] == 0]
+            rng.shuffle(empty)
+            placed = False
+            for mv in empty[:40]:
+                if mv in wins[p] or mv in wins[3 - p]:
+                    continue
+                cells[mv] = p
+                new = set()
+                r0, c0 = divmod(mv, N)
+                for dr, dc in ((0, 1), (1, 0), (1, 1), (1, -1)):
+                    for k in range(-4, 5):
+                        rr, cc = r0 + k * dr, c0 + k * dc
+                        if 0 <= rr < N and 0 <= cc < N and cells[rr * N + cc] == 0 and _wins(cells, rr, cc, p):
+                            new.add(rr * N + cc)
+                if new:
+                    cells[mv] = 0
+                    continue
+                wins[1].discard(mv)
+                wins[2].discard(mv)
+                moves.append(mv)
+                placed = True
+                break
+            if not placed:
+                ok = False
+                break
+            p = 3 - p
+        if ok:
+            return moves
+    raise RuntimeError("could not generate a quiet position")
+
+
 def replay(h, moves):
     b = h.gb.GomokuBoard()
     for m in moves:
@@ -509,6 +550,58 @@ def part_mcts():
     dump("mcts", {"seed": SEED, "cases": out})
 
 
+def part_mcts2():
+    """Quiet positions: long rollouts and a real UCB phase (sims > legal + 1)."""
+    import random as pyrandom
+    rng = pyrandom.Random(13)
+    tasks = []
+    i = 300
+    for k in range(40):
+        L = [24, 40, 60, 80, 100, 120, 140, 160][k % 8] + rng.randint(0, 6)
+        legal = 225 - L
+        extra = rng.randint(5, 40) if L >= 80 else rng.randint(3, 12)
+        tasks.append((i, gen_quiet(rng, L), legal + 1 + extra, [0.0, 0.2][k % 2],
+                      ["medium", "easy", "hard"][k % 3]))
+        i += 1
+    tasks.sort(key=lambda t: -(225 - len(t[1])) * t[2])
+    with Pool(8) as pool:
+        out = pool.map(_mcts_task, tasks, chunksize=1)
+    out.sort(key=lambda r: r["game_id"])
+    dump("mcts2", {"seed": SEED, "cases": out})
+
+
+def part_pvnet():
+    """G4: reference GomokuModel on deterministic weights (gzero.weights.init_state_dict)."""
+    import base64
+    import random as pyrandom
+    import numpy as np
+    import torch
+    from gzero import weights
+    h = ref()
+    sd = weights.init_state_dict(seed=7)
+    path = os.path.join(os.getcwd(), "pv_golden.pth")
+    torch.save({"model_state_dict": sd, "model_type": "alphazero_gomoku", "board_size": 15, "device": "cpu"}, path)
+    model = h.nn.GomokuModel(model_path=path, board_size=15, device="cpu")
+    rng = pyrandom.Random(17)
+    cases = []
+    logits_all, value_all, probs_all = [], [], []
+    for i in range(96):
+        L = rng.randint(0, 150)
+        mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.5) if L else []
+        b = replay(h, mv)
+        probs, value = model.predict(b.get_board_state())
+        x = torch.from_numpy(b.get_board_tensor()).unsqueeze(0)
+        with torch.no_grad():
+            lg, v = model.model(x)
+        cases.append({"moves": mv})
+        logits_all.append(lg.numpy().reshape(-1))
+        value_all.append(float(value))
+        probs_all.append(np.asarray(probs, np.float32))
+    enc = lambda a: base64.b64encode(np.ascontiguousarray(a, np.float32).tobytes()).decode()
+    dump("pvnet", {"weights_seed": 7, "cases": cases, "logits_f32_b64": enc(np.stack(logits_all)),
+                   "value_f32_b64": enc(np.asarray(value_all)), "probs_f32_b64": enc(np.stack(probs_all))})
+
+
 # ---------------------------------------------------------------------------
 # G7 full self-play games (training.play_one_game)
 # ---------------------------------------------------------------------------
@@ -545,7 +638,8 @@ def part_games():
 
 
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
-         "rollout": part_rollout, "mcts": part_mcts, "games": part_games}
+         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet,
+         "games": part_games}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(PARTS)
