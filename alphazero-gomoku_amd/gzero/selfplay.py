@@ -1,0 +1,120 @@
+"""Device-resident self-play collector: the batched form of
+``training.play_one_game`` (training.py:141-218) over thousands of concurrent games.
+
+One call of :meth:`SelfPlayEngine.step` advances every game slot by ``n_plies``
+plies inside one kernel launch (one wavefront per game), then -- in
+reference-work mode -- evaluates the policy-value network on every node the
+searches created, exactly the ``GomokuModel.predict`` calls the reference makes
+(``ai_agent.py:522-523``).  The forward's outputs are produced but, as in the
+reference, never read by the search.  Finished games are appended as
+(planes, move, player, z) records; slots restart with the next game id.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .boards import RECORD_DTYPE, STATE_DTYPE, words_to_cells
+from .device import PVWeights, ptr, require_gpu, search_params, stream
+
+COUNTER_DTYPE = np.dtype([("records", "<i4"), ("leaves", "<i4"), ("records_dropped", "<i4"),
+                          ("leaves_dropped", "<i4"), ("moves", "<i8"), ("games", "<i8")])
+
+
+class SelfPlayEngine:
+    def __init__(self, n_slots=4096, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2,
+                 seed=0, max_depth=100, pv_weights=None, plies_per_step=1, game_id_base=0,
+                 game_id_stride=None, planner_steps=0):
+        self.lib = require_gpu()
+        if planner_steps:
+            raise _lib.GzeroError("planner_steps > 0 (BG-planner rollouts) is not implemented on the device yet")
+        self.n_slots = int(n_slots)
+        self.plies_per_step = int(plies_per_step)
+        self.gather = pv_weights is not None
+        self.params = search_params(num_simulations, c_puct, exploration, beta, seed, max_depth, 0, self.gather)
+        self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
+            else PVWeights(pv_weights)
+        S = self.params.num_simulations
+        slot_bytes = self.lib.gz_slot_bytes(S)
+        self.d_slots = torch.zeros(self.n_slots * slot_bytes, dtype=torch.uint8, device="cuda")
+        # a slot can finish one 200-ply game plus any games played inside a step
+        self.record_cap = self.n_slots * (_lib.GZ_MAX_GAME_PLIES + self.plies_per_step)
+        self.d_records = torch.zeros(self.record_cap * RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        self.d_counters = torch.zeros(COUNTER_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        self.leaf_cap = self.n_slots * self.plies_per_step * (S + 1) if self.gather else 0
+        if self.gather:
+            self.d_leaves = torch.zeros(self.leaf_cap * 16, dtype=torch.int32, device="cuda")
+            self.d_logits = torch.empty(self.leaf_cap * 225, dtype=torch.float32, device="cuda")
+            self.d_value = torch.empty(self.leaf_cap, dtype=torch.float32, device="cuda")
+            self.d_probs = torch.empty(self.leaf_cap * 225, dtype=torch.float32, device="cuda")
+        else:
+            self.d_leaves = self.d_logits = self.d_value = self.d_probs = None
+        base = int(game_id_base)
+        stride = self.n_slots if game_id_stride is None else int(game_id_stride)
+        _lib.check(self.lib.gz_selfplay_init(ptr(self.d_slots), self.n_slots, S, base, stride, stream()),
+                   "gz_selfplay_init")
+
+    # ---- launches (asynchronous, current torch stream)
+    def launch_search(self, n_plies=None):
+        n = self.plies_per_step if n_plies is None else int(n_plies)
+        if n > self.plies_per_step and self.gather:
+            raise ValueError("n_plies exceeds the leaf buffer sized for plies_per_step")
+        self.d_counters.zero_()
+        _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
+                                            ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
+                                            self.leaf_cap, ptr(self.d_counters), stream()), "gz_selfplay_run")
+
+    def launch_pv(self):
+        if not self.gather:
+            return
+        d_count = self.d_counters[4:8]  # counters.leaves
+        _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
+                                          ptr(d_count), ptr(self.d_logits), ptr(self.d_value),
+                                          ptr(self.d_probs), stream()), "gz_pv_forward")
+
+    def step(self, n_plies=None):
+        self.launch_search(n_plies)
+        self.launch_pv()
+
+    # ---- host views (synchronising)
+    def counters(self):
+        return np.frombuffer(self.d_counters.cpu().numpy().tobytes(), COUNTER_DTYPE)[0]
+
+    def records(self):
+        """Records of the games that finished during the last step."""
+        c = self.counters()
+        n = min(int(c["records"]), self.record_cap)
+        raw = self.d_records[: n * RECORD_DTYPE.itemsize].cpu().numpy()
+        return np.frombuffer(raw.tobytes(), RECORD_DTYPE)
+
+    def records_device(self):
+        """(device uint8 tensor of records, count) without copying to the host."""
+        n = min(int(self.counters()["records"]), self.record_cap)
+        return self.d_records[: n * RECORD_DTYPE.itemsize], n
+
+    def boards(self):
+        out = torch.zeros(self.n_slots * STATE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        gids = torch.zeros(self.n_slots, dtype=torch.int64, device="cuda")
+        _lib.check(self.lib.gz_selfplay_boards(ptr(self.d_slots), self.n_slots, self.params.num_simulations,
+                                               ptr(out), ptr(gids), stream()), "gz_selfplay_boards")
+        return np.frombuffer(out.cpu().numpy().tobytes(), STATE_DTYPE), gids.cpu().numpy()
+
+
+def records_to_games(recs):
+    """Group records by game id -> {game_id: dict(moves, players, z, cells)} (ply order)."""
+    out = {}
+    for gid in np.unique(recs["game_id"]):
+        r = recs[recs["game_id"] == gid]
+        r = r[np.argsort(r["ply"])]
+        out[int(gid)] = {"moves": [int(x) for x in r["move"]], "players": [int(x) for x in r["player"]],
+                         "z": [int(x) for x in r["z"]], "cells": words_to_cells(r["black"], r["white"])}
+    return out
+
+
+def records_to_replay(recs):
+    """SimpleReplay fields (training.py:77-97): states float32 [n,3,15,15], move
+    indices, players, outcomes."""
+    cells = words_to_cells(recs["black"], recs["white"]).reshape(-1, 15, 15)
+    planes = np.stack([(cells == 1), (cells == 2), (cells == 0)], axis=1).astype(np.float32)
+    return planes, recs["move"].astype(np.int64), recs["player"].astype(np.int64), recs["z"].astype(np.int64)

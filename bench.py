@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""bench.py -- self-play moves/sec at 200 sims/move on a 15x15 board (BASELINE.json).
+
+Workload (BASELINE config 2, per GPU): 4096 concurrent self-play games from the
+empty board, 200 simulations per move, medium difficulty (c_puct 1.6,
+exploration 0.05), beta = 0, planner_steps = 0, random-init network weights
+(numpy default_rng(0)), continuous refill of finished games.
+
+One "step" = every game slot plays `--plies-per-step` plies (one kernel launch,
+one wavefront per game) followed by the policy-value forward of EVERY node
+those searches created -- the GomokuModel.predict calls the reference makes
+(ai_agent.py:522-523) -- on the fp32 MFMA kernel, and (N > 1) the RCCL
+all-gather of the finished games' (s, pi, z) records.  `value` counts every
+ply played by every rank.
+
+Also reported: the roofline of the dominant kernel (the PV forward), the
+prior-elided MCTS-only rate (the search never reads the priors, so moves are
+identical without them), and the C oracle ("port") timed on the host cores.
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torchrun.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "alphazero-gomoku_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from gzero import dist as gdist  # noqa: E402
+from gzero import weights  # noqa: E402
+from gzero.device import PVWeights  # noqa: E402
+from gzero.selfplay import COUNTER_DTYPE, SelfPlayEngine  # noqa: E402
+
+METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_traffic():
+    p = os.path.join(REPO, "profiles", "pv_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("bytes_per_launch"), d
+    return None, None
+
+
+def cpu_baseline(positions, sims, seed, budget_s, torch_threads):
+    """C oracle (single thread) searching the same positions the GPU starts its
+    timed window from, plus torch-CPU fp32 forwards for the nodes it created."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    O.build()
+    from gzero.boards import words_to_cells
+    t_search = 0.0
+    plies = 0
+    predicts = 0
+    t_start = time.perf_counter()
+    for (black, white, n_moves, player, gid) in positions:
+        cells = words_to_cells(black, white)
+        b = O.Board()
+        O.lib().or_board_init(b)
+        for i in range(225):
+            b.cell[i] = int(cells[i])
+        b.n_moves, b.player = int(n_moves), int(player)
+        p = O.make_params("medium", sims=sims, beta=0.0, seed=seed)
+        while not b.over and time.perf_counter() - t_start < budget_s:
+            t0 = time.perf_counter()
+            mv, tree = O.get_move(b, b.player, p, gid, cap=8)
+            t_search += time.perf_counter() - t0
+            predicts += tree["predicts"]
+            plies += 1
+            O.lib().or_make_move(b, mv // 15, mv % 15)
+            if plies >= 8:
+                break
+        if time.perf_counter() - t_start >= budget_s:
+            break
+    # PV forwards on the host cores, timed on a bounded number of boards and scaled
+    torch.set_num_threads(torch_threads)
+    net = weights.PolicyValueNet()
+    net.load_state_dict(weights.init_state_dict(0))
+    net.eval()
+    n_eval = max(1, min(predicts, 1024))
+    x = torch.from_numpy(np.random.default_rng(0).integers(0, 2, (n_eval, 3, 15, 15)).astype(np.float32))
+    with torch.no_grad():
+        net(x[:8])
+        t0 = time.perf_counter()
+        for i in range(0, n_eval, 256):
+            net(x[i:i + 256])
+        t_pv = (time.perf_counter() - t0) * predicts / n_eval
+    total = t_search + t_pv
+    return {
+        "value": plies / total if total > 0 else None,
+        "unit": "moves/s",
+        "cores": int(torch_threads),
+        "kind": "port",
+        "sample": (f"{plies} MCTS plies at {sims} sims from the GPU run's timed-window start positions: "
+                   f"C oracle search {t_search:.2f}s on 1 thread + {predicts} policy-value forwards "
+                   f"(torch fp32 CPU, batch 256, {torch_threads} threads; {n_eval} timed, scaled) {t_pv:.2f}s"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--slots", type=int, default=4096, help="concurrent games per GPU")
+    ap.add_argument("--sims", type=int, default=200)
+    ap.add_argument("--beta", type=float, default=0.0)
+    ap.add_argument("--plies-per-step", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
+    ap.add_argument("--elided-plies", type=int, default=20)
+    ap.add_argument("--no-elided", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, ws = gdist.init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws != args.gpus and rank == 0:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")
+
+    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)))
+    base, stride = gdist.shard_ids(rank, ws, args.slots)
+    P = args.plies_per_step
+    eng = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
+                         beta=args.beta, seed=args.seed, pv_weights=w, plies_per_step=P,
+                         game_id_base=base, game_id_stride=stride)
+
+    def barrier():
+        if ws > 1:
+            dist.barrier()
+
+    gathered = [0]
+
+    def step():
+        eng.launch_search()
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        eng.launch_pv()
+        ev[1].record()
+        ctr = eng.d_counters.clone()  # per-step counters, stays on the device
+        if ws > 1:  # RCCL all-gather of the (s, pi, z) records finished in this step
+            rec, n = eng.records_device()
+            out = gdist.all_gather_records(rec, n)
+            gathered[0] += out.numel()
+        return ev, ctr
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    boards0, gids0 = eng.boards()  # timed-window start positions (for the CPU baseline)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    recs = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c in recs]
+    moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs))], dtype=torch.float64, device="cuda")
+    if ws > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(moves, op=dist.ReduceOp.SUM)
+    T = float(elapsed.item())
+    total_moves = float(moves.item())
+    value = total_moves / T
+    pv_ms = [a.elapsed_time(b) for (a, b), _ in recs]
+    leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
+    dropped = sum(int(c["leaves_dropped"]) + max(0, int(c["leaves"]) - eng.leaf_cap) for c in ctrs)
+    mean_leaves = float(np.mean(leaves))
+    mean_pv_s = float(np.mean(pv_ms)) / 1e3
+    achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
+    traffic, _ = load_traffic()
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "moves/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(T / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: self-play from the empty board with random-init weights (numpy default_rng(0))",
+            "config": {
+                "workload": (f"BASELINE config 2: {args.slots} concurrent self-play games per GPU, 15x15, "
+                             f"{args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), beta={args.beta}, "
+                             "planner_steps=0, continuous refill; policy-value forward (fp32 MFMA) on every "
+                             "non-terminal node the searches create (reference-work mode)"),
+                "games_per_gpu": args.slots,
+                "global_games": args.slots * ws,
+                "sims_per_move": args.sims,
+                "plies_per_step": P,
+                "parallelism": f"dp{ws} (games sharded by id, all-gather of records)",
+                "pv_boards_per_step": round(mean_leaves, 1),
+                "pv_boards_dropped": dropped,
+            },
+            "roofline": {
+                "kernel": "pv_kernel (AlphaZeroGomokuNet forward, fp32 MFMA)",
+                "bound": "mfma",
+                "achieved": round(achieved, 3),
+                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "per_launch": {"boards": round(mean_leaves, 1), "flop_per_board": PV_FLOP,
+                               "avg_ms": round(float(np.mean(pv_ms)), 3)},
+            },
+        }
+
+    # ---- prior-elided run (same kernel, no PV gather / forward)
+    if not args.no_elided:
+        el = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
+                            beta=args.beta, seed=args.seed, pv_weights=None, plies_per_step=10,
+                            game_id_base=base, game_id_stride=stride)
+        done = 0
+        while done < args.elided_warmup:
+            n = min(10, args.elided_warmup - done)
+            el.launch_search(n)
+            done += n
+        torch.cuda.synchronize()
+        barrier()
+        e0 = time.perf_counter()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        mv_el = 0
+        done = 0
+        while done < args.elided_plies:
+            n = min(10, args.elided_plies - done)
+            el.launch_search(n)
+            mv_el += int(el.counters()["moves"])
+            done += n
+        ev1.record()
+        torch.cuda.synchronize()
+        barrier()
+        e1 = torch.tensor([time.perf_counter() - e0], dtype=torch.float64, device="cuda")
+        mv_t = torch.tensor([float(mv_el)], dtype=torch.float64, device="cuda")
+        if ws > 1:
+            dist.all_reduce(e1, op=dist.ReduceOp.MAX)
+            dist.all_reduce(mv_t, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            out["prior_elided"] = {
+                "value": round(float(mv_t.item()) / float(e1.item()), 3),
+                "unit": "moves/s",
+                "window": f"plies {args.elided_warmup}..{args.elided_warmup + args.elided_plies} of every slot",
+                "kernel_ms": round(ev0.elapsed_time(ev1), 3),
+                "note": "identical moves and tuples; the reference never reads the priors (ai_agent.py:523)",
+            }
+
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        pos = [(boards0["black"][i], boards0["white"][i], boards0["n_moves"][i], boards0["player"][i], int(gids0[i]))
+               for i in range(min(8, len(boards0)))]
+        threads = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(pos, args.sims, args.seed, args.cpu_seconds, threads)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

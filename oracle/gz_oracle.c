@@ -462,7 +462,7 @@ int or_get_move(const or_board* b, int ai, const or_params* p, int64_t game_id, 
 /* training.play_one_game (no timeouts) + SimpleReplay, training.py:77-97,141-218 */
 int or_play_game(const or_params* black, const or_params* white, int64_t game_id, int8_t* cells_out,
                  int32_t* moves_out, int8_t* players_out, int8_t* z_out, int cap, int* winner,
-                 int64_t* predicts) {
+                 int64_t* predicts, int max_plies) {
     or_board b;
     or_board_init(&b);
     int n = 0;
@@ -470,7 +470,7 @@ int or_play_game(const or_params* black, const or_params* white, int64_t game_id
     int32_t parent[1], move[1], visits[1];
     double value[1];
     or_tree_info info = {0, 0, 0, 0, parent, move, visits, value, 0};
-    while (!b.over) {
+    while (!b.over && (max_plies <= 0 || n < max_plies)) {
         int pl = b.player;
         const or_params* p = (pl == 1) ? black : white;
         int mv = or_get_move(&b, pl, p, game_id, &info);

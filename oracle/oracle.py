@@ -86,7 +86,7 @@ def lib():
         L.or_play_game.restype = ctypes.c_int
         L.or_play_game.argtypes = [P(Params), P(Params), ctypes.c_int64, P(ctypes.c_int8),
                                    P(ctypes.c_int32), P(ctypes.c_int8), P(ctypes.c_int8), ctypes.c_int,
-                                   P(ctypes.c_int), P(ctypes.c_int64)]
+                                   P(ctypes.c_int), P(ctypes.c_int64), ctypes.c_int]
         _lib = L
     return _lib
 
@@ -139,7 +139,7 @@ def get_move(b, ai_player, params, game_id, cap=4096):
     return m, tree
 
 
-def play_game(black, white, game_id, cap=256, want_cells=False):
+def play_game(black, white, game_id, cap=256, want_cells=False, max_plies=0):
     cells = (ctypes.c_int8 * (cap * CELLS))() if want_cells else None
     moves = (ctypes.c_int32 * cap)()
     players = (ctypes.c_int8 * cap)()
@@ -147,7 +147,7 @@ def play_game(black, white, game_id, cap=256, want_cells=False):
     winner = ctypes.c_int(0)
     pred = ctypes.c_int64(0)
     n = lib().or_play_game(ctypes.byref(black), ctypes.byref(white), game_id, cells, moves, players, z,
-                           cap, ctypes.byref(winner), ctypes.byref(pred))
+                           cap, ctypes.byref(winner), ctypes.byref(pred), int(max_plies))
     out = {"n": n, "moves": list(moves[:n]), "players": list(players[:n]), "z": list(z[:n]),
            "winner": winner.value, "predicts": pred.value}
     if want_cells:
