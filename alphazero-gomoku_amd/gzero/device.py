@@ -154,7 +154,7 @@ def search(states, game_ids, params, want_trees=False, leaf_cap=0):
 
 # ---------------------------------------------------------------- PV forward
 class PVWeights:
-    """Packed weight blob resident on the device."""
+    """Packed weight blob resident on the device (+ the kernel's scratch slab)."""
 
     def __init__(self, blob):
         lib = require_gpu()
@@ -162,6 +162,8 @@ class PVWeights:
         if blob.size != lib.gz_pv_weight_floats():
             raise ValueError(f"weight blob has {blob.size} floats, kernel expects {lib.gz_pv_weight_floats()}")
         self.tensor = torch.from_numpy(blob).cuda()
+        ws = lib.gz_pv_workspace_bytes(1 << 30)
+        self.workspace = torch.empty(ws, dtype=torch.uint8, device="cuda")
 
 
 def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=None, d_probs=None):
@@ -172,7 +174,7 @@ def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=No
     if d_value is None:
         d_value = torch.empty(n, dtype=torch.float32, device="cuda")
     _lib.check(lib.gz_pv_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_logits),
-                                 ptr(d_value), ptr(d_probs), stream()), "gz_pv_forward")
+                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace), stream()), "gz_pv_forward")
     return d_logits, d_value, d_probs
 
 

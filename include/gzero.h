@@ -138,10 +138,12 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
  * fp32 MFMA.  d_weights: packed blob of gz_pv_weight_floats() floats (layout in
  * gzero/weights.py).  Boards [n][16] uint32 bit planes.  If d_count is not
  * NULL it holds the number of valid boards on the device (n = capacity).
- * Outputs: logits [n][225], value [n] (tanh), probs [n][225] (softmax) or NULL. */
+ * Outputs: logits [n][225], value [n] (tanh), probs [n][225] (softmax) or NULL.
+ * d_workspace: gz_pv_workspace_bytes(n) bytes of scratch (skip connections). */
 size_t gz_pv_weight_floats(void);
+size_t gz_pv_workspace_bytes(int32_t n);
 int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                  float* d_logits, float* d_value, float* d_probs, void* stream);
+                  float* d_logits, float* d_value, float* d_probs, void* d_workspace, void* stream);
 
 #ifdef __cplusplus
 }
