@@ -33,7 +33,11 @@ constexpr int V1_WT = V_B + 4;               // [225][64]
 constexpr int V1_B = V1_WT + 225 * 64;       // [64]
 constexpr int V2_W = V1_B + 64;              // [64]
 constexpr int V2_B = V2_W + 64;              // [1] (+3 pad)
-constexpr int TOTAL = V2_B + 4;
+// fp16x3 section: per residual conv W^T[n][k] as fp16 hi then fp16 lo
+// (2 halves per float slot); S/T are shared with the fp32 section
+constexpr int F16_RES0 = (V2_B + 4 + 3) & ~3;  // 16-byte aligned for h8 loads
+constexpr int F16_STRIDE = K * CH;           // floats: K*CH halves hi + K*CH halves lo
+constexpr int TOTAL = F16_RES0 + 4 * F16_STRIDE;
 
 // algorithmic work of one forward (neural_network.py:132-159), MACs
 constexpr long long MACS = 133690114LL;

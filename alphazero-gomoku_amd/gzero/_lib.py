@@ -14,6 +14,8 @@ GZ_OK = 0
 GZ_FLAG_GATHER_LEAVES = 1
 GZ_MAX_SIMULATIONS = 4095
 GZ_MAX_GAME_PLIES = 200
+GZ_PV_FP32 = 0
+GZ_PV_F16X3 = 1
 
 
 class GzeroUnavailable(RuntimeError):
@@ -78,7 +80,7 @@ SIGNATURES = {
     "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "gz_pv_weight_floats": (_SZ, []),
     "gz_pv_workspace_bytes": (_SZ, [_I32]),
-    "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),
+    "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _P]),
 }
 
 _lib = None

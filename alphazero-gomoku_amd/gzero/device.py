@@ -154,10 +154,17 @@ def search(states, game_ids, params, want_trees=False, leaf_cap=0):
 
 # ---------------------------------------------------------------- PV forward
 class PVWeights:
-    """Packed weight blob resident on the device (+ the kernel's scratch slab)."""
+    """Packed weight blob resident on the device (+ the fp32 kernel's scratch slab).
 
-    def __init__(self, blob):
+    precision: "fp32" (exact f32 MFMA) or "f16x3" (3-term fp16 split on the
+    fp16 MFMA, f32 accumulation)."""
+
+    def __init__(self, blob, precision="f16x3"):
         lib = require_gpu()
+        if precision not in ("fp32", "f16x3"):
+            raise ValueError(f"unknown precision {precision!r}")
+        self.precision = precision
+        self.mode = _lib.GZ_PV_FP32 if precision == "fp32" else _lib.GZ_PV_F16X3
         blob = np.ascontiguousarray(blob, np.float32)
         if blob.size != lib.gz_pv_weight_floats():
             raise ValueError(f"weight blob has {blob.size} floats, kernel expects {lib.gz_pv_weight_floats()}")
@@ -174,7 +181,8 @@ def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=No
     if d_value is None:
         d_value = torch.empty(n, dtype=torch.float32, device="cuda")
     _lib.check(lib.gz_pv_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_logits),
-                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace), stream()), "gz_pv_forward")
+                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace), weights.mode, stream()),
+               "gz_pv_forward")
     return d_logits, d_value, d_probs
 
 

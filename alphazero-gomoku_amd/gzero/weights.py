@@ -123,7 +123,11 @@ V1_WT = V_B + 4
 V1_B = V1_WT + 225 * 64
 V2_W = V1_B + 64
 V2_B = V2_W + 64
-TOTAL = V2_B + 4
+F16_RES0 = (V2_B + 4 + 3) & ~3  # 16-byte aligned (h8 loads)
+F16_STRIDE = K * CH
+TOTAL = F16_RES0 + 4 * F16_STRIDE
+
+PRECISIONS = {"fp32": 0, "f16x3": 1}  # GZ_PV_FP32, GZ_PV_F16X3
 
 PV_MACS = 133_690_114  # conv0 777,600 + 4 x 33,177,600 + heads 202,114
 PV_FLOPS = 2 * PV_MACS
@@ -147,6 +151,13 @@ def pack_pv_weights(sd):
         wk = w.permute(2, 3, 1, 0).reshape(K, CH)  # k = (kh*3+kw)*128 + cin
         base = RES0 + j * RES_STRIDE
         blob[base:base + K * CH] = wk.float().numpy().reshape(-1)
+        # fp16x3 copy: W^T[n][k] split into hi = fp16(w), lo = fp16(w - hi)
+        wt = wk.float().numpy().T.copy()  # [n][k]
+        hi = wt.astype(np.float16)
+        lo = (wt - hi.astype(np.float32)).astype(np.float16)
+        halves = np.concatenate([hi.reshape(-1), lo.reshape(-1)])
+        fb = F16_RES0 + j * F16_STRIDE
+        blob[fb:fb + F16_STRIDE] = halves.view(np.float32)
         blob[base + K * CH:base + K * CH + CH] = s.numpy()
         blob[base + K * CH + CH:base + K * CH + 2 * CH] = t.numpy()
     blob[P_W:P_W + 2 * CH] = sd["policy_conv.weight"].reshape(2, CH).numpy().reshape(-1)

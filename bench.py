@@ -9,7 +9,9 @@ exploration 0.05), beta = 0, planner_steps = 0, random-init network weights
 One "step" = every game slot plays `--plies-per-step` plies (one kernel launch,
 one wavefront per game) followed by the policy-value forward of EVERY node
 those searches created -- the GomokuModel.predict calls the reference makes
-(ai_agent.py:522-523) -- on the fp32 MFMA kernel, and (N > 1) the RCCL
+(ai_agent.py:522-523) -- on the MFMA kernel (default: 3-term fp16 split with
+f32 accumulation, within the 1e-4 logit tolerance; --pv-precision fp32 for the
+exact-f32 kernel), and (N > 1) the RCCL
 all-gather of the finished games' (s, pi, z) records.  `value` counts every
 ply played by every rank.
 
@@ -37,7 +39,8 @@ from gzero.device import PVWeights  # noqa: E402
 from gzero.selfplay import COUNTER_DTYPE, SelfPlayEngine  # noqa: E402
 
 METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2 dense peak
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (spec)
 PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
 
 
@@ -119,6 +122,8 @@ def main():
     ap.add_argument("--beta", type=float, default=0.0)
     ap.add_argument("--plies-per-step", type=int, default=1)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--pv-precision", default="f16x3", choices=["f16x3", "fp32"],
+                    help="policy-value forward: 3-term fp16 split (f32 accumulate) or exact fp32 MFMA")
     ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
     ap.add_argument("--elided-plies", type=int, default=20)
     ap.add_argument("--no-elided", action="store_true")
@@ -132,7 +137,7 @@ def main():
     if ws != args.gpus and rank == 0:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")
 
-    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)))
+    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision=args.pv_precision)
     base, stride = gdist.shard_ids(rank, ws, args.slots)
     P = args.plies_per_step
     eng = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
@@ -185,6 +190,25 @@ def main():
     mean_pv_s = float(np.mean(pv_ms)) / 1e3
     achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
     traffic, _ = load_traffic()
+    if args.pv_precision == "fp32":
+        peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
+    else:
+        # each algorithmic multiply of the 3x3 convs costs 3 fp16 MFMA products
+        peak = F16_MFMA_PEAK_TFLOPS / 3.0
+        note = ("3-term fp16 split on v_mfma_f32_16x16x32_f16 (f32 accumulate): peak = dense fp16 MFMA "
+                "peak / 3 products per fp32-equivalent multiply")
+    roofline = {
+        "kernel": f"pv_kernel<{args.pv_precision}> (AlphaZeroGomokuNet forward)",
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": round(peak, 1),
+        "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": traffic,
+        "per_launch": {"boards": round(mean_leaves, 1), "flop_per_board": PV_FLOP,
+                       "avg_ms": round(float(np.mean(pv_ms)), 3)},
+        "note": note,
+    }
 
     out = None
     if rank == 0:
@@ -199,13 +223,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.pv_precision == "fp32" else "f16x3 (fp32-equivalent split, f32 accumulate)",
             "data": "synthetic: self-play from the empty board with random-init weights (numpy default_rng(0))",
             "config": {
                 "workload": (f"BASELINE config 2: {args.slots} concurrent self-play games per GPU, 15x15, "
                              f"{args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), beta={args.beta}, "
-                             "planner_steps=0, continuous refill; policy-value forward (fp32 MFMA) on every "
-                             "non-terminal node the searches create (reference-work mode)"),
+                             "planner_steps=0, continuous refill; policy-value forward on every non-terminal node "
+                             f"the searches create (reference-work mode, {args.pv_precision})"),
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,
@@ -214,17 +238,7 @@ def main():
                 "pv_boards_per_step": round(mean_leaves, 1),
                 "pv_boards_dropped": dropped,
             },
-            "roofline": {
-                "kernel": "pv_kernel (AlphaZeroGomokuNet forward, fp32 MFMA)",
-                "bound": "mfma",
-                "achieved": round(achieved, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": traffic,
-                "per_launch": {"boards": round(mean_leaves, 1), "flop_per_board": PV_FLOP,
-                               "avg_ms": round(float(np.mean(pv_ms)), 3)},
-            },
+            "roofline": roofline,
         }
 
     # ---- prior-elided run (same kernel, no PV gather / forward)

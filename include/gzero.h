@@ -135,15 +135,20 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
                        gz_board_state* d_out, int64_t* d_game_ids, void* stream);
 
 /* ---- K6: AlphaZeroGomokuNet forward (neural_network.py:94-159,214-252) ----
- * fp32 MFMA.  d_weights: packed blob of gz_pv_weight_floats() floats (layout in
- * gzero/weights.py).  Boards [n][16] uint32 bit planes.  If d_count is not
- * NULL it holds the number of valid boards on the device (n = capacity).
- * Outputs: logits [n][225], value [n] (tanh), probs [n][225] (softmax) or NULL.
- * d_workspace: gz_pv_workspace_bytes(n) bytes of scratch (skip connections). */
+ * d_weights: packed blob of gz_pv_weight_floats() floats (layout in
+ * csrc/gz_pvnet.h / gzero/weights.py).  Boards [n][16] uint32 bit planes.  If
+ * d_count is not NULL it holds the number of valid boards on the device
+ * (n = capacity).  Outputs: logits [n][225], value [n] (tanh), probs
+ * [n][225] (softmax) or NULL.  precision: GZ_PV_FP32 (exact f32 MFMA; needs
+ * d_workspace of gz_pv_workspace_bytes(n) bytes) or GZ_PV_F16X3 (3-term fp16
+ * split on the fp16 MFMA, ~22-bit operands, f32 accumulation; no workspace). */
+#define GZ_PV_FP32 0
+#define GZ_PV_F16X3 1
 size_t gz_pv_weight_floats(void);
 size_t gz_pv_workspace_bytes(int32_t n);
 int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                  float* d_logits, float* d_value, float* d_probs, void* d_workspace, void* stream);
+                  float* d_logits, float* d_value, float* d_probs, void* d_workspace, int32_t precision,
+                  void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,7 +23,10 @@ trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.cs
 
 
 def short(name):
-    return name.split("::")[-1].split("(")[0]
+    n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("(")[0].split("<")[0].split("::")[-1]
 
 
 durs = {}

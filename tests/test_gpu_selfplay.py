@@ -63,7 +63,7 @@ def test_selfplay_leaf_count_equals_reference_predicts(oracle):
     the reference's GomokuModel.predict calls (one per non-terminal node)."""
     from gzero import weights
     from gzero.device import PVWeights
-    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)))
+    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision="f16x3")
     for gid in (900, 901):
         p = oracle.make_params("medium", sims=24, beta=0.0, seed=SEED)
         ref = oracle.play_game(p, p, gid)

@@ -15,8 +15,9 @@ from gzero import boards, device, weights  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--precision", default="f16x3")
 a = ap.parse_args()
-w = device.PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)))
+w = device.PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision=a.precision)
 rng = np.random.default_rng(0)
 cells = rng.choice(3, size=(a.n, 225), p=[0.5, 0.25, 0.25]).astype(np.int8)
 bl, wh = boards.cells_to_words(cells)
@@ -36,5 +37,5 @@ for _ in range(a.iters):
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1) / 1e3)
 t = float(np.median(ts))
-print(f"pv_kernel n={a.n}: {t*1e3:.1f} ms, {a.n/t:.0f} boards/s, {a.n*weights.PV_FLOPS/t/1e12:.1f} TFLOP/s "
+print(f"pv_kernel[{a.precision}] n={a.n}: {t*1e3:.1f} ms, {a.n/t:.0f} boards/s, {a.n*weights.PV_FLOPS/t/1e12:.1f} TFLOP/s "
       f"({a.n*weights.PV_FLOPS/t/1e12/157.3*100:.1f}% of fp32 MFMA peak)")
