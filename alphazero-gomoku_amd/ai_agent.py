@@ -1,0 +1,127 @@
+"""Drop-in ``ai_agent`` module (reference: ai_agent.py:23-623).
+
+``AlphaZeroGomokuAI.get_move`` runs the reference's search -- opening book,
+MCTS with UCT + beta*tanh(pattern/1e4), heuristic rollouts, exploration -- as
+one wavefront on the MI355X (``gz_search``), and evaluates the policy-value
+network on every node the search creates exactly as the reference does
+(``ai_agent.py:522-523``; the result is not read by the search there either).
+
+Randomness: the reference draws from the global ``random`` module (OS-seeded,
+irreproducible).  Here every draw comes from counter-based streams keyed by
+(``seed``, ``game_id``, ply, simulation) (gzero/rng.py); ``seed`` defaults to
+a fresh random value, so unseeded AIs are as random as the reference's while a
+fixed (seed, game_id) reproduces a game exactly, on any number of GPUs.
+
+Not yet on the device: BG-planner-guided rollout plies (``planner_steps > 0``).
+Such an AI raises ``GzeroError`` as soon as it needs a search; pass
+``planner_steps=0``.  ``time_limit`` is accepted for compatibility; the GPU
+completes every simulation (200 simulations take well under a millisecond), so
+the reference's wall-clock cut-off (ai_agent.py:183-189) never applies.
+"""
+import logging
+import random
+import time
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from gomoku_board import GomokuBoard
+from neural_network import GomokuModel
+from gzero import _lib, device
+
+
+class AlphaZeroGomokuAI:
+    def __init__(self, player: int, difficulty: str = "medium", model_path: Optional[str] = None,
+                 device: Optional[str] = None, beta: float = 0.2, planner_steps: int = 5,
+                 time_limit: float = 5.0, time_reward_factor: float = 0.1, seed: Optional[int] = None,
+                 game_id: int = 0, compute_priors: bool = True):
+        self.player = player
+        self.difficulty = difficulty
+        self.name = f"AlphaZero_{difficulty}"
+        self.device = device or "cpu"
+        self.beta = float(beta)
+        self.planner_steps = int(max(0, planner_steps))
+        self.time_limit = float(time_limit)
+        self.time_reward_factor = float(time_reward_factor)
+        self.logger = logging.getLogger(__name__)
+        self.model = GomokuModel(model_path=model_path, device=self.device)
+        # live knobs of the reference's table (ai_agent.py:65-90); bg_weight and
+        # planning_steps are kept but, as in the reference, never read
+        self.difficulty_params = {
+            "easy": {"device": "cpu", "bg_weight": 0.1, "planning_steps": 2, "num_simulations": 100,
+                     "c_puct": 1.4, "exploration": 0.2},
+            "medium": {"device": "cpu", "bg_weight": 0.2, "planning_steps": 3, "num_simulations": 200,
+                       "c_puct": 1.6, "exploration": 0.05},
+            "hard": {"device": "cpu", "bg_weight": 0.25, "planning_steps": 4, "num_simulations": 400,
+                     "c_puct": 1.8, "exploration": 0.01},
+        }
+        self.params = self.difficulty_params.get(difficulty, self.difficulty_params["medium"])
+        self.seed = random.getrandbits(64) if seed is None else int(seed)
+        self.game_id = int(game_id)
+        self.compute_priors = bool(compute_priors)
+        self.games_played = 0
+        self._last_decision_time = None
+        self.last_search_stats = None
+
+    def _search_params(self, gather):
+        if self.planner_steps:
+            raise _lib.GzeroError("planner_steps > 0 (BG-planner rollout plies) is not implemented on the device yet; "
+                                  "construct the AI with planner_steps=0")
+        return device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
+                                    self.params["exploration"], self.beta, self.seed, 100, 0, gather)
+
+    def get_move(self, board: GomokuBoard) -> Optional[Tuple[int, int]]:
+        """ai_agent.py:109-136 (opening book, MCTS, exploration) on the GPU."""
+        if not board.get_valid_moves():
+            return None
+        t0 = time.time()
+        needs_search = board.get_move_count() >= 6
+        gather = self.compute_priors and needs_search
+        if needs_search:
+            p = self._search_params(gather)
+        else:  # openings draw no simulation
+            p = device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
+                                     self.params["exploration"], self.beta, self.seed, 100, 0, False)
+        cap = p.num_simulations + 1 if gather else 0
+        mv, stats, _, leaves = device.search(board.to_state(), [self.game_id], p, leaf_cap=cap)
+        if gather and leaves is not None and len(leaves):
+            from gzero import boards
+            self.model.predict_batch(boards.words_to_cells(leaves[:, :8], leaves[:, 8:]))
+        self._last_decision_time = time.time() - t0
+        self.last_search_stats = stats[0]
+        self.games_played += 1
+        m = int(mv[0])
+        return None if m < 0 else (m // 15, m % 15)
+
+    def evaluate_position(self, board: GomokuBoard) -> float:
+        if board.game_over:
+            if board.winner == self.player:
+                return 1.0
+            return -1.0 if board.winner is not None else 0.0
+        _, value = self.model.predict(board.get_board_state())
+        return value
+
+    def _auto_save_model(self):
+        try:
+            return self.model.auto_save_model(suffix=f"_{self.difficulty}")
+        except Exception as e:  # ai_agent.py:484-485 logs and continues
+            self.logger.error(f"Failed to auto-save model: {e}")
+
+
+class AIFactory:
+    @staticmethod
+    def create_ai(ai_type: str, player: int, difficulty: str = "medium", **kwargs):
+        if ai_type == "alphazero":
+            return AlphaZeroGomokuAI(player, difficulty, **kwargs)
+        if ai_type == "bg_planner":
+            from bg_planner import BGPlannerAI
+            return BGPlannerAI(player, difficulty, device=kwargs.get("device", "cpu"))
+        raise ValueError(f"Unsupported ai_type: {ai_type}")
+
+    @staticmethod
+    def get_available_ai_types() -> List[str]:
+        return ["alphazero", "bg_planner"]
+
+    @staticmethod
+    def get_available_difficulties() -> List[str]:
+        return ["easy", "medium", "hard"]

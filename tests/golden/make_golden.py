@@ -602,6 +602,22 @@ def part_pvnet():
                    "value_f32_b64": enc(np.asarray(value_all)), "probs_f32_b64": enc(np.stack(probs_all))})
 
 
+def part_augment():
+    """G8: training.augment_sample -- label index and where the plane's stone lands."""
+    import numpy as np
+    h = ref()
+    out = []
+    for idx in range(225):
+        planes = np.zeros((3, 15, 15), np.float32)
+        planes[0].flat[idx] = 1.0
+        planes[2] = 1.0 - planes[0]
+        row = []
+        for x, y in h.tr.augment_sample(planes, idx):
+            row.append([int(y), int(np.argmax(x[0]))])
+        out.append(row)
+    dump("augment", {"cases": out})
+
+
 # ---------------------------------------------------------------------------
 # G7 full self-play games (training.play_one_game)
 # ---------------------------------------------------------------------------
@@ -638,7 +654,7 @@ def part_games():
 
 
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
-         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet,
+         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "augment": part_augment,
          "games": part_games}
 
 if __name__ == "__main__":

@@ -1,0 +1,91 @@
+"""The drop-in Python API (ai_agent / training / neural_network) driving the GPU
+engine, against the reference's golden vectors."""
+import base64
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import SEED, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _board(moves):
+    from gomoku_board import GomokuBoard
+    b = GomokuBoard()
+    for m in moves:
+        assert b.make_move(m // 15, m % 15)
+    return b
+
+
+def test_ai_get_move_golden():
+    from ai_agent import AlphaZeroGomokuAI
+    for c in golden("mcts")["cases"] + golden("mcts2")["cases"][:12]:
+        b = _board(c["moves"])
+        ai = AlphaZeroGomokuAI(b.current_player, c["difficulty"], beta=c["beta"], planner_steps=0, seed=SEED,
+                               game_id=c["game_id"])
+        ai.params["num_simulations"] = c["sims"]
+        mv = ai.get_move(b)
+        assert (mv[0] * 15 + mv[1]) == c["move"], c["game_id"]
+        assert ai.last_search_stats["predicts"] == c["predicts"]
+        assert b.get_move_count() == len(c["moves"])  # get_move does not mutate the board
+
+
+def test_play_one_game_golden():
+    from ai_agent import AlphaZeroGomokuAI
+    from training import play_one_game
+    for g in golden("games")["games"]:
+        kw = dict(beta=g["beta"], planner_steps=0, seed=SEED, game_id=g["game_id"])
+        ab = AlphaZeroGomokuAI(1, g["difficulty"], **kw)
+        aw = AlphaZeroGomokuAI(2, g["difficulty"], **kw)
+        ab.params["num_simulations"] = aw.params["num_simulations"] = g["sims"]
+        aw.model = ab.model
+        buf, n = play_one_game(ab, aw, step_timeout=1e9, game_timeout=1e9)
+        assert buf.move_indices == g["moves"]
+        assert buf.players == g["players"]
+        assert buf.outcomes == g["outcomes"]
+        assert n == g["len"]
+
+
+def test_batched_selfplay_matches_golden_games():
+    from training import selfplay
+    games = [g for g in golden("games")["games"] if g["sims"] == 2 and g["beta"] == 0.0]
+    rep, stats = selfplay(n_games=6, num_simulations=2, beta=0.0, seed=SEED, game_id_base=100)
+    assert stats["games"] == 6
+    for g in games:
+        s, n = stats["game_slices"][g["game_id"]]
+        assert rep.move_indices[s:s + n] == g["moves"]
+        assert rep.players[s:s + n] == g["players"]
+        assert rep.outcomes[s:s + n] == g["outcomes"]
+        assert rep.states[s][2].sum() == 225  # every game starts from the empty board
+
+
+def test_gomoku_model_predict_and_checkpoint(tmp_path):
+    from gzero import weights
+    from neural_network import GomokuModel
+    g = golden("pvnet")
+    sd = weights.init_state_dict(seed=g["weights_seed"])
+    path = str(tmp_path / "m.pth")
+    torch.save({"model_state_dict": sd, "model_type": "alphazero_gomoku", "board_size": 15, "device": "cpu"}, path)
+    m = GomokuModel(model_path=path)
+    n = len(g["cases"])
+    ref_p = np.frombuffer(base64.b64decode(g["probs_f32_b64"]), np.float32).reshape(n, 225)
+    ref_v = np.frombuffer(base64.b64decode(g["value_f32_b64"]), np.float32)
+    for i, c in enumerate(g["cases"][:16]):
+        b = _board(c["moves"])
+        p, v = m.predict(b.get_board_state())
+        assert np.abs(p - ref_p[i]).max() < 1e-4 and abs(v - ref_v[i]) < 1e-4
+        p3, v3 = m.predict(b.get_board_tensor())
+        assert np.abs(p3 - p).max() == 0 and v3 == v
+    # save / load round trip, and repacking after a parameter update
+    out = str(tmp_path / "models" / "x.pth")
+    m.save_model(out)
+    m2 = GomokuModel(model_path=out)
+    b = _board(g["cases"][3]["moves"])
+    assert np.array_equal(m.predict(b.get_board_state())[0], m2.predict(b.get_board_state())[0])
+    with torch.no_grad():
+        m2.model.policy_fc.bias.add_(1.0)  # uniform shift: softmax unchanged, repack must happen
+        m2.model.value_fc2.bias.add_(0.5)
+    assert m2.predict(b.get_board_state())[1] != m.predict(b.get_board_state())[1]
