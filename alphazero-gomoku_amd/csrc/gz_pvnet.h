@@ -33,11 +33,16 @@ constexpr int V1_WT = V_B + 4;               // [225][64]
 constexpr int V1_B = V1_WT + 225 * 64;       // [64]
 constexpr int V2_W = V1_B + 64;              // [64]
 constexpr int V2_B = V2_W + 64;              // [1] (+3 pad)
-// fp16x3 section: per residual conv W^T[n][k] as fp16 hi then fp16 lo
-// (2 halves per float slot); S/T are shared with the fp32 section
+// fp16x3 section: per residual conv, fp16 hi then fp16 lo (2 halves per float
+// slot), each in v_mfma_f32_16x16x32_f16 B-fragment order
+//   [ks 36][n-tile 8][lane 64][8]:  n = 16*n_tile + lane%16, k = 32*ks + 8*(lane/16) + j
+// so one wave's fragment is one contiguous 1 KiB load; S/T are shared with the fp32 section
 constexpr int F16_RES0 = (V2_B + 4 + 3) & ~3;  // 16-byte aligned for h8 loads
 constexpr int F16_STRIDE = K * CH;           // floats: K*CH halves hi + K*CH halves lo
-constexpr int TOTAL = F16_RES0 + 4 * F16_STRIDE;
+// conv0 in fp16 MFMA A-fragment order [n-tile 8][lane 64][8]: n = 16*n_tile + lane%16,
+// k = 8*(lane/16) + j (k >= 27 zero); hi then lo
+constexpr int F16_C0 = F16_RES0 + 4 * F16_STRIDE;
+constexpr int TOTAL = F16_C0 + 8 * 64 * 8;
 
 // algorithmic work of one forward (neural_network.py:132-159), MACs
 constexpr long long MACS = 133690114LL;

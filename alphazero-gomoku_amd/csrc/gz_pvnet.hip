@@ -5,21 +5,21 @@
 // over boards.  The board's 128x225 activation map stays in LDS for the whole
 // tower; every 3x3 conv is an implicit GEMM
 //   C[pos][ch] = sum_k A[pos][k] * W[k][ch],  A[pos][tap*128+cin] = act[cin][pos+tap]
-// with M = 225 positions (15 tiles of 16), N = 128 channels (8 tiles of 16):
-// wave w owns N tile w for all 15 M tiles, so each weight fragment is read
-// once per board per workgroup and reused 15 times.  Off-board neighbours read
-// a zero slot instead of predicating.  Two precisions (same layout of work):
+// with M = 225 positions (15 tiles of 16), N = 128 channels (8 tiles of 16).
+// Off-board neighbours read a zero slot instead of predicating.  Two precisions:
 //
 //  * GZ_PV_FP32: v_mfma_f32_16x16x4_f32 -- exact f32 products, f32 accumulate.
-//    Activations fp32, channel-major [ch][240].  The skip input of a residual
-//    block is parked in a per-wave global slab (registers are full).
+//    Wave w owns N tile w for all 15 M tiles (each weight fragment read once per
+//    board per workgroup).  Activations fp32, channel-major [ch][240].  The skip
+//    input of a residual block is parked in a per-wave global slab.
 //  * GZ_PV_F16X3: v_mfma_f32_16x16x32_f16 on a 3-term split, x = x_hi + x_lo
 //    (x_hi = fp16(x), x_lo = fp16(x - x_hi)):  a*w ~ a_hi*w_hi + a_hi*w_lo +
 //    a_lo*w_hi, every product exact in the f32 accumulator, ~22-bit operands.
 //    16x the f32 MFMA rate per instruction, 5.3x per fp32-equivalent product.
-//    Activations as hi/lo fp16 planes, position-major [240][136] (272-byte
-//    rows: 16-byte A fragments by ds_read_b128 with few bank conflicts).  The
-//    skip input stays in registers.
+//    Wave w owns 2 N tiles x 8 (or 7) M tiles, halving the LDS A-fragment reads
+//    per MFMA; activations as hi/lo fp16 planes [16 ch-groups][240][8]
+//    (conflict-free ds_read_b128); weights pre-arranged in B-fragment order.
+//    The skip input of a residual block stays in registers.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -34,24 +34,53 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
-constexpr int NT = 512;    // 8 waves: wave w owns output channels [16w, 16w+16)
 constexpr int MT = 15;     // 16-position M tiles (240 >= 225)
 constexpr int ROWS = 240;  // positions incl. 15 zero rows / slots
 constexpr int ZERO = POS;  // index of a zero slot: the out-of-board neighbour
-constexpr int RS = 136;    // fp16 row: 128 channels + 8 pad (272 B)
+constexpr int SLAB_F = 4096;  // per-wave skip slab (floats): fp32 15*4*64, f16x3 2*8*4*64
 
 // LDS layout (bytes): activation area first, then shared small buffers
 constexpr int ACT_BYTES_F32 = CH * ROWS * 4;      // 122880
-constexpr int ACT_BYTES_F16 = 2 * ROWS * RS * 2;  // 130560
+constexpr int ACT_BYTES_F16 = 2 * CH * 256 * 2;  // 131072: hi + lo planes of 256 rows
 constexpr int ACT_BYTES = ACT_BYTES_F16 > ACT_BYTES_F32 ? ACT_BYTES_F16 : ACT_BYTES_F32;
-constexpr int PLANES_F = 3 * ROWS;
-constexpr int SMALL_F = PLANES_F + 2 * POS + POS + 64 + 32 + 256;
-constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
 
 __device__ inline f32x4 zero4() {
     f32x4 z = {0.f, 0.f, 0.f, 0.f};
     return z;
 }
+
+// Phase stamps (tools/pv_stamps.py only): -DGZ_PV_STAMPS accumulates s_memtime
+// deltas of workgroup 0 / wave 0 per phase; compiled out otherwise.
+#ifdef GZ_PV_STAMPS
+__device__ unsigned long long gz_pv_stamps[32];
+#define PV_STAMP(i)                                                             \
+    do {                                                                        \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                              \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            gz_pv_stamps[i] += t_ - gz_pv_stamps[31];                           \
+            gz_pv_stamps[31] = t_;                                              \
+        }                                                                       \
+    } while (0)
+#define PV_WAVE_T0() unsigned long long wt0_ = __builtin_amdgcn_s_memtime()
+#define PV_WAVE_STAMP(slot)                                                                          \
+    do {                                                                                             \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                            \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
+            atomicAdd(&gz_pv_stamps[(slot) + (threadIdx.x >> 6)], t_ - wt0_);                         \
+            wt0_ = t_;                                                                               \
+        }                                                                                            \
+    } while (0)
+#else
+#define PV_WAVE_T0() \
+    do {             \
+    } while (0)
+#define PV_WAVE_STAMP(slot) \
+    do {                    \
+    } while (0)
+#define PV_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
 
 // neighbour index of the lane's position in M tile m for tap (dr, dc); ZERO if off-board
 __device__ inline int nbr(int m, int li, int dr, int dc) {
@@ -67,8 +96,12 @@ struct ActF32 {
     float* slab;
     __device__ float get(int ch, int pos) const { return a[ch * ROWS + pos]; }
     __device__ void put(int ch, int pos, float y) { a[ch * ROWS + pos] = y; }
-    __device__ void zero_slots(int tid) {
-        for (int i = tid; i < CH * (ROWS - POS); i += NT) a[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
+    __device__ void get8(int c0, int pos, float* x) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = a[(c0 + j) * ROWS + pos];
+    }
+    __device__ void zero_slots(int tid, int nth) {
+        for (int i = tid; i < CH * (ROWS - POS); i += nth) a[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
     }
     // k = tap*128 + cin, 4 input channels per k-step; B double-buffered 8 k-steps ahead
     __device__ __forceinline__ void conv(const float* __restrict__ Wk, int nt, int lane, f32x4 acc[MT]) const {
@@ -109,64 +142,393 @@ struct ActF32 {
 };
 
 // ============================================================ fp16x3 policy
+// Activations as hi/lo fp16 planes [CG][ROWS16][8]: channel group cg = ch/8 holds
+// 16 B per position, so the 16 lanes of a ds_read_b128 bank group read 16
+// consecutive positions = 16 distinct 16-B bank slots.  Rows 225..255 are zero;
+// an off-board neighbour with virtual index v reads zero row 225 + ((v-225) mod 16),
+// which keeps its bank slot = v mod 16, so no tap or board edge conflicts.
+constexpr int CG = CH / 8;
+constexpr int ROWS16 = 256;
+__device__ inline int nbr16(int m, int li, int dr, int dc) {
+    int pos = m * 16 + li;
+    int r = pos / 15 + dr, c = pos % 15 + dc;
+    bool ok = pos < POS && r >= 0 && r < 15 && c >= 0 && c < 15;
+    return ok ? r * 15 + c : POS + ((pos + dr * 15 + dc - POS) & 15);
+}
 struct ActF16x3 {
-    _Float16* hi;  // [ROWS][RS]
+    _Float16* hi;
     _Float16* lo;
+    __device__ static int off(int ch, int pos) { return ((ch >> 3) * ROWS16 + pos) * 8 + (ch & 7); }
     __device__ float get(int ch, int pos) const {
-        int o = pos * RS + ch;
+        int o = off(ch, pos);
         return (float)hi[o] + (float)lo[o];
     }
     __device__ void put(int ch, int pos, float y) {
         _Float16 h = (_Float16)y;
         _Float16 l = (_Float16)(y - (float)h);  // y - h is exact in f32
-        int o = pos * RS + ch;
+        int o = off(ch, pos);
         hi[o] = h;
         lo[o] = l;
     }
-    __device__ void zero_slots(int tid) {
-        for (int i = tid; i < (ROWS - POS) * RS; i += NT) {
-            hi[POS * RS + i] = (_Float16)0.f;
-            lo[POS * RS + i] = (_Float16)0.f;
-        }
+    __device__ void get8(int c0, int pos, float* x) const {  // channels c0..c0+7, c0 % 8 == 0
+        const h8 xh = *(const h8*)(hi + ((c0 >> 3) * ROWS16 + pos) * 8);
+        const h8 xl = *(const h8*)(lo + ((c0 >> 3) * ROWS16 + pos) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = (float)xh[j] + (float)xl[j];
     }
-    // k = tap*128 + cin, 32 input channels per k-step (lane group q = lane>>4 holds 8)
-    __device__ __forceinline__ void conv(const _Float16* __restrict__ Whi, const _Float16* __restrict__ Wlo, int nt,
-                                         int lane, f32x4 acc[MT]) const {
-        const int li = lane & 15, q = lane >> 4;
-        const _Float16* wh = Whi + (size_t)(nt * 16 + li) * K + 8 * q;  // W^T [n][k]
-        const _Float16* wl = Wlo + (size_t)(nt * 16 + li) * K + 8 * q;
-        h8 bh = *(const h8*)wh, bl = *(const h8*)wl;
-        for (int tap = 0; tap < 9; tap++) {
-            const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-            int lv = li;
-            asm volatile("" : "+v"(lv));
-            int nb[MT];
-#pragma unroll
-            for (int m = 0; m < MT; m++) nb[m] = nbr(m, lv, dr, dc) * RS + 8 * q;
-#pragma unroll
-            for (int cq = 0; cq < 4; cq++) {
-                const int ks = tap * 4 + cq;
-                h8 bhn = bh, bln = bl;
-                if (ks + 1 < 36) {
-                    bhn = *(const h8*)(wh + (ks + 1) * 32);
-                    bln = *(const h8*)(wl + (ks + 1) * 32);
-                }
-                const _Float16* ahp = hi + cq * 32;
-                const _Float16* alp = lo + cq * 32;
-#pragma unroll
-                for (int m = 0; m < MT; m++) {
-                    const h8 ah = *(const h8*)(ahp + nb[m]);
-                    const h8 al = *(const h8*)(alp + nb[m]);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[m], 0, 0, 0);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[m], 0, 0, 0);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[m], 0, 0, 0);
-                }
-                bh = bhn;
-                bl = bln;
-            }
+    __device__ void zero_slots(int tid, int nth) {
+        constexpr int PAD = (ROWS16 - POS) * 8;
+        for (int i = tid; i < CG * PAD; i += nth) {
+            int o = (i / PAD) * ROWS16 * 8 + POS * 8 + i % PAD;
+            hi[o] = (_Float16)0.f;
+            lo[o] = (_Float16)0.f;
         }
     }
 };
+
+// Residual tower in f16x3.  Wave w owns n-tiles {2(w&3), 2(w&3)+1} (32 output
+// channels) x M tiles [8(w>>2), 8(w>>2)+NM): NM = 8 for waves 0-3, 7 for waves
+// 4-7 (waves w and w+4 share a SIMD, so every SIMD carries 15 tile rows).
+// Per 32-deep k-step a wave issues 2*NM ds_read_b128 for 6*NM MFMAs and two
+// 1-KiB B-fragment loads per n-tile (hi, lo), prefetched one k-step ahead.
+constexpr int KS_HALVES = 8 * 64 * 8;  // B fragments of one k-step, all n-tiles
+
+template <int NM>
+__device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __restrict__ Wf, int np, int m0,
+                                         int lane, f32x4 (&acc)[2][NM]) {
+    // Software pipeline over half k-steps: the A fragments of M tiles [HA, NM)
+    // are read while the MFMAs of tiles [0, HA) run, and those of [0, HA) for
+    // the next k-step while the MFMAs of [HA, NM) run.  The order is pinned with
+    // sched_group_barrier (the default scheduler sinks every read to its use).
+    // Branch-free: the last k-step prefetches k-step 0 / tap 9 (valid addresses,
+    // results unused) so each tap is one basic block.
+    constexpr int HA = (NM + 1) / 2, HB = NM - HA;
+    const int li = lane & 15, q = lane >> 4;
+    const _Float16* wh = Wf + ((size_t)(2 * np) * 64 + lane) * 8;
+    const _Float16* wl = wh + K * CH;
+    h8 b[2][2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        b[n][0] = *(const h8*)(wh + n * 512);
+        b[n][1] = *(const h8*)(wl + n * 512);
+    }
+    h8 ah[NM], al[NM];
+    int nb[NM];
+    int lv = li;
+    asm volatile("" : "+v"(lv));
+#pragma unroll
+    for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lv, -1, -1) + q * ROWS16) * 8;
+#pragma unroll
+    for (int m = 0; m < HA; m++) {
+        ah[m] = *(const h8*)(act.hi + nb[m]);
+        al[m] = *(const h8*)(act.lo + nb[m]);
+    }
+    for (int tap = 0; tap < 9; tap++) {
+#pragma unroll
+        for (int cq = 0; cq < 4; cq++) {
+            const int ks = tap * 4 + cq;
+            const int ao = cq * 4 * ROWS16 * 8;
+#ifndef GZ_PV_EXP_NO_A
+#pragma unroll
+            for (int m = HA; m < NM; m++) {
+                ah[m] = *(const h8*)(act.hi + ao + nb[m]);
+                al[m] = *(const h8*)(act.lo + ao + nb[m]);
+            }
+#endif
+            h8 bn[2][2];
+            {
+#ifndef GZ_PV_EXP_NO_B
+                const int ks1 = ks + 1 < 36 ? ks + 1 : 0;
+#else
+                const int ks1 = 0;
+#endif
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    bn[n][0] = *(const h8*)(wh + ks1 * KS_HALVES + n * 512);
+                    bn[n][1] = *(const h8*)(wl + ks1 * KS_HALVES + n * 512);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < HA; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
+            }
+            if (cq == 3) {  // next tap: new neighbour offsets (tap 9 after the last: unused)
+                const int t2 = tap + 1, dr = t2 / 3 - 1, dc = t2 % 3 - 1;
+                int lw = li;
+                asm volatile("" : "+v"(lw));
+#pragma unroll
+                for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lw, dr, dc) + q * ROWS16) * 8;
+            }
+            {
+                const int ao2 = ((cq + 1) & 3) * 4 * ROWS16 * 8;
+#ifndef GZ_PV_EXP_NO_A
+#pragma unroll
+                for (int m = 0; m < HA; m++) {
+                    ah[m] = *(const h8*)(act.hi + ao2 + nb[m]);
+                    al[m] = *(const h8*)(act.lo + ao2 + nb[m]);
+                }
+#else
+                (void)ao2;
+#endif
+            }
+#pragma unroll
+            for (int m = HA; m < NM; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
+            }
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                b[n][0] = bn[n][0];
+                b[n][1] = bn[n][1];
+            }
+#ifndef GZ_PV_NO_SCHED
+            // pin the interleave: B prefetch first, then 2 A reads per 6 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);  // VMEM read
+#pragma unroll
+            for (int m = 0; m < HA; m++) {
+                if (m < HB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);              // MFMA
+            }
+#pragma unroll
+            for (int m = 0; m + 1 < HB; m++) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * (HA - HB), 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+#endif
+        }
+    }
+}
+
+#ifdef GZ_PV_EXP_DB
+// experiment: full double buffering of the A fragments (one k-step ahead)
+template <int NM>
+__device__ __forceinline__ void f16_conv_db(const ActF16x3& act, const _Float16* __restrict__ Wf, int np, int m0,
+                                            int lane, f32x4 (&acc)[2][NM]) {
+    const int li = lane & 15, q = lane >> 4;
+    const _Float16* wh = Wf + ((size_t)(2 * np) * 64 + lane) * 8;
+    const _Float16* wl = wh + K * CH;
+    h8 b[2][2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        b[n][0] = *(const h8*)(wh + n * 512);
+        b[n][1] = *(const h8*)(wl + n * 512);
+    }
+    h8 ah[NM], al[NM];
+    int nb[NM];
+    int lv = li;
+    asm volatile("" : "+v"(lv));
+#pragma unroll
+    for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lv, -1, -1) + q * ROWS16) * 8;
+#pragma unroll
+    for (int m = 0; m < NM; m++) {
+        ah[m] = *(const h8*)(act.hi + nb[m]);
+        al[m] = *(const h8*)(act.lo + nb[m]);
+    }
+    for (int tap = 0; tap < 9; tap++) {
+#pragma unroll
+        for (int cq = 0; cq < 4; cq++) {
+            const int ks = tap * 4 + cq;
+            h8 bn[2][2];
+            const int ks1 = ks + 1 < 36 ? ks + 1 : 0;
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                bn[n][0] = *(const h8*)(wh + ks1 * KS_HALVES + n * 512);
+                bn[n][1] = *(const h8*)(wl + ks1 * KS_HALVES + n * 512);
+            }
+            if (cq == 3) {
+                const int t2 = tap + 1, dr = t2 / 3 - 1, dc = t2 % 3 - 1;
+                int lw = li;
+                asm volatile("" : "+v"(lw));
+#pragma unroll
+                for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lw, dr, dc) + q * ROWS16) * 8;
+            }
+            const int ao2 = ((cq + 1) & 3) * 4 * ROWS16 * 8;
+            h8 nh[NM], nl[NM];
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                nh[m] = *(const h8*)(act.hi + ao2 + nb[m]);
+                nl[m] = *(const h8*)(act.lo + ao2 + nb[m]);
+            }
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
+            }
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                ah[m] = nh[m];
+                al[m] = nl[m];
+            }
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                b[n][0] = bn[n][0];
+                b[n][1] = bn[n][1];
+            }
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            }
+        }
+    }
+}
+#endif
+
+// The f16 MFMAs compute C^T[ch][pos] (A = weight fragment, B = activation
+// fragment), so lane (li, g) holds channels 4g..4g+3 of its N tile for position
+// 16*tile + li: 4 consecutive channels = 8 bytes of the hi plane and 8 of the lo.
+__device__ __forceinline__ void f16_get4(const ActF16x3& act, int ch0, int pos, f32x4& out) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const int o = ActF16x3::off(ch0, pos);
+    const h4 xh = *(const h4*)(act.hi + o);
+    const h4 xl = *(const h4*)(act.lo + o);
+#pragma unroll
+    for (int r = 0; r < 4; r++) out[r] = (float)xh[r] + (float)xl[r];
+}
+
+// y = acc*S + T (+ skip), ReLU, split into hi/lo and stored as two 8-byte writes
+template <bool SKIP>
+__device__ __forceinline__ void f16_put4(ActF16x3& act, const f32x4& acc, const f32x4& s, const f32x4& t,
+                                         const f32x4& skip, int ch0, int pos) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    h4 hi, lo;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        float y = acc[r] * s[r] + t[r];
+        if (SKIP) y += skip[r];
+        y = y > 0.f ? y : 0.f;
+        const _Float16 h = (_Float16)y;
+        hi[r] = h;
+        lo[r] = (_Float16)(y - (float)h);  // y - h is exact in f32
+    }
+    const int o = ActF16x3::off(ch0, pos);
+    *(h4*)(act.hi + o) = hi;
+    *(h4*)(act.lo + o) = lo;
+}
+
+template <int NM>
+__device__ __forceinline__ void f16_load(const ActF16x3& act, f32x4 (&out)[2][NM], int np, int m0, int lane) {
+    asm volatile("" : "+v"(lane));  // addresses are recomputed per layer, not hoisted (and spilled)
+    lane &= 63;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = (m0 + m) * 16 + (lane & 15);
+            if (pos < POS) f16_get4(act, ch0, pos, out[n][m]);
+            else out[n][m] = zero4();
+        }
+    }
+}
+
+template <int NM, bool SKIP>
+__device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][NM], const float* __restrict__ S,
+                                          const float* __restrict__ T, const f32x4 (&skip)[2][NM], int np, int m0,
+                                          int lane) {
+    asm volatile("" : "+v"(lane));  // addresses are recomputed per layer, not hoisted (and spilled)
+    lane &= 63;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(S + ch0), t = *(const f32x4*)(T + ch0);
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = (m0 + m) * 16 + (lane & 15);
+            if (pos < POS) f16_put4<SKIP>(act, acc[n][m], s, t, skip[n][m], ch0, pos);
+        }
+    }
+}
+
+template <int NM, int m0>
+__device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict__ W, int wave, int lane) {
+    const int np = wave & 3;
+    for (int blk = 0; blk < 2; blk++) {
+        f32x4 skip[2][NM];
+        for (int half = 0; half < 2; half++) {
+            const int layer = 2 * blk + half;
+            const float* R = W + RES0 + layer * RES_STRIDE;
+            f32x4 acc[2][NM];
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int m = 0; m < NM; m++) acc[n][m] = zero4();
+            PV_WAVE_T0();
+#ifdef GZ_PV_EXP_HALF_WAVES
+            if (wave < 4)
+#endif
+#ifdef GZ_PV_EXP_DB
+            f16_conv_db<NM>(act, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, m0, lane, acc);
+#else
+            f16_conv<NM>(act, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, m0, lane, acc);
+#endif
+            PV_STAMP(2);
+            PV_WAVE_STAMP(8);
+#ifndef GZ_PV_EXP_NOSKIP
+            if (half == 0) f16_load<NM>(act, skip, np, m0, lane);  // block input, for the skip connection
+#endif
+            __syncthreads();
+            PV_WAVE_STAMP(16);
+            PV_STAMP(3);
+            if (half == 0)
+                f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+            else
+#ifndef GZ_PV_EXP_NOSKIP
+                f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+#else
+                f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+#endif
+            __syncthreads();
+            PV_STAMP(4);
+        }
+    }
+}
+
+// conv0 3->128 + BN + ReLU in f16 (C^T form): the input planes are 0/1, exact in
+// fp16, so a*w = a*w_hi + a*w_lo (2 MFMAs, no a_lo term); K = 27 (k = tap*3 + cin)
+// padded to one 32-deep k-step.  Wave w: N tile w, all 15 M tiles.
+__device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict__ W, const float* planes, int nt,
+                                          int lane) {
+    const int li = lane & 15, q = lane >> 4;
+    const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
+    const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
+    const int ch0 = nt * 16 + 4 * q;
+    const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
+    const f32x4 none = zero4();
+    int lv = li;
+    asm volatile("" : "+v"(lv));
+    for (int m = 0; m < MT; m++) {
+        h8 a;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = 8 * q + j;  // lane-uniform within each quarter-wave
+            const int tap = k / 3, cin = k % 3;
+            const int idx = k < 27 ? nbr(m, lv, tap / 3 - 1, tap % 3 - 1) : ZERO;
+            a[j] = (_Float16)planes[(k < 27 ? cin : 0) * ROWS + idx];
+        }
+        f32x4 acc = zero4();
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
+        const int pos = m * 16 + li;
+        if (pos < POS) f16_put4<false>(act, acc, s, t, none, ch0, pos);
+    }
+}
 
 // epilogue: y = acc*S + T (+ skip), ReLU, back into the map.
 // C layout of the 16x16 MFMAs: column (channel) = lane&15, row (position) = 4*(lane>>4) + r.
@@ -185,19 +547,6 @@ __device__ __forceinline__ void store_tiles(Act& act, const f32x4 acc[MT], const
                 if (skip) y += skip[m][r];
                 act.put(ch, pos, y > 0.f ? y : 0.f);
             }
-        }
-    }
-}
-
-template <class Act>
-__device__ __forceinline__ void load_tiles(const Act& act, f32x4 out[MT], int nt, int lane) {
-    const int ch = nt * 16 + (lane & 15), g = lane >> 4;
-#pragma unroll
-    for (int m = 0; m < MT; m++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            int pos = m * 16 + 4 * g + r;
-            out[m][r] = pos < POS ? act.get(ch, pos) : 0.f;
         }
     }
 }
@@ -233,169 +582,280 @@ __device__ inline float wave_max(float v) {
     return v;
 }
 
-template <int PREC>
-__global__ __launch_bounds__(NT, 1) void pv_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards, int n,
-                                                   const int32_t* d_count, float* __restrict__ logits,
-                                                   float* __restrict__ value, float* __restrict__ probs,
-                                                   float* __restrict__ scratch) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-    float* small = (float*)(lds + ACT_BYTES);
-    float* planes = small;  // [3][ROWS] fp32
-    float* hp = planes + PLANES_F;
-    float* hv = hp + 2 * POS;
-    float* hh = hv + POS;
-    float* red = hh + 64;
-    float* lg = red + 32;
-    using Act = typename std::conditional<PREC == GZ_PV_FP32, ActF32, ActF16x3>::type;
-    Act act;
-    if constexpr (PREC == GZ_PV_FP32) {
-        act.a = (float*)lds;
-    } else {
-        act.hi = (_Float16*)lds;
-        act.lo = act.hi + ROWS * RS;
+// sum_i w[i*stride] * x[i] for one output column; BATCH independent loads in flight
+template <int NI, int BATCH>
+__device__ __forceinline__ float dot_col(const float* __restrict__ wp, int stride, const float* __restrict__ xp) {
+    static_assert(NI % BATCH == 0, "batch must divide the input count");
+    float acc = 0.f;
+#pragma unroll 1
+    for (int i0 = 0; i0 < NI; i0 += BATCH) {
+        float w[BATCH];
+#pragma unroll
+        for (int j = 0; j < BATCH; j++) w[j] = wp[(size_t)(i0 + j) * stride];
+#pragma unroll
+        for (int j = 0; j < BATCH; j++) acc += w[j] * xp[i0 + j];
     }
+    return acc;
+}
 
-    int count = n;
-    if (d_count) {
-        int c = *d_count;
-        count = c < n ? c : n;
+// ---- shared pieces of both kernels; NTH = threads per workgroup
+
+struct Smem {
+    float* planes;  // [3][ROWS] fp32 input planes
+    float* hp;      // [2*POS] policy 1x1 conv output (channel-major flatten)
+    float* hv;      // [POS] value 1x1 conv output
+    float* red;     // [32] softmax reductions
+    float* lg;      // [256] logits, then exp(logit - max)
+    float* part;    // [2][256] policy_fc partial sums
+    float* vq;      // [3][64] value_fc1 partial sums
+};
+constexpr int SMALL_F = 3 * ROWS + 2 * POS + POS + 32 + 256 + 512 + 192;
+constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
+
+__device__ inline Smem smem_layout(char* lds) {
+    Smem m;
+    m.planes = (float*)(lds + ACT_BYTES);
+    m.hp = m.planes + 3 * ROWS;
+    m.hv = m.hp + 2 * POS;
+    m.red = m.hv + POS;
+    m.lg = m.red + 32;
+    m.part = m.lg + 256;
+    m.vq = m.part + 512;
+    return m;
+}
+
+// input planes [black, white, empty] (gomoku_board.py:239-260, absolute colours)
+template <int NTH>
+__device__ __forceinline__ void load_planes(float* planes, const uint32_t* __restrict__ bd, int tid) {
+    for (int p = tid; p < POS; p += NTH) {
+        int bit = (p / 15) * 16 + (p % 15);
+        uint32_t bl = (bd[bit >> 5] >> (bit & 31)) & 1u;
+        uint32_t wh = (bd[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+        planes[p] = (float)bl;
+        planes[ROWS + p] = (float)wh;
+        planes[2 * ROWS + p] = (float)(1u - (bl | wh));
     }
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nt = wave;
-    float* slab = scratch ? scratch + ((size_t)blockIdx.x * (NT / 64) + wave) * (MT * 4 * 64) : nullptr;
-    act.zero_slots(tid);
-    for (int i = tid; i < 3 * (ROWS - POS); i += NT) planes[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
+}
 
-    for (int b = blockIdx.x; b < count; b += gridDim.x) {
-        // ---- input planes [black, white, empty] (gomoku_board.py:239-260, absolute colours)
-        const uint32_t* bd = boards + (size_t)b * 16;
-        for (int p = tid; p < POS; p += NT) {
-            int bit = (p / 15) * 16 + (p % 15);
-            uint32_t bl = (bd[bit >> 5] >> (bit & 31)) & 1u;
-            uint32_t wh = (bd[8 + (bit >> 5)] >> (bit & 31)) & 1u;
-            planes[p] = (float)bl;
-            planes[ROWS + p] = (float)wh;
-            planes[2 * ROWS + p] = (float)(1u - (bl | wh));
+// conv0 3->128 + BN + ReLU for N tile nt (exact f32 MFMA in both modes): K = 27 (k = tap*3+cin) -> 28
+template <class Act>
+__device__ __forceinline__ void conv0_tile(Act& act, const float* __restrict__ W, const float* planes, int nt,
+                                           int lane) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[m] = zero4();
+    int li = lane & 15;
+    asm volatile("" : "+v"(li));
+    const int g = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < K0 / 4; s++) {
+        const int k = 4 * s + g;
+        const int tap = k / 3, cin = k % 3;
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        const float bw = W[C0_W + k * CH + nt * 16 + li];  // row 27 is zero
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+            int idx = k < 27 ? nbr(m, li, dr, dc) : ZERO;
+            float a = planes[(k < 27 ? cin : 0) * ROWS + idx];
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw, acc[m], 0, 0, 0);
         }
-        __syncthreads();
+    }
+    store_tiles(act, acc, W + C0_S, W + C0_T, (const f32x4*)nullptr, nt, lane);
+}
 
-        // ---- conv0 3->128 + BN + ReLU (exact f32 MFMA in both modes): K = 27 (k = tap*3+cin) -> 28
-        f32x4 acc[MT];
+// heads (neural_network.py:132-159) + softmax (neural_network.py:240-247) for board b;
+// the tower's output map is in act.  Ends with a barrier.
+template <int NTH, class Act>
+__device__ __forceinline__ void heads(const Act& act, const Smem& sm, const float* __restrict__ W, int b, int tid,
+                                      float* __restrict__ logits, float* __restrict__ value,
+                                      float* __restrict__ probs) {
+    const int lane = tid & 63, wave = tid >> 6;
+    // 1x1 convs (policy 128->2, value 128->1), one thread per position
+    if (tid < POS) {
+        const int pos = tid;
+        float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
+        for (int c0 = 0; c0 < CH; c0 += 8) {
+            float a[8];
+            act.get8(c0, pos, a);
 #pragma unroll
-        for (int m = 0; m < MT; m++) acc[m] = zero4();
-        {
-            int li = lane & 15;
-            asm volatile("" : "+v"(li));
-            const int g = lane >> 4;
-#pragma unroll
-            for (int s = 0; s < K0 / 4; s++) {
-                const int k = 4 * s + g;
-                const int tap = k / 3, cin = k % 3;
-                const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-                const float bw = W[C0_W + k * CH + nt * 16 + li];  // row 27 is zero
-#pragma unroll
-                for (int m = 0; m < MT; m++) {
-                    int idx = k < 27 ? nbr(m, li, dr, dc) : ZERO;
-                    float a = planes[(k < 27 ? cin : 0) * ROWS + idx];
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw, acc[m], 0, 0, 0);
-                }
+            for (int j = 0; j < 8; j++) {
+                p0 += W[P_W + c0 + j] * a[j];
+                p1 += W[P_W + CH + c0 + j] * a[j];
+                v += W[V_W + c0 + j] * a[j];
             }
         }
-        store_tiles(act, acc, W + C0_S, W + C0_T, (const f32x4*)nullptr, nt, lane);
-        __syncthreads();
+        sm.hp[pos] = p0;  // flatten order: channel-major (policy.view(B, -1))
+        sm.hp[POS + pos] = p1;
+        sm.hv[pos] = v;
+    }
+    __syncthreads();
+    PV_STAMP(5);
+    // policy_fc 450->225: thread (h, o) sums input part h of NTH/256 for output o
+    constexpr int NH = NTH / 256, HI = 2 * POS / NH;
+    {
+        const int o = tid & 255, h = tid >> 8;
+        if (o < POS) sm.part[h * 256 + o] = dot_col<HI, 45>(W + PF_WT + (size_t)h * HI * POS + o, POS, sm.hp + h * HI);
+    }
+    __syncthreads();
+    // logits = bias + parts; value_fc1 225->64 in input thirds (192 threads: waves 4-6, or 0-2 at 256 threads)
+    if (tid < POS) {
+        float l = W[PF_B + tid];
+#pragma unroll
+        for (int h = 0; h < NH; h++) l += sm.part[h * 256 + tid];
+        sm.lg[tid] = l;
+    }
+    {
+        const int t = NTH == 512 ? tid - 256 : tid;
+        if (t >= 0 && t < 192) {
+            const int j = t & 63, t3 = t >> 6;
+            sm.vq[t3 * 64 + j] = dot_col<75, 25>(W + V1_WT + t3 * 75 * 64 + j, 64, sm.hv + t3 * 75);
+        }
+    }
+    __syncthreads();
+    PV_STAMP(6);
+    // value_fc1 bias + ReLU, value_fc2 + tanh (wave 0); softmax max/sum over 225 logits (waves 0..3)
+    if (wave == 0) {
+        float h1 = W[V1_B + lane] + (sm.vq[lane] + sm.vq[64 + lane] + sm.vq[128 + lane]);
+        h1 = h1 > 0.f ? h1 : 0.f;
+        float part2 = W[V2_W + lane] * h1;
+        float tot = wave_sum(part2) + W[V2_B];
+        if (lane == 0) value[b] = tanhf(tot);
+    }
+    if (wave < 4) {
+        float x = tid < POS ? sm.lg[tid] : -3.0e38f;
+        float mx = wave_max(x);
+        if (lane == 0) sm.red[wave] = mx;
+    }
+    __syncthreads();
+    if (wave < 4) {
+        const float mx = fmaxf(fmaxf(sm.red[0], sm.red[1]), fmaxf(sm.red[2], sm.red[3]));
+        float e = tid < POS ? __expf(sm.lg[tid] - mx) : 0.f;
+        float s = wave_sum(e);
+        if (lane == 0) sm.red[8 + wave] = s;
+        if (tid < POS) {
+            logits[(size_t)b * POS + tid] = sm.lg[tid];
+            sm.lg[tid] = e;
+        }
+    }
+    __syncthreads();
+    if (wave < 4 && probs) {
+        const float s = (sm.red[8] + sm.red[9]) + (sm.red[10] + sm.red[11]);
+        if (tid < POS) probs[(size_t)b * POS + tid] = sm.lg[tid] / s;
+    }
+    __syncthreads();
+    PV_STAMP(7);
+}
 
-        // ---- residual tower (ResidualBlock, neural_network.py:74-91)
+__device__ inline int board_count(int n, const int32_t* d_count) {
+    if (!d_count) return n;
+    int c = *d_count;
+    return c < n ? c : n;
+}
+
+// ============================================================ fp32 kernel: 8 waves, wave w = N tile w
+constexpr int NT32 = 512;
+__global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict__ W,
+                                                       const uint32_t* __restrict__ boards, int n,
+                                                       const int32_t* d_count, float* __restrict__ logits,
+                                                       float* __restrict__ value, float* __restrict__ probs,
+                                                       float* __restrict__ scratch) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const Smem sm = smem_layout(lds);
+    ActF32 act;
+    act.a = (float*)lds;
+    const int count = board_count(n, d_count);
+    float* slab = scratch + ((size_t)blockIdx.x * (NT32 / 64) + (threadIdx.x >> 6)) * SLAB_F;
+    act.zero_slots(threadIdx.x, NT32);
+    for (int i = threadIdx.x; i < 3 * (ROWS - POS); i += NT32)
+        sm.planes[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
+
+    for (int b = blockIdx.x; b < count; b += gridDim.x) {
+        // re-derive the lane ids per board: nothing lane-dependent is hoisted out
+        // of this loop and kept live (spilled) across the whole tower
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, nt = __builtin_amdgcn_readfirstlane(tid >> 6);
+        load_planes<NT32>(sm.planes, boards + (size_t)b * 16, tid);
+        __syncthreads();
+        conv0_tile(act, W, sm.planes, nt, lane);
+        __syncthreads();
+        // residual tower (ResidualBlock, neural_network.py:74-91)
         for (int blk = 0; blk < 2; blk++) {
-            f32x4 skip[MT];
             for (int half = 0; half < 2; half++) {
                 const int layer = 2 * blk + half;
                 const float* R = W + RES0 + layer * RES_STRIDE;
+                f32x4 acc[MT];
 #pragma unroll
                 for (int m = 0; m < MT; m++) acc[m] = zero4();
-                if constexpr (PREC == GZ_PV_FP32) {
-                    act.conv(R + RES_W, nt, lane, acc);
-                } else {
-                    const _Float16* wh = (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE);
-                    act.conv(wh, wh + K * CH, nt, lane, acc);
-                }
-                if (half == 0) {  // keep the block input for the skip connection
-                    if constexpr (PREC == GZ_PV_FP32) slab_save(act, slab, nt, lane);
-                    else load_tiles(act, skip, nt, lane);
-                }
+                act.conv(R + RES_W, nt, lane, acc);
+                if (half == 0) slab_save(act, slab, nt, lane);  // keep the block input for the skip connection
                 __syncthreads();
                 if (half == 0) {
                     store_tiles(act, acc, R + RES_S, R + RES_T, (const f32x4*)nullptr, nt, lane);
                 } else {
-                    if constexpr (PREC == GZ_PV_FP32) slab_load(slab, skip, lane);
+                    f32x4 skip[MT];
+                    slab_load(slab, skip, lane);
                     store_tiles(act, acc, R + RES_S, R + RES_T, skip, nt, lane);
                 }
                 __syncthreads();
             }
         }
+        heads<NT32>(act, sm, W, b, tid, logits, value, probs);
+    }
+}
 
-        // ---- heads: 1x1 convs (policy 128->2, value 128->1)
-        if (tid < POS) {
-            const int pos = tid;
-            float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
-            for (int c = 0; c < CH; c++) {
-                float a = act.get(c, pos);
-                p0 += W[P_W + c] * a;
-                p1 += W[P_W + CH + c] * a;
-                v += W[V_W + c] * a;
-            }
-            hp[pos] = p0;  // flatten order: channel-major (policy.view(B, -1))
-            hp[POS + pos] = p1;
-            hv[pos] = v;
-        }
+// ============================================================ f16x3 kernel: 8 waves (two per SIMD)
+// (one wave per SIMD with 512 registers and all 15 M tiles per wave measured 37%
+// slower: the compiler serialises the A-fragment reads of a single stream)
+constexpr int NT16 = 512;
+__global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restrict__ W,
+                                                         const uint32_t* __restrict__ boards, int n,
+                                                         const int32_t* d_count, float* __restrict__ logits,
+                                                         float* __restrict__ value, float* __restrict__ probs) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const Smem sm = smem_layout(lds);
+    ActF16x3 act;
+    act.hi = (_Float16*)lds;
+    act.lo = act.hi + CH * ROWS16;
+    const int count = board_count(n, d_count);
+    act.zero_slots(threadIdx.x, NT16);
+    for (int i = threadIdx.x; i < 3 * (ROWS - POS); i += NT16)
+        sm.planes[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
+
+#ifdef GZ_PV_EXP_PRIO
+    if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+    PV_STAMP(30);  // start of the clock (slot 30 is not a phase)
+    for (int b = blockIdx.x; b < count; b += gridDim.x) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        load_planes<NT16>(sm.planes, boards + (size_t)b * 16, tid);
         __syncthreads();
-        // policy_fc 450->225, value_fc1 225->64 (+ReLU)
-        if (tid < POS) {
-            const int o = tid;
-            float acc1 = W[PF_B + o];
-            for (int i = 0; i < 2 * POS; i++) acc1 += W[PF_WT + i * POS + o] * hp[i];
-            lg[o] = acc1;
-        } else if (tid >= 256 && tid < 256 + 64) {
-            const int j = tid - 256;
-            float acc1 = W[V1_B + j];
-            for (int i = 0; i < POS; i++) acc1 += W[V1_WT + i * 64 + j] * hv[i];
-            hh[j] = acc1 > 0.f ? acc1 : 0.f;
-        }
+        PV_STAMP(0);
+        conv0_f16(act, W, sm.planes, wave, lane);
         __syncthreads();
-        // value_fc2 + tanh (wave 0); softmax max/sum over 225 logits (waves 0..3)
-        if (wave == 0) {
-            float part = W[V2_W + lane] * hh[lane];
-            float tot = wave_sum(part) + W[V2_B];
-            if (lane == 0) value[b] = tanhf(tot);
-        }
-        if (wave < 4) {
-            const int o = tid;
-            float x = o < POS ? lg[o] : -3.0e38f;
-            float mx = wave_max(x);
-            if (lane == 0) red[wave] = mx;
-        }
-        __syncthreads();
-        if (wave < 4) {
-            const int o = tid;
-            const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-            float e = o < POS ? __expf(lg[o] - mx) : 0.f;
-            float sm = wave_sum(e);
-            if (lane == 0) red[8 + wave] = sm;
-            if (o < POS) {
-                logits[(size_t)b * POS + o] = lg[o];
-                lg[o] = e;
-            }
-        }
-        __syncthreads();
-        if (wave < 4 && probs) {
-            const int o = tid;
-            const float sm = (red[8] + red[9]) + (red[10] + red[11]);
-            if (o < POS) probs[(size_t)b * POS + o] = lg[o] / sm;
-        }
-        __syncthreads();
+        PV_STAMP(1);
+        if (wave >> 2)
+            f16_tower<7, 8>(act, W, wave, lane);
+        else
+            f16_tower<8, 0>(act, W, wave, lane);
+        heads<NT16>(act, sm, W, b, tid, logits, value, probs);
     }
 }
 
 }  // namespace
+
+#ifdef GZ_PV_STAMPS
+extern "C" int gz_pv_stamps_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_pv_stamps), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pv_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 extern "C" void gz_internal_set_error(const char* msg);
 
@@ -412,7 +872,7 @@ static int pv_grid(int n) {
 
 extern "C" size_t gz_pv_workspace_bytes(int32_t n) {
     int grid = pv_grid(n < 1 ? 1 : n);
-    return (size_t)grid * (NT / 64) * MT * 4 * 64 * sizeof(float);
+    return (size_t)grid * (NT32 / 64) * SLAB_F * sizeof(float);
 }
 
 extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
@@ -426,19 +886,18 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
         gz_internal_set_error("gz_pv_forward: unknown precision");
         return GZ_ERR_ARG;
     }
-    if (precision == GZ_PV_FP32 && !d_workspace) {
-        gz_internal_set_error("gz_pv_forward: fp32 mode needs d_workspace");
+    if (!d_workspace) {
+        gz_internal_set_error("gz_pv_forward: d_workspace is required");
         return GZ_ERR_ARG;
     }
     if (n == 0) return GZ_OK;
     int grid = pv_grid(n);
     hipStream_t s = (hipStream_t)stream;
     if (precision == GZ_PV_FP32)
-        pv_kernel<GZ_PV_FP32><<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs,
-                                                  (float*)d_workspace);
+        pv_kernel_f32<<<grid, NT32, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs,
+                                            (float*)d_workspace);
     else
-        pv_kernel<GZ_PV_F16X3><<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs,
-                                                   nullptr);
+        pv_kernel_f16x3<<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_kernel: ") + hipGetErrorString(e)).c_str());

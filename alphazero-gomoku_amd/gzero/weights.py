@@ -125,7 +125,8 @@ V2_W = V1_B + 64
 V2_B = V2_W + 64
 F16_RES0 = (V2_B + 4 + 3) & ~3  # 16-byte aligned (h8 loads)
 F16_STRIDE = K * CH
-TOTAL = F16_RES0 + 4 * F16_STRIDE
+F16_C0 = F16_RES0 + 4 * F16_STRIDE
+TOTAL = F16_C0 + 8 * 64 * 8
 
 PRECISIONS = {"fp32": 0, "f16x3": 1}  # GZ_PV_FP32, GZ_PV_F16X3
 
@@ -142,6 +143,16 @@ def pack_pv_weights(sd):
     blob[C0_W:C0_W + 27 * CH] = w0.float().numpy().reshape(-1)
     blob[C0_S:C0_S + CH] = s.numpy()
     blob[C0_T:C0_T + CH] = t.numpy()
+    # fp16 conv0 A fragments: [n-tile][lane][8], n = 16*nt + lane%16, k = 8*(lane//16) + j
+    w0p = np.zeros((32, CH), np.float32)
+    w0p[:27] = w0.float().numpy()
+    w0t = w0p.T  # [n][k]
+    h0 = w0t.astype(np.float16)
+    l0 = (w0t - h0.astype(np.float32)).astype(np.float16)
+
+    def frag0(x):  # [n=(nt,li)][k=(q,j)] -> [nt][q][li][j]
+        return x.reshape(8, 16, 4, 8).transpose(0, 2, 1, 3).reshape(-1)
+    blob[F16_C0:F16_C0 + 8 * 64 * 8] = np.concatenate([frag0(h0), frag0(l0)]).view(np.float32)
     convs = []
     for i in range(2):
         convs.append((f"residual_tower.{i}.conv1", f"residual_tower.{i}.bn1"))
@@ -151,11 +162,16 @@ def pack_pv_weights(sd):
         wk = w.permute(2, 3, 1, 0).reshape(K, CH)  # k = (kh*3+kw)*128 + cin
         base = RES0 + j * RES_STRIDE
         blob[base:base + K * CH] = wk.float().numpy().reshape(-1)
-        # fp16x3 copy: W^T[n][k] split into hi = fp16(w), lo = fp16(w - hi)
+        # fp16x3 copy: W^T split into hi = fp16(w), lo = fp16(w - hi), each in
+        # MFMA B-fragment order [ks 36][n-tile 8][lane 64][8 halves] with
+        # n = 16*n_tile + lane%16, k = 32*ks + 8*(lane//16) + j (1 KiB per wave load)
         wt = wk.float().numpy().T.copy()  # [n][k]
         hi = wt.astype(np.float16)
         lo = (wt - hi.astype(np.float32)).astype(np.float16)
-        halves = np.concatenate([hi.reshape(-1), lo.reshape(-1)])
+
+        def frag(x):  # [n=(nt,li)][k=(ks,q,j)] -> [ks][nt][q][li][j]
+            return x.reshape(8, 16, 36, 4, 8).transpose(2, 0, 3, 1, 4).reshape(-1)
+        halves = np.concatenate([frag(hi), frag(lo)])
         fb = F16_RES0 + j * F16_STRIDE
         blob[fb:fb + F16_STRIDE] = halves.view(np.float32)
         blob[base + K * CH:base + K * CH + CH] = s.numpy()
