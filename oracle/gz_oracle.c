@@ -7,6 +7,7 @@
  */
 #include "gz_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -285,6 +286,241 @@ double or_bg_score(const or_board* b, int player) {
     return k >= GZ_TANH_N ? 1.0 : GZ_TANH_TABLE[k];
 }
 
+/* -------------------------------------------------------- BG planner */
+/* KnowledgeSearch._opponent_can_win_next, bg_planner.py:116-125: for every empty
+ * cell (get_valid_moves ignores game_over) a copy with current_player forced to
+ * the opponent tries the move; make_move fails on a finished board, whose copy
+ * then still reports the old game_over / winner. */
+static int opp_can_win_next(const or_board* b, int opp) {
+    for (int i = 0; i < CELLS; i++) {
+        if (b->cell[i]) continue;
+        or_board t = *b;
+        t.player = (int8_t)opp;
+        or_make_move(&t, i / N, i % N);
+        if (t.over && t.winner == opp) return 1;
+    }
+    return 0;
+}
+
+/* KnowledgeSearch.score_move, bg_planner.py:90-106 (the stone placed is the side to move's) */
+double or_ks_score(const or_board* b, int move, int P) {
+    if (move < 0 || move >= CELLS || b->cell[move] != 0 || b->over) return -1e9;
+    or_board t = *b;
+    or_make_move(&t, move / N, move % N);
+    if (t.over && t.winner == P) return 1e6;
+    int opp = (P == 2) ? 1 : 2;
+    if (opp_can_win_next(&t, opp)) return -1e5;
+    double line = (double)or_pattern_score(&t, P);
+    int dr = abs(move / N - 7), dc = abs(move % N - 7);
+    double cb = (6 - (dr + dc)) * 0.5;
+    return line + (cb > 0.0 ? cb : 0.0);
+}
+
+/* top_k_moves, bg_planner.py:108-114: Python's stable sort, descending */
+int or_topk(const or_board* b, int P, int k, int32_t* out) {
+    int L[CELLS];
+    int n = legal_list(b, L);
+    double sc[CELLS];
+    for (int i = 0; i < n; i++) sc[i] = or_ks_score(b, L[i], P);
+    int taken[CELLS] = {0};
+    int m = n < k ? n : k;
+    for (int r = 0; r < m; r++) {
+        int bi = -1;
+        for (int i = 0; i < n; i++)
+            if (!taken[i] && (bi < 0 || sc[i] > sc[bi])) bi = i;
+        taken[bi] = 1;
+        out[r] = L[bi];
+    }
+    return m;
+}
+
+/* BGPlannerAI.get_move, bg_planner.py:232-269, with the nets' p / q given */
+int or_planner_move(const or_board* b, int P, const or_planner_params* pp, const float* p, const float* q,
+                    uint64_t key, uint64_t* draws) {
+    int L[CELLS];
+    int n = legal_list(b, L);
+    if (n == 0) return -1;
+    int32_t top[CELLS];
+    int m = or_topk(b, P, pp->k, top);
+    if (m == 0) return L[choice_idx(key, draws, n)];
+    int best = -1;
+    double bs = -1e18;
+    for (int i = 0; i < m; i++) {
+        double composed = pp->alpha * (double)p[top[i]] - (1 - pp->alpha) * (double)q[top[i]];
+        if (composed > bs) {
+            bs = composed;
+            best = top[i];
+        }
+    }
+    if (to_unit(or_draw(key, (*draws)++)) < pp->explore) return top[choice_idx(key, draws, m)];
+    return best >= 0 ? best : L[choice_idx(key, draws, n)];
+}
+
+/* GraphNet / OpponentDQN in plain fp32 loops (bg_planner.py:22-78).  Offsets of
+ * gzero/planner_nets.py's blob, recomputed here (or_gnet_layout lets the tests
+ * check the two agree). */
+#define GH 64
+#define GDQ 256
+enum { G_K3 = 9 * GH };
+static void gnet_offsets(int32_t* o) {
+    int off = 0;
+    o[0] = off;            /* embed W [28][64] */
+    off += 28 * GH;
+    o[1] = off;            /* embed b */
+    off += GH;
+    for (int i = 0; i < 8; i++) {
+        o[2 + i] = off;    /* layer i W, then bias */
+        off += ((i % 2 == 0) ? G_K3 * GH : GH * GH) + GH;
+    }
+    o[10] = off;           /* policy conv W [2][64] */
+    off += 2 * GH;
+    o[11] = off;           /* policy conv b [2] (+2) */
+    off += 4;
+    o[12] = off;           /* policy fc W^T [450][225] */
+    off += 450 * CELLS;
+    o[13] = off;           /* policy fc b (+3) */
+    off += 228;
+    o[14] = off;           /* dqn fc0 W^T [675][256] */
+    off += 3 * CELLS * GDQ;
+    o[15] = off;
+    off += GDQ;
+    o[16] = off;           /* fc1 W^T [256][256] */
+    off += GDQ * GDQ;
+    o[17] = off;
+    off += GDQ;
+    o[18] = off;           /* fc2 W^T [256][225] */
+    off += GDQ * CELLS;
+    o[19] = off;           /* fc2 b (+3) */
+}
+
+int or_gnet_layout(int32_t* out, int cap) {
+    int32_t o[20];
+    gnet_offsets(o);
+    for (int i = 0; i < 20 && i < cap; i++) out[i] = o[i];
+    return 20;
+}
+
+static void planes_of(const or_board* b, float* x) { /* [3][225]: black, white, empty */
+    for (int i = 0; i < CELLS; i++) {
+        x[i] = b->cell[i] == 1;
+        x[CELLS + i] = b->cell[i] == 2;
+        x[2 * CELLS + i] = b->cell[i] == 0;
+    }
+}
+
+/* 3x3 conv (padding 1) + bias + ReLU; W K-major [tap*cin_n + cin][cout] */
+static void conv3(const float* in, int cin_n, const float* W, const float* bias, float* out) {
+    for (int co = 0; co < GH; co++)
+        for (int pos = 0; pos < CELLS; pos++) {
+            int r = pos / N, c = pos % N;
+            float acc = bias[co];
+            for (int tap = 0; tap < 9; tap++) {
+                int rr = r + tap / 3 - 1, cc = c + tap % 3 - 1;
+                if (rr < 0 || rr >= N || cc < 0 || cc >= N) continue;
+                for (int ci = 0; ci < cin_n; ci++)
+                    acc += in[ci * CELLS + rr * N + cc] * W[(tap * cin_n + ci) * GH + co];
+            }
+            out[co * CELLS + pos] = acc > 0.f ? acc : 0.f;
+        }
+}
+
+void or_gnet_forward(const float* blob, const or_board* b, float* logits, float* p, float* q) {
+    int32_t o[20];
+    gnet_offsets(o);
+    float x[3 * CELLS];
+    planes_of(b, x);
+    float* h = (float*)malloc(sizeof(float) * GH * CELLS);
+    float* g = (float*)malloc(sizeof(float) * GH * CELLS);
+    conv3(x, 3, blob + o[0], blob + o[1], h);
+    for (int i = 0; i < 8; i++) {
+        const float* W = blob + o[2 + i];
+        if (i % 2 == 0) {
+            conv3(h, GH, W, W + G_K3 * GH, g);
+        } else {
+            const float* bias = W + GH * GH;
+            for (int co = 0; co < GH; co++)
+                for (int pos = 0; pos < CELLS; pos++) {
+                    float acc = bias[co];
+                    for (int ci = 0; ci < GH; ci++) acc += h[ci * CELLS + pos] * W[ci * GH + co];
+                    g[co * CELLS + pos] = acc > 0.f ? acc : 0.f;
+                }
+        }
+        float* t = h;
+        h = g;
+        g = t;
+    }
+    float pc[2 * CELLS]; /* policy conv, flattened channel-major (nn.Flatten) */
+    for (int k = 0; k < 2; k++)
+        for (int pos = 0; pos < CELLS; pos++) {
+            float acc = blob[o[11] + k];
+            for (int ci = 0; ci < GH; ci++) acc += blob[o[10] + k * GH + ci] * h[ci * CELLS + pos];
+            pc[k * CELLS + pos] = acc;
+        }
+    float lg[CELLS], mx = -3.0e38f;
+    for (int j = 0; j < CELLS; j++) {
+        float acc = blob[o[13] + j];
+        for (int i = 0; i < 2 * CELLS; i++) acc += blob[o[12] + i * CELLS + j] * pc[i];
+        lg[j] = acc;
+        if (acc > mx) mx = acc;
+    }
+    float sum = 0.f, e[CELLS];
+    for (int j = 0; j < CELLS; j++) {
+        e[j] = expf(lg[j] - mx);
+        sum += e[j];
+    }
+    for (int j = 0; j < CELLS; j++) {
+        if (logits) logits[j] = lg[j];
+        if (p) p[j] = e[j] / sum;
+    }
+    if (q) {
+        float a[GDQ], c[GDQ];
+        for (int j = 0; j < GDQ; j++) {
+            float acc = blob[o[15] + j];
+            for (int i = 0; i < 3 * CELLS; i++) acc += blob[o[14] + i * GDQ + j] * x[i];
+            a[j] = acc > 0.f ? acc : 0.f;
+        }
+        for (int j = 0; j < GDQ; j++) {
+            float acc = blob[o[17] + j];
+            for (int i = 0; i < GDQ; i++) acc += blob[o[16] + i * GDQ + j] * a[i];
+            c[j] = acc > 0.f ? acc : 0.f;
+        }
+        for (int j = 0; j < CELLS; j++) {
+            float acc = blob[o[19] + j];
+            for (int i = 0; i < GDQ; i++) acc += blob[o[18] + i * CELLS + j] * c[i];
+            q[j] = acc;
+        }
+    }
+    free(h);
+    free(g);
+}
+
+/* _simulate, ai_agent.py:251-285: planner plies first, then the offensive policy */
+double or_rollout_planner(const or_board* start, int ai, const or_params* p, int64_t game_id, int32_t sim,
+                          uint64_t key, uint64_t* draws, or_board* final_out) {
+    or_board b = *start;
+    if (!b.over) {
+        int steps = 0;
+        int tmp[CELLS];
+        float pv[CELLS], qv[CELLS];
+        while (!b.over && steps < p->planner_steps) {
+            if (p->pq) p->pq(p->pq_ctx, &b, game_id, sim, steps, pv, qv);
+            else or_gnet_forward(p->gn_blob, &b, NULL, pv, qv);
+            int mv = or_planner_move(&b, ai, &p->planner, pv, qv, key, draws);
+            if (mv < 0) break;
+            or_make_move(&b, mv / N, mv % N);
+            steps++;
+        }
+        while (!b.over && steps < p->max_depth) {
+            if (legal_list(&b, tmp) == 0) break;
+            int mv = or_offensive_move(&b, key, draws);
+            or_make_move(&b, mv / N, mv % N);
+            steps++;
+        }
+    }
+    if (final_out) *final_out = b;
+    return terminal_value(&b, ai);
+}
+
 /* ----------------------------------------------------------------- MCTS */
 typedef struct {
     or_board b;
@@ -384,6 +620,7 @@ static int mcts_search(const or_board* b, int ai, const or_params* p, int64_t ga
         }
         double v; /* _simulate :251-285 */
         if (t.nodes[x].term) v = terminal_value(&t.nodes[x].b, ai);
+        else if (p->planner_steps > 0) v = or_rollout_planner(&t.nodes[x].b, ai, p, game_id, k, key, &dk, NULL);
         else v = or_rollout(&t.nodes[x].b, ai, p->max_depth, key, &dk, NULL);
         sim_draws += (int64_t)dk;
         while (x >= 0) { /* _backpropagate :441-448 */

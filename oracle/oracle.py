@@ -23,11 +23,20 @@ class Board(ctypes.Structure):
         return np.frombuffer(bytes(self.cell), dtype=np.int8).copy()
 
 
+PQ_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Board), ctypes.c_int64, ctypes.c_int32,
+                         ctypes.c_int32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float))
+
+
+class PlannerParams(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("alpha", ctypes.c_double), ("explore", ctypes.c_double)]
+
+
 class Params(ctypes.Structure):
     _fields_ = [("num_simulations", ctypes.c_int32), ("c_puct", ctypes.c_double),
                 ("exploration", ctypes.c_double), ("beta", ctypes.c_double),
                 ("planner_steps", ctypes.c_int32), ("max_depth", ctypes.c_int32),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("planner", PlannerParams),
+                ("gn_blob", ctypes.POINTER(ctypes.c_float)), ("pq", PQ_FN), ("pq_ctx", ctypes.c_void_p)]
 
 
 class TreeInfo(ctypes.Structure):
@@ -42,6 +51,11 @@ DIFFICULTY = {  # ai_agent.py:65-90 (live keys only)
     "easy": {"num_simulations": 100, "c_puct": 1.4, "exploration": 0.2},
     "medium": {"num_simulations": 200, "c_puct": 1.6, "exploration": 0.05},
     "hard": {"num_simulations": 400, "c_puct": 1.8, "exploration": 0.01},
+}
+
+
+PLANNER = {  # BGPlannerAI.params, bg_planner.py:215-219
+    "easy": (8, 0.5, 0.2), "medium": (12, 0.65, 0.1), "hard": (16, 0.75, 0.05),
 }
 
 
@@ -83,6 +97,20 @@ def lib():
         L.or_bg_score.argtypes = [P(Board), ctypes.c_int]
         L.or_get_move.restype = ctypes.c_int
         L.or_get_move.argtypes = [P(Board), ctypes.c_int, P(Params), ctypes.c_int64, P(TreeInfo)]
+        L.or_ks_score.restype = ctypes.c_double
+        L.or_ks_score.argtypes = [P(Board), ctypes.c_int, ctypes.c_int]
+        L.or_topk.restype = ctypes.c_int
+        L.or_topk.argtypes = [P(Board), ctypes.c_int, ctypes.c_int, P(ctypes.c_int32)]
+        L.or_gnet_forward.argtypes = [P(ctypes.c_float), P(Board), P(ctypes.c_float), P(ctypes.c_float),
+                                      P(ctypes.c_float)]
+        L.or_gnet_layout.restype = ctypes.c_int
+        L.or_gnet_layout.argtypes = [P(ctypes.c_int32), ctypes.c_int]
+        L.or_planner_move.restype = ctypes.c_int
+        L.or_planner_move.argtypes = [P(Board), ctypes.c_int, P(PlannerParams), P(ctypes.c_float),
+                                      P(ctypes.c_float), ctypes.c_uint64, P(ctypes.c_uint64)]
+        L.or_rollout_planner.restype = ctypes.c_double
+        L.or_rollout_planner.argtypes = [P(Board), ctypes.c_int, P(Params), ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.c_uint64, P(ctypes.c_uint64), P(Board)]
         L.or_play_game.restype = ctypes.c_int
         L.or_play_game.argtypes = [P(Params), P(Params), ctypes.c_int64, P(ctypes.c_int8),
                                    P(ctypes.c_int32), P(ctypes.c_int8), P(ctypes.c_int8), ctypes.c_int,
@@ -100,10 +128,74 @@ def new_board(moves=()):
     return b
 
 
-def make_params(difficulty="medium", sims=None, beta=0.2, seed=0, max_depth=100, planner_steps=0):
+def make_params(difficulty="medium", sims=None, beta=0.2, seed=0, max_depth=100, planner_steps=0,
+                gn_blob=None, pq=None):
+    """gn_blob: float32 numpy blob of gzero.planner_nets (kept alive on the Params);
+    pq: python callable (board, game_id, sim, step) -> (p[225], q[225]) overriding the nets."""
     d = DIFFICULTY[difficulty]
-    return Params(d["num_simulations"] if sims is None else sims, d["c_puct"], d["exploration"],
-                  float(beta), planner_steps, max_depth, seed)
+    k, a, e = PLANNER.get(difficulty, PLANNER["medium"])
+    prm = Params(d["num_simulations"] if sims is None else sims, d["c_puct"], d["exploration"],
+                 float(beta), planner_steps, max_depth, seed, PlannerParams(k, a, e))
+    if gn_blob is not None:
+        arr = np.ascontiguousarray(gn_blob, np.float32)
+        prm._gn_keep = arr
+        prm.gn_blob = arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    if pq is not None:
+        def cb(ctx, bptr, game_id, sim, step, pp, qq):
+            pv, qv = pq(bptr.contents, game_id, sim, step)
+            ctypes.memmove(pp, np.ascontiguousarray(pv, np.float32).ctypes.data, 225 * 4)
+            ctypes.memmove(qq, np.ascontiguousarray(qv, np.float32).ctypes.data, 225 * 4)
+        prm._pq_keep = PQ_FN(cb)
+        prm.pq = prm._pq_keep
+    return prm
+
+
+def planner_params(difficulty):
+    return PlannerParams(*PLANNER.get(difficulty, PLANNER["medium"]))
+
+
+def ks_score(b, move, P):
+    return lib().or_ks_score(ctypes.byref(b), move, P)
+
+
+def topk(b, P, k):
+    out = (ctypes.c_int32 * 225)()
+    n = lib().or_topk(ctypes.byref(b), P, k, out)
+    return list(out[:n])
+
+
+def gnet_forward(blob, b):
+    arr = np.ascontiguousarray(blob, np.float32)
+    lg = np.zeros(225, np.float32)
+    p = np.zeros(225, np.float32)
+    q = np.zeros(225, np.float32)
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    lib().or_gnet_forward(fp(arr), ctypes.byref(b), fp(lg), fp(p), fp(q))
+    return lg, p, q
+
+
+def gnet_layout():
+    out = (ctypes.c_int32 * 32)()
+    n = lib().or_gnet_layout(out, 32)
+    return list(out[:n])
+
+
+def planner_move(b, P, difficulty, p, q, key):
+    d = ctypes.c_uint64(0)
+    pa = np.ascontiguousarray(p, np.float32)
+    qa = np.ascontiguousarray(q, np.float32)
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    pp = planner_params(difficulty)
+    mv = lib().or_planner_move(ctypes.byref(b), P, ctypes.byref(pp), fp(pa), fp(qa), key, ctypes.byref(d))
+    return mv, d.value
+
+
+def rollout_planner(b, ai_player, params, game_id, sim, key):
+    d = ctypes.c_uint64(0)
+    fb = Board()
+    v = lib().or_rollout_planner(ctypes.byref(b), ai_player, ctypes.byref(params), game_id, sim, key,
+                                 ctypes.byref(d), ctypes.byref(fb))
+    return v, d.value, fb
 
 
 def legal_mask_int(b):

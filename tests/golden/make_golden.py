@@ -653,9 +653,228 @@ def part_games():
     dump("games", {"seed": SEED, "games": out})
 
 
+# ---------------------------------------------------------------------------
+# G5 BG planner: GraphNet / OpponentDQN, knowledge search, planner moves,
+# planner-guided searches (bg_planner.py:22-269, ai_agent.py:251-285)
+# ---------------------------------------------------------------------------
+
+GN_SEED, DQN_SEED = 21, 22
+
+
+def _f32hex(a):
+    import numpy as np
+    return [format(int(x), "08x") for x in np.asarray(a, np.float32).view(np.uint32)]
+
+
+def _planner_weights(h):
+    if not hasattr(h, "planner_sd"):
+        from gzero import planner_nets
+        h.planner_sd = (planner_nets.init_graphnet_state(GN_SEED), planner_nets.init_dqn_state(DQN_SEED))
+    return h.planner_sd
+
+
+def _load_planner(h, planner):
+    gsd, dsd = _planner_weights(h)
+    planner.graph_net.load_state_dict(gsd)
+    planner.opp_dqn.load_state_dict(dsd)
+    planner.graph_net.eval()
+    planner.opp_dqn.eval()
+
+
+def _pq(h, planner, b):
+    import torch
+    planes = planner._board_to_planes(b.get_board_state())
+    x = torch.from_numpy(planes).unsqueeze(0)
+    with torch.no_grad():
+        p = torch.softmax(planner.graph_net(x).squeeze(0), dim=0).numpy()
+        q = planner.opp_dqn(x).squeeze(0).numpy()
+    return p, q
+
+
+def _install_planner_capture(h):
+    """Wrap BGPlannerAI.get_move: record board, top-k, p/q at the top-k cells and the move."""
+    if getattr(h, "planner_capture_installed", False):
+        return
+    B = h.bg.BGPlannerAI
+    orig = B.get_move
+    h.planner_calls = None
+
+    def get_move(self, board):
+        if h.planner_calls is None:
+            return orig(self, board)
+        top = self.k_search.top_k_moves(board, self.player, k=self.params["k"])
+        p, q = _pq(h, self, board)
+        idx = [r * N + c for r, c in top]
+        key = (h.rs.game_id, h.rs.ply, h.rs.sim)
+        before = h.rs.count(*key)
+        mv = orig(self, board)
+        h.planner_calls.append({"sim": h.rs.sim, "board": board_str(board), "n": len(board.move_history),
+                                "mover": board.current_player, "top": idx,
+                                "p": _f32hex(p[idx]), "q": _f32hex(q[idx]),
+                                "move": None if mv is None else mv[0] * N + mv[1],
+                                "draws": h.rs.count(*key) - before})
+        return mv
+
+    B.get_move = get_move
+    h.planner_capture_installed = True
+
+
+def part_gnet():
+    import base64
+    import random as pyrandom
+    import numpy as np
+    import torch
+    h = ref()
+    gsd, dsd = _planner_weights(h)
+    planner = h.bg.BGPlannerAI(1, "medium", device="cpu")
+    _load_planner(h, planner)
+    rng = pyrandom.Random(23)
+    cases, lg_all, p_all, q_all = [], [], [], []
+    for i in range(64):
+        L = rng.randint(0, 160)
+        mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.5) if L else []
+        b = replay(h, mv)
+        planes = planner._board_to_planes(b.get_board_state())
+        x = torch.from_numpy(planes).unsqueeze(0)
+        with torch.no_grad():
+            lg = planner.graph_net(x).squeeze(0).numpy()
+        p, q = _pq(h, planner, b)
+        cases.append({"moves": mv})
+        lg_all.append(lg)
+        p_all.append(p)
+        q_all.append(q)
+    enc = lambda a: base64.b64encode(np.ascontiguousarray(a, np.float32).tobytes()).decode()
+    dump("gnet", {"gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": cases, "logits_f32_b64": enc(np.stack(lg_all)),
+                  "p_f32_b64": enc(np.stack(p_all)), "q_f32_b64": enc(np.stack(q_all))})
+
+
+def _threat_position(rng):
+    """A position where some side has an open or closed four (so the 1e6 / -1e5 scores occur)."""
+    for _ in range(200):
+        L = rng.randint(10, 120)
+        mv = gen_moves(rng, L, avoid_five=True, near=True)
+        cells = [0] * 225
+        p = 1
+        for m in mv:
+            cells[m] = p
+            p = 3 - p
+        threat = any(cells[i] == 0 and (_wins(cells, i // N, i % N, 1) or _wins(cells, i // N, i % N, 2))
+                     for i in range(225))
+        if threat:
+            return mv
+    return mv
+
+
+def _planner_task(args):
+    idx, moves, P, difficulty, full = args
+    h = ref()
+    _install_planner_capture(h)
+    key = ("planner", P, difficulty)
+    if not hasattr(h, "planners"):
+        h.planners = {}
+    if key not in h.planners:
+        pl = h.bg.BGPlannerAI(P, difficulty, device="cpu")
+        _load_planner(h, pl)
+        h.planners[key] = pl
+    pl = h.planners[key]
+    b = replay(h, moves)
+    res = {"moves": moves, "P": P, "difficulty": difficulty}
+    if full:
+        res["scores"] = [pl.k_search.score_move(b, (r, c), P) for r, c in b.get_valid_moves()]
+    h.planner_calls = []
+    h.rs.set(game_id=idx, ply=len(moves), sim=1)
+    mv = pl.get_move(b)
+    call = h.planner_calls[0]
+    h.planner_calls = None
+    res.update({"top": call["top"], "p": call["p"], "q": call["q"], "move": None if mv is None else mv[0] * N + mv[1],
+                "draws": call["draws"], "game_id": idx})
+    return res
+
+
+def part_planner():
+    import random as pyrandom
+    rng = pyrandom.Random(29)
+    tasks = []
+    for i in range(360):
+        kind = i % 6
+        if kind == 0:
+            mv = gen_moves(rng, rng.randint(0, 8), avoid_five=True)
+        elif kind in (1, 2):
+            mv = _threat_position(rng)
+        elif kind == 3:
+            mv = gen_moves(rng, rng.randint(20, 120), avoid_five=True, near=True)
+        elif kind == 4:
+            mv = gen_moves(rng, rng.randint(120, 190), avoid_five=True, near=rng.random() < 0.5)
+        else:
+            mv = gen_moves(rng, rng.choice([197, 198, 199]), avoid_five=True)
+        P = rng.choice([1, 2])
+        diff = ["easy", "medium", "hard"][i % 3]
+        tasks.append((5000 + i, mv, P, diff, i % 2 == 0))
+    with Pool(8) as pool:
+        out = pool.map(_planner_task, tasks, chunksize=4)
+    dump("planner", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
+
+
+def _planner_mcts_task(args):
+    idx, moves, sims, beta, difficulty, steps = args
+    h = ref()
+    _install_planner_capture(h)
+    b = replay(h, moves)
+    player = b.current_player
+    ai = h.ai.AlphaZeroGomokuAI(player, difficulty, device="cpu", beta=beta, planner_steps=steps,
+                                time_limit=float("inf"))
+    _load_planner(h, ai.bg_planner)
+    ai.params["num_simulations"] = sims
+    h.rs.set(game_id=idx)
+    h.last_root = None
+    h.predicts = 0
+    h.planner_calls = []
+    t0 = time.time()
+    mv = ai.get_move(b)
+    dt = time.time() - t0
+    calls = h.planner_calls
+    h.planner_calls = None
+    root = h.last_root
+    ply = len(moves)
+    res = {"moves": moves, "sims": sims, "beta": beta, "difficulty": difficulty, "planner_steps": steps,
+           "game_id": idx, "move": None if mv is None else mv[0] * N + mv[1],
+           "predicts": h.predicts, "main_draws": h.rs.count(idx, ply, 0),
+           "sim_draws": [h.rs.count(idx, ply, k) for k in range(1, sims + 1)], "seconds": dt, "calls": calls}
+    if root is not None and len(moves) >= 6:
+        res["root_visits"] = root.visits
+        res["root_value"] = root.value
+        res["children"] = [[c.move[0] * N + c.move[1], c.visits, c.value] for c in root.children]
+    return res
+
+
+def part_planner_mcts():
+    import random as pyrandom
+    rng = pyrandom.Random(31)
+    tasks = []
+    i = 7000
+    for k in range(6):  # parallel phase only
+        L = rng.randint(8, 60)
+        tasks.append((i, gen_moves(rng, L, True, True), rng.choice([4, 6, 8]), [0.0, 0.2][k % 2],
+                      ["medium", "easy", "hard"][k % 3], [5, 2][k % 2])); i += 1
+    for k in range(10):  # sequential phase: late positions
+        L = rng.randint(175, 196)
+        legal = 225 - L
+        tasks.append((i, gen_moves(rng, L, True, rng.random() < 0.5), legal + 1 + rng.randint(2, 8),
+                      [0.0, 0.2][k % 2], ["medium", "easy", "hard"][k % 3], [5, 3][k % 2])); i += 1
+    for k in range(4):  # quiet mid-game, some sequential sims
+        L = rng.randint(150, 170)
+        legal = 225 - L
+        tasks.append((i, gen_quiet(rng, L), legal + 1 + rng.randint(1, 4), 0.2, "medium", 5)); i += 1
+    tasks.sort(key=lambda t: -t[2] * t[5] * (225 - len(t[1])))
+    with Pool(8) as pool:
+        out = pool.map(_planner_mcts_task, tasks, chunksize=1)
+    out.sort(key=lambda r: r["game_id"])
+    dump("planner_mcts", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
+
+
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
          "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "augment": part_augment,
-         "games": part_games}
+         "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(PARTS)

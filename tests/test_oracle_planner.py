@@ -1,0 +1,146 @@
+"""The C restatement of the BG planner (oracle/gz_oracle.c) against the reference's
+own outputs (tests/golden/{gnet,planner,planner_mcts}.json.gz, made by
+tests/golden/make_golden.py from bg_planner.py / ai_agent.py).
+
+Integer / fp64 parts (knowledge-search scores, top-k order, the composed
+argmax, RNG draws, the search tree) are compared exactly; the nets' fp32 outputs
+within tolerance.  Where the planner's move depends on the nets, the reference's
+recorded p / q (at the top-k cells) are injected, so that the rest of the search
+is compared bit for bit.
+"""
+import base64
+
+import numpy as np
+import pytest
+
+from conftest import golden
+import oracle as O
+from gzero import planner_nets
+
+N = 15
+
+
+def _dec(s, shape):
+    return np.frombuffer(base64.b64decode(s), dtype=np.float32).reshape(shape)
+
+
+def _hexf(hs):
+    return np.array([int(h, 16) for h in hs], dtype=np.uint32).view(np.float32)
+
+
+@pytest.fixture(scope="module")
+def gn():
+    g = golden("gnet")
+    gsd = planner_nets.init_graphnet_state(g["gn_seed"])
+    dsd = planner_nets.init_dqn_state(g["dqn_seed"])
+    return g, gsd, dsd, planner_nets.pack_planner_weights(gsd, dsd)
+
+
+def test_layout_matches_packer():
+    lay = O.gnet_layout()
+    P = planner_nets
+    want = [P.GE_W, P.GE_B] + [P._layer_off(i) for i in range(8)] + [
+        P.GP_W, P.GP_B, P.GF_WT, P.GF_B, P.D0_WT, P.D0_B, P.D1_WT, P.D1_B, P.D2_WT, P.D2_B]
+    assert lay == want
+
+
+def test_torch_modules_match_reference(gn):
+    """gzero.planner_nets.GraphNet/OpponentDQN (same names, same init) reproduce the reference modules."""
+    g, gsd, dsd, _ = gn
+    n = len(g["cases"])
+    planes = np.zeros((n, 3, N, N), np.float32)
+    for i, c in enumerate(g["cases"]):
+        cells = np.zeros(225, np.int8)
+        p = 1
+        for m in c["moves"]:
+            cells[m] = p
+            p = 3 - p
+        planes[i, 0] = (cells == 1).reshape(N, N)
+        planes[i, 1] = (cells == 2).reshape(N, N)
+        planes[i, 2] = (cells == 0).reshape(N, N)
+    lg, p, q = planner_nets.reference_forward(gsd, dsd, planes)
+    np.testing.assert_allclose(lg, _dec(g["logits_f32_b64"], (n, 225)), rtol=0, atol=1e-5)
+    np.testing.assert_allclose(p, _dec(g["p_f32_b64"], (n, 225)), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(q, _dec(g["q_f32_b64"], (n, 225)), rtol=0, atol=1e-5)
+
+
+def test_oracle_nets_vs_reference(gn):
+    g, _, _, blob = gn
+    n = len(g["cases"])
+    lg_ref = _dec(g["logits_f32_b64"], (n, 225))
+    p_ref = _dec(g["p_f32_b64"], (n, 225))
+    q_ref = _dec(g["q_f32_b64"], (n, 225))
+    for i, c in enumerate(g["cases"][:16]):
+        b = O.new_board(c["moves"])
+        lg, p, q = O.gnet_forward(blob, b)
+        np.testing.assert_allclose(lg, lg_ref[i], rtol=0, atol=1e-4)
+        np.testing.assert_allclose(p, p_ref[i], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(q, q_ref[i], rtol=0, atol=1e-4)
+
+
+def test_knowledge_scores_and_topk():
+    g = golden("planner")
+    checked = 0
+    for c in g["cases"]:
+        b = O.new_board(c["moves"])
+        k = O.PLANNER[c["difficulty"]][0]
+        assert O.topk(b, c["P"], k) == c["top"], c["moves"]
+        if c.get("scores"):
+            legal = [i for i in range(225) if b.cell[i] == 0]
+            got = [O.ks_score(b, m, c["P"]) for m in legal]
+            assert got == c["scores"]
+            checked += 1
+    assert checked >= 150
+
+
+def test_planner_move_with_reference_nets():
+    g = golden("planner")
+    for c in g["cases"]:
+        b = O.new_board(c["moves"])
+        p = np.zeros(225, np.float32)
+        q = np.zeros(225, np.float32)
+        p[c["top"]] = _hexf(c["p"])
+        q[c["top"]] = _hexf(c["q"])
+        key = O.lib().or_stream_key(g["seed"], c["game_id"], len(c["moves"]), 1)
+        mv, draws = O.planner_move(b, c["P"], c["difficulty"], p, q, key)
+        assert mv == c["move"] and draws == c["draws"], (c["game_id"], mv, c["move"])
+
+
+def _board_str(b):
+    return "".join(str(int(v)) for v in b.cells())
+
+
+@pytest.mark.parametrize("idx", range(20))
+def test_planner_search_vs_reference(idx):
+    g = golden("planner_mcts")
+    c = g["cases"][idx]
+    steps = {}
+    seen = {}
+    for call in c["calls"]:
+        s = call["sim"]
+        t = seen.get(s, 0)
+        seen[s] = t + 1
+        steps[(s, t)] = call
+
+    def pq(board, game_id, sim, step):
+        call = steps[(sim, step)]
+        assert _board_str(board) == call["board"], (sim, step)
+        p = np.zeros(225, np.float32)
+        q = np.zeros(225, np.float32)
+        p[call["top"]] = _hexf(call["p"])
+        q[call["top"]] = _hexf(call["q"])
+        return p, q
+
+    b = O.new_board(c["moves"])
+    prm = O.make_params(c["difficulty"], sims=c["sims"], beta=c["beta"], seed=g["seed"],
+                        planner_steps=c["planner_steps"], pq=pq)
+    mv, tree = O.get_move(b, b.player, prm, c["game_id"])
+    assert mv == c["move"]
+    assert tree["main_draws"] == c["main_draws"]
+    assert tree["sim_draws"] == sum(c["sim_draws"])
+    if "children" in c:
+        assert tree["visits"][0] == c["root_visits"]
+        assert tree["value"][0] == c["root_value"]
+        kids = [[tree["move"][i], tree["visits"][i], tree["value"][i]]
+                for i in range(len(tree["parent"])) if tree["parent"][i] == 0]
+        assert kids == c["children"]
