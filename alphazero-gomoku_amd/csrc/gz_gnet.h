@@ -1,0 +1,48 @@
+// gz_gnet.h -- packed weight layout of the BG planner's GraphNet + OpponentDQN
+// (bg_planner.py:22-78), produced by gzero/planner_nets.py:pack_planner_weights().
+//
+// fp32 section (K-major like gz_pvnet.h; the C oracle reads it too):
+//   embed W [28][64] (k = tap*3 + cin, row 27 zero), b [64]
+//   layers 0..7: W then b; even = 3x3 [576][64] (k = tap*64 + cin), odd = 1x1 [64][64]
+//   policy conv W [2][64], b [2](+2); policy fc W^T [450][225], b [225](+3)
+//   dqn fc0 W^T [675][256], b; fc1 W^T [256][256], b; fc2 W^T [256][225], b (+3)
+// fp16 section: embed A fragments hi/lo [4][64][8]; per layer hi then lo in
+// v_mfma_f32_16x16x32_f16 A-fragment order [ks][n-tile 4][lane 64][8]
+// (n = 16*n_tile + lane%16, k = 32*ks + 8*(lane/16) + j).
+#pragma once
+
+namespace gzgn {
+constexpr int HID = 64;
+constexpr int DQH = 256;
+constexpr int POS = 225;
+constexpr int K3 = 9 * HID;
+
+constexpr int GE_W = 0;
+constexpr int GE_B = GE_W + 28 * HID;
+constexpr int GL0 = GE_B + HID;
+constexpr int layer_off(int i) {
+    int off = GL0;
+    for (int j = 0; j < i; j++) off += ((j % 2 == 0) ? K3 * HID : HID * HID) + HID;
+    return off;
+}
+constexpr int layer_bias(int i) { return layer_off(i) + ((i % 2 == 0) ? K3 * HID : HID * HID); }
+constexpr int GP_W = layer_off(8);
+constexpr int GP_B = GP_W + 2 * HID;
+constexpr int GF_WT = GP_B + 4;
+constexpr int GF_B = GF_WT + 450 * POS;
+constexpr int D0_WT = GF_B + 228;
+constexpr int D0_B = D0_WT + 3 * POS * DQH;
+constexpr int D1_WT = D0_B + DQH;
+constexpr int D1_B = D1_WT + DQH * DQH;
+constexpr int D2_WT = D1_B + DQH;
+constexpr int D2_B = D2_WT + DQH * POS;
+constexpr int GH_E = (D2_B + 228 + 3) & ~3;
+constexpr int GH_L0 = GH_E + 4 * 64 * 8;
+constexpr int KS3 = 18, KS1 = 2;
+constexpr int h_layer_off(int i) {
+    int off = GH_L0;
+    for (int j = 0; j < i; j++) off += ((j % 2 == 0) ? KS3 : KS1) * 4 * 64 * 8;
+    return off;
+}
+constexpr int TOTAL = h_layer_off(8);
+}  // namespace gzgn

@@ -1,0 +1,258 @@
+// gz_gnet.hip -- the BG planner's nets for a batch of boards on gfx950:
+//   p = softmax(GraphNet(planes)), q = OpponentDQN(planes)   (bg_planner.py:22-78,243-250)
+//
+// One 512-thread workgroup (8 waves) evaluates one board at a time and loops over
+// boards; two workgroups share a CU (LDS 76 KB each).  GraphNet's 64x225 map
+// stays in LDS as f16x3 hi/lo planes (gz_f16conv.h); every conv is an implicit
+// GEMM on v_mfma_f32_16x16x32_f16 in C^T form.  Wave w owns n-tiles
+// {2(w&1), 2(w&1)+1} x M tiles [4(w>>1), 4(w>>1)+4) (tile 15 = zero rows, unused).
+// The embed conv reads 0/1 planes, exact in fp16, so it takes 2 MFMAs (w_hi, w_lo).
+// Heads (policy conv 1x1, FC 450->225, softmax) and the DQN MLP run on VALU.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "gz_f16conv.h"
+#include "gz_gnet.h"
+#include "../../include/gzero.h"
+
+using namespace gzc;
+using namespace gzgn;
+
+namespace {
+
+constexpr int NT = 512;
+constexpr int NM = 4;        // M tiles per wave
+constexpr int PROWS = 240;   // fp32 planes [3][240]
+constexpr int ACT_BYTES = 2 * HID * ROWS16 * 2;  // 65536
+constexpr int SMALL_F = 3 * PROWS + 2 * POS + 256 + 2 * 256 + 32 + 2 * DQH + 2 * DQH;
+constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
+
+// neighbour of the lane's position in M tile m for tap (dr, dc); POS (a zero plane slot) if off-board
+__device__ inline int pnbr(int m, int li, int dr, int dc) {
+    int pos = m * 16 + li;
+    int r = pos / 15 + dr, c = pos % 15 + dc;
+    bool ok = pos < POS && r >= 0 && r < 15 && c >= 0 && c < 15;
+    return ok ? r * 15 + c : POS;
+}
+
+// epilogue: y = relu(acc + bias) for the wave's 2 n-tiles x NM M tiles
+__device__ __forceinline__ void gn_store(ActF16x3& act, const f32x4 (&acc)[2][NM], const float* __restrict__ bias,
+                                         int np, int m0, int lane) {
+    asm volatile("" : "+v"(lane));
+    lane &= 63;
+    const f32x4 one = {1.f, 1.f, 1.f, 1.f};
+    const f32x4 none = zero4();
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 t = *(const f32x4*)(bias + ch0);
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = (m0 + m) * 16 + (lane & 15);
+            if (pos < POS) f16_put4<false>(act, acc[n][m], one, t, none, ch0, pos);
+        }
+    }
+}
+
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void gn_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards,
+                                                   int n, const int32_t* d_count, float* __restrict__ p_out,
+                                                   float* __restrict__ q_out, float* __restrict__ logits_out) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    ActF16x3 act;
+    act.hi = (_Float16*)lds;
+    act.lo = act.hi + HID * ROWS16;
+    float* planes = (float*)(lds + ACT_BYTES);  // [3][240]
+    float* pc = planes + 3 * PROWS;             // [450] policy conv output, channel-major
+    float* lg = pc + 2 * POS;                   // [256]
+    float* part = lg + 256;                     // [2][256]
+    float* red = part + 2 * 256;                // [32]
+    float* da = red + 32;                       // [2][256] dqn partial sums / activations
+    float* dc = da + 2 * DQH;                   // [2][256]
+
+    int count = n;
+    if (d_count) {
+        int c = *d_count;
+        count = c < n ? c : n;
+    }
+    act.zero_slots(threadIdx.x, NT, HID);
+    for (int i = threadIdx.x; i < 3 * (PROWS - POS); i += NT)
+        planes[(i / (PROWS - POS)) * PROWS + POS + i % (PROWS - POS)] = 0.f;
+
+    for (int b = blockIdx.x; b < count; b += gridDim.x) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int np = wave & 1, m0 = (wave >> 1) * NM;
+        // ---- input planes [black, white, empty] (bg_planner.py:225-230)
+        const uint32_t* bd = boards + (size_t)b * 16;
+        for (int p = tid; p < POS; p += NT) {
+            int bit = (p / 15) * 16 + (p % 15);
+            uint32_t bl = (bd[bit >> 5] >> (bit & 31)) & 1u;
+            uint32_t wh = (bd[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+            planes[p] = (float)bl;
+            planes[PROWS + p] = (float)wh;
+            planes[2 * PROWS + p] = (float)(1u - (bl | wh));
+        }
+        __syncthreads();
+
+        // ---- OpponentDQN (bg_planner.py:68-78): fc0 over the 225 one-hot inputs that are 1
+        {
+            const int j = tid & 255, h = tid >> 8;
+            float acc = 0.f;
+            for (int pos = h; pos < POS; pos += 2) {
+                const int plane = planes[pos] != 0.f ? 0 : (planes[PROWS + pos] != 0.f ? 1 : 2);
+                acc += W[D0_WT + (size_t)(plane * POS + pos) * DQH + j];
+            }
+            da[h * DQH + j] = acc;
+        }
+        __syncthreads();
+        if (tid < DQH) {
+            float a = W[D0_B + tid] + (da[tid] + da[DQH + tid]);
+            dc[tid] = a > 0.f ? a : 0.f;
+        }
+        __syncthreads();
+        {  // fc1 256->256 in two input halves
+            const int j = tid & 255, h = tid >> 8;
+            da[h * DQH + j] = dot_col<128, 32>(W + D1_WT + (size_t)(h * 128) * DQH + j, DQH, dc + h * 128);
+        }
+        __syncthreads();
+        if (tid < DQH) {
+            float a = W[D1_B + tid] + (da[tid] + da[DQH + tid]);
+            dc[DQH + tid] = a > 0.f ? a : 0.f;
+        }
+        __syncthreads();
+        {  // fc2 256->225 in two input halves
+            const int j = tid & 255, h = tid >> 8;
+            if (j < POS) da[h * DQH + j] = dot_col<128, 32>(W + D2_WT + (size_t)(h * 128) * POS + j, POS, dc + DQH + h * 128);
+        }
+        __syncthreads();
+        if (tid < POS) q_out[(size_t)b * POS + tid] = W[D2_B + tid] + (da[tid] + da[DQH + tid]);
+
+        // ---- embed conv 3->64 (K = 27 -> 32): planes are 0/1, so a*w = a*w_hi + a*w_lo
+        {
+            const int li = lane & 15, q = lane >> 4;
+            f32x4 acc[2][NM];
+            h8 wa[2][2];
+#pragma unroll
+            for (int nn = 0; nn < 2; nn++) {
+                const _Float16* wf = (const _Float16*)(W + GH_E) + ((size_t)(2 * np + nn) * 64 + lane) * 8;
+                wa[nn][0] = *(const h8*)wf;
+                wa[nn][1] = *(const h8*)(wf + 4 * 64 * 8);
+            }
+            int lv = li;
+            asm volatile("" : "+v"(lv));
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                h8 a;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int k = 8 * q + j;
+                    const int tap = k / 3, cin = k % 3;
+                    const int idx = k < 27 ? pnbr(m0 + m, lv, tap / 3 - 1, tap % 3 - 1) : POS;
+                    a[j] = (_Float16)planes[(k < 27 ? cin : 0) * PROWS + idx];
+                }
+#pragma unroll
+                for (int nn = 0; nn < 2; nn++) {
+                    acc[nn][m] = zero4();
+                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][0], a, acc[nn][m], 0, 0, 0);
+                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][1], a, acc[nn][m], 0, 0, 0);
+                }
+            }
+            gn_store(act, acc, W + GE_B, np, m0, lane);
+        }
+        __syncthreads();
+
+        // ---- 4 x [conv3x3 + ReLU, conv1x1 + ReLU] (bg_planner.py:50-54)
+        for (int i = 0; i < 8; i++) {
+            f32x4 acc[2][NM];
+#pragma unroll
+            for (int nn = 0; nn < 2; nn++)
+#pragma unroll
+                for (int m = 0; m < NM; m++) acc[nn][m] = zero4();
+            const _Float16* wf = (const _Float16*)(W + h_layer_off(i));
+            if (i % 2 == 0)
+                f16_conv<NM, 2, 4, 9>(act, wf, np, m0, lane, acc);
+            else
+                f16_conv<NM, 2, 4, 1>(act, wf, np, m0, lane, acc);
+            __syncthreads();  // every wave has read the layer input
+            gn_store(act, acc, W + layer_bias(i), np, m0, lane);
+            __syncthreads();
+        }
+
+        // ---- policy head: conv1x1 64->2 (one thread per position), flatten channel-major
+        if (tid < POS) {
+            float p0 = W[GP_B], p1 = W[GP_B + 1];
+            for (int c0 = 0; c0 < HID; c0 += 8) {
+                float a[8];
+                act.get8(c0, tid, a);
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    p0 += W[GP_W + c0 + j] * a[j];
+                    p1 += W[GP_W + HID + c0 + j] * a[j];
+                }
+            }
+            pc[tid] = p0;
+            pc[POS + tid] = p1;
+        }
+        __syncthreads();
+        {  // Linear 450->225 in two input halves
+            const int o = tid & 255, h = tid >> 8;
+            if (o < POS) part[h * 256 + o] = dot_col<POS, 45>(W + GF_WT + (size_t)h * POS * POS + o, POS, pc + h * POS);
+        }
+        __syncthreads();
+        if (tid < POS) lg[tid] = W[GF_B + tid] + (part[tid] + part[256 + tid]);
+        __syncthreads();
+        // ---- softmax over 225 logits (waves 0..3), torch.softmax(dim=0) semantics in fp32
+        if (wave < 4) {
+            float x = tid < POS ? lg[tid] : -3.0e38f;
+            float mx = wave_max(x);
+            if (lane == 0) red[wave] = mx;
+        }
+        __syncthreads();
+        if (wave < 4) {
+            const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+            float e = tid < POS ? __expf(lg[tid] - mx) : 0.f;
+            float s = wave_sum(e);
+            if (lane == 0) red[8 + wave] = s;
+            if (tid < POS) {
+                if (logits_out) logits_out[(size_t)b * POS + tid] = lg[tid];
+                lg[tid] = e;
+            }
+        }
+        __syncthreads();
+        if (wave < 4) {
+            const float s = (red[8] + red[9]) + (red[10] + red[11]);
+            if (tid < POS) p_out[(size_t)b * POS + tid] = lg[tid] / s;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" void gz_internal_set_error(const char* msg);
+
+extern "C" size_t gz_gn_weight_floats(void) { return (size_t)TOTAL; }
+
+extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
+                             float* d_p, float* d_q, float* d_logits, void* stream) {
+    if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_p || !d_q))) {
+        gz_internal_set_error("gz_gn_forward: bad arguments");
+        return GZ_ERR_ARG;
+    }
+    if (n == 0) return GZ_OK;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    }
+    int grid = n < 2 * cus ? n : 2 * cus;
+    gn_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(d_weights, d_boards, n, d_count, d_p, d_q, d_logits);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string("gn_kernel: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}

@@ -24,6 +24,7 @@
 
 #include <string>
 
+#include "gz_f16conv.h"
 #include "gz_pvnet.h"
 #include "../../include/gzero.h"
 
@@ -31,8 +32,7 @@ using namespace gzpv;
 
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+using namespace gzc;
 
 constexpr int MT = 15;     // 16-position M tiles (240 >= 225)
 constexpr int ROWS = 240;  // positions incl. 15 zero rows / slots
@@ -44,10 +44,6 @@ constexpr int ACT_BYTES_F32 = CH * ROWS * 4;      // 122880
 constexpr int ACT_BYTES_F16 = 2 * CH * 256 * 2;  // 131072: hi + lo planes of 256 rows
 constexpr int ACT_BYTES = ACT_BYTES_F16 > ACT_BYTES_F32 ? ACT_BYTES_F16 : ACT_BYTES_F32;
 
-__device__ inline f32x4 zero4() {
-    f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    return z;
-}
 
 // Phase stamps (tools/pv_stamps.py only): -DGZ_PV_STAMPS accumulates s_memtime
 // deltas of workgroup 0 / wave 0 per phase; compiled out otherwise.
@@ -141,287 +137,7 @@ struct ActF32 {
     }
 };
 
-// ============================================================ fp16x3 policy
-// Activations as hi/lo fp16 planes [CG][ROWS16][8]: channel group cg = ch/8 holds
-// 16 B per position, so the 16 lanes of a ds_read_b128 bank group read 16
-// consecutive positions = 16 distinct 16-B bank slots.  Rows 225..255 are zero;
-// an off-board neighbour with virtual index v reads zero row 225 + ((v-225) mod 16),
-// which keeps its bank slot = v mod 16, so no tap or board edge conflicts.
-constexpr int CG = CH / 8;
-constexpr int ROWS16 = 256;
-__device__ inline int nbr16(int m, int li, int dr, int dc) {
-    int pos = m * 16 + li;
-    int r = pos / 15 + dr, c = pos % 15 + dc;
-    bool ok = pos < POS && r >= 0 && r < 15 && c >= 0 && c < 15;
-    return ok ? r * 15 + c : POS + ((pos + dr * 15 + dc - POS) & 15);
-}
-struct ActF16x3 {
-    _Float16* hi;
-    _Float16* lo;
-    __device__ static int off(int ch, int pos) { return ((ch >> 3) * ROWS16 + pos) * 8 + (ch & 7); }
-    __device__ float get(int ch, int pos) const {
-        int o = off(ch, pos);
-        return (float)hi[o] + (float)lo[o];
-    }
-    __device__ void put(int ch, int pos, float y) {
-        _Float16 h = (_Float16)y;
-        _Float16 l = (_Float16)(y - (float)h);  // y - h is exact in f32
-        int o = off(ch, pos);
-        hi[o] = h;
-        lo[o] = l;
-    }
-    __device__ void get8(int c0, int pos, float* x) const {  // channels c0..c0+7, c0 % 8 == 0
-        const h8 xh = *(const h8*)(hi + ((c0 >> 3) * ROWS16 + pos) * 8);
-        const h8 xl = *(const h8*)(lo + ((c0 >> 3) * ROWS16 + pos) * 8);
-#pragma unroll
-        for (int j = 0; j < 8; j++) x[j] = (float)xh[j] + (float)xl[j];
-    }
-    __device__ void zero_slots(int tid, int nth) {
-        constexpr int PAD = (ROWS16 - POS) * 8;
-        for (int i = tid; i < CG * PAD; i += nth) {
-            int o = (i / PAD) * ROWS16 * 8 + POS * 8 + i % PAD;
-            hi[o] = (_Float16)0.f;
-            lo[o] = (_Float16)0.f;
-        }
-    }
-};
-
-// Residual tower in f16x3.  Wave w owns n-tiles {2(w&3), 2(w&3)+1} (32 output
-// channels) x M tiles [8(w>>2), 8(w>>2)+NM): NM = 8 for waves 0-3, 7 for waves
-// 4-7 (waves w and w+4 share a SIMD, so every SIMD carries 15 tile rows).
-// Per 32-deep k-step a wave issues 2*NM ds_read_b128 for 6*NM MFMAs and two
-// 1-KiB B-fragment loads per n-tile (hi, lo), prefetched one k-step ahead.
-constexpr int KS_HALVES = 8 * 64 * 8;  // B fragments of one k-step, all n-tiles
-
-template <int NM>
-__device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __restrict__ Wf, int np, int m0,
-                                         int lane, f32x4 (&acc)[2][NM]) {
-    // Software pipeline over half k-steps: the A fragments of M tiles [HA, NM)
-    // are read while the MFMAs of tiles [0, HA) run, and those of [0, HA) for
-    // the next k-step while the MFMAs of [HA, NM) run.  The order is pinned with
-    // sched_group_barrier (the default scheduler sinks every read to its use).
-    // Branch-free: the last k-step prefetches k-step 0 / tap 9 (valid addresses,
-    // results unused) so each tap is one basic block.
-    constexpr int HA = (NM + 1) / 2, HB = NM - HA;
-    const int li = lane & 15, q = lane >> 4;
-    const _Float16* wh = Wf + ((size_t)(2 * np) * 64 + lane) * 8;
-    const _Float16* wl = wh + K * CH;
-    h8 b[2][2];
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        b[n][0] = *(const h8*)(wh + n * 512);
-        b[n][1] = *(const h8*)(wl + n * 512);
-    }
-    h8 ah[NM], al[NM];
-    int nb[NM];
-    int lv = li;
-    asm volatile("" : "+v"(lv));
-#pragma unroll
-    for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lv, -1, -1) + q * ROWS16) * 8;
-#pragma unroll
-    for (int m = 0; m < HA; m++) {
-        ah[m] = *(const h8*)(act.hi + nb[m]);
-        al[m] = *(const h8*)(act.lo + nb[m]);
-    }
-    for (int tap = 0; tap < 9; tap++) {
-#pragma unroll
-        for (int cq = 0; cq < 4; cq++) {
-            const int ks = tap * 4 + cq;
-            const int ao = cq * 4 * ROWS16 * 8;
-#ifndef GZ_PV_EXP_NO_A
-#pragma unroll
-            for (int m = HA; m < NM; m++) {
-                ah[m] = *(const h8*)(act.hi + ao + nb[m]);
-                al[m] = *(const h8*)(act.lo + ao + nb[m]);
-            }
-#endif
-            h8 bn[2][2];
-            {
-#ifndef GZ_PV_EXP_NO_B
-                const int ks1 = ks + 1 < 36 ? ks + 1 : 0;
-#else
-                const int ks1 = 0;
-#endif
-#pragma unroll
-                for (int n = 0; n < 2; n++) {
-                    bn[n][0] = *(const h8*)(wh + ks1 * KS_HALVES + n * 512);
-                    bn[n][1] = *(const h8*)(wl + ks1 * KS_HALVES + n * 512);
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < HA; m++) {
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
-            }
-            if (cq == 3) {  // next tap: new neighbour offsets (tap 9 after the last: unused)
-                const int t2 = tap + 1, dr = t2 / 3 - 1, dc = t2 % 3 - 1;
-                int lw = li;
-                asm volatile("" : "+v"(lw));
-#pragma unroll
-                for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lw, dr, dc) + q * ROWS16) * 8;
-            }
-            {
-                const int ao2 = ((cq + 1) & 3) * 4 * ROWS16 * 8;
-#ifndef GZ_PV_EXP_NO_A
-#pragma unroll
-                for (int m = 0; m < HA; m++) {
-                    ah[m] = *(const h8*)(act.hi + ao2 + nb[m]);
-                    al[m] = *(const h8*)(act.lo + ao2 + nb[m]);
-                }
-#else
-                (void)ao2;
-#endif
-            }
-#pragma unroll
-            for (int m = HA; m < NM; m++) {
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
-            }
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                b[n][0] = bn[n][0];
-                b[n][1] = bn[n][1];
-            }
-#ifndef GZ_PV_NO_SCHED
-            // pin the interleave: B prefetch first, then 2 A reads per 6 MFMAs
-            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);  // VMEM read
-#pragma unroll
-            for (int m = 0; m < HA; m++) {
-                if (m < HB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);              // MFMA
-            }
-#pragma unroll
-            for (int m = 0; m + 1 < HB; m++) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * (HA - HB), 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#endif
-        }
-    }
-}
-
-#ifdef GZ_PV_EXP_DB
-// experiment: full double buffering of the A fragments (one k-step ahead)
-template <int NM>
-__device__ __forceinline__ void f16_conv_db(const ActF16x3& act, const _Float16* __restrict__ Wf, int np, int m0,
-                                            int lane, f32x4 (&acc)[2][NM]) {
-    const int li = lane & 15, q = lane >> 4;
-    const _Float16* wh = Wf + ((size_t)(2 * np) * 64 + lane) * 8;
-    const _Float16* wl = wh + K * CH;
-    h8 b[2][2];
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        b[n][0] = *(const h8*)(wh + n * 512);
-        b[n][1] = *(const h8*)(wl + n * 512);
-    }
-    h8 ah[NM], al[NM];
-    int nb[NM];
-    int lv = li;
-    asm volatile("" : "+v"(lv));
-#pragma unroll
-    for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lv, -1, -1) + q * ROWS16) * 8;
-#pragma unroll
-    for (int m = 0; m < NM; m++) {
-        ah[m] = *(const h8*)(act.hi + nb[m]);
-        al[m] = *(const h8*)(act.lo + nb[m]);
-    }
-    for (int tap = 0; tap < 9; tap++) {
-#pragma unroll
-        for (int cq = 0; cq < 4; cq++) {
-            const int ks = tap * 4 + cq;
-            h8 bn[2][2];
-            const int ks1 = ks + 1 < 36 ? ks + 1 : 0;
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                bn[n][0] = *(const h8*)(wh + ks1 * KS_HALVES + n * 512);
-                bn[n][1] = *(const h8*)(wl + ks1 * KS_HALVES + n * 512);
-            }
-            if (cq == 3) {
-                const int t2 = tap + 1, dr = t2 / 3 - 1, dc = t2 % 3 - 1;
-                int lw = li;
-                asm volatile("" : "+v"(lw));
-#pragma unroll
-                for (int m = 0; m < NM; m++) nb[m] = (nbr16(m0 + m, lw, dr, dc) + q * ROWS16) * 8;
-            }
-            const int ao2 = ((cq + 1) & 3) * 4 * ROWS16 * 8;
-            h8 nh[NM], nl[NM];
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-                nh[m] = *(const h8*)(act.hi + ao2 + nb[m]);
-                nl[m] = *(const h8*)(act.lo + ao2 + nb[m]);
-            }
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
-            }
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-                ah[m] = nh[m];
-                al[m] = nl[m];
-            }
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                b[n][0] = bn[n][0];
-                b[n][1] = bn[n][1];
-            }
-            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-            }
-        }
-    }
-}
-#endif
-
-// The f16 MFMAs compute C^T[ch][pos] (A = weight fragment, B = activation
-// fragment), so lane (li, g) holds channels 4g..4g+3 of its N tile for position
-// 16*tile + li: 4 consecutive channels = 8 bytes of the hi plane and 8 of the lo.
-__device__ __forceinline__ void f16_get4(const ActF16x3& act, int ch0, int pos, f32x4& out) {
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const int o = ActF16x3::off(ch0, pos);
-    const h4 xh = *(const h4*)(act.hi + o);
-    const h4 xl = *(const h4*)(act.lo + o);
-#pragma unroll
-    for (int r = 0; r < 4; r++) out[r] = (float)xh[r] + (float)xl[r];
-}
-
-// y = acc*S + T (+ skip), ReLU, split into hi/lo and stored as two 8-byte writes
-template <bool SKIP>
-__device__ __forceinline__ void f16_put4(ActF16x3& act, const f32x4& acc, const f32x4& s, const f32x4& t,
-                                         const f32x4& skip, int ch0, int pos) {
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    h4 hi, lo;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        float y = acc[r] * s[r] + t[r];
-        if (SKIP) y += skip[r];
-        y = y > 0.f ? y : 0.f;
-        const _Float16 h = (_Float16)y;
-        hi[r] = h;
-        lo[r] = (_Float16)(y - (float)h);  // y - h is exact in f32
-    }
-    const int o = ActF16x3::off(ch0, pos);
-    *(h4*)(act.hi + o) = hi;
-    *(h4*)(act.lo + o) = lo;
-}
-
+// ============================================================ fp16x3 policy (gz_f16conv.h)
 template <int NM>
 __device__ __forceinline__ void f16_load(const ActF16x3& act, f32x4 (&out)[2][NM], int np, int m0, int lane) {
     asm volatile("" : "+v"(lane));  // addresses are recomputed per layer, not hoisted (and spilled)
@@ -470,30 +186,17 @@ __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict
 #pragma unroll
                 for (int m = 0; m < NM; m++) acc[n][m] = zero4();
             PV_WAVE_T0();
-#ifdef GZ_PV_EXP_HALF_WAVES
-            if (wave < 4)
-#endif
-#ifdef GZ_PV_EXP_DB
-            f16_conv_db<NM>(act, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, m0, lane, acc);
-#else
-            f16_conv<NM>(act, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, m0, lane, acc);
-#endif
+            f16_conv<NM, 4, 8, 9>(act, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, m0, lane, acc);
             PV_STAMP(2);
             PV_WAVE_STAMP(8);
-#ifndef GZ_PV_EXP_NOSKIP
             if (half == 0) f16_load<NM>(act, skip, np, m0, lane);  // block input, for the skip connection
-#endif
             __syncthreads();
             PV_WAVE_STAMP(16);
             PV_STAMP(3);
             if (half == 0)
                 f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
             else
-#ifndef GZ_PV_EXP_NOSKIP
                 f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
-#else
-                f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
-#endif
             __syncthreads();
             PV_STAMP(4);
         }
@@ -569,33 +272,6 @@ __device__ __forceinline__ void slab_load(const float* __restrict__ slab, f32x4 
     for (int m = 0; m < MT; m++)
 #pragma unroll
         for (int r = 0; r < 4; r++) out[m][r] = slab[(m * 4 + r) * 64 + lane];
-}
-
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-__device__ inline float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-    return v;
-}
-
-// sum_i w[i*stride] * x[i] for one output column; BATCH independent loads in flight
-template <int NI, int BATCH>
-__device__ __forceinline__ float dot_col(const float* __restrict__ wp, int stride, const float* __restrict__ xp) {
-    static_assert(NI % BATCH == 0, "batch must divide the input count");
-    float acc = 0.f;
-#pragma unroll 1
-    for (int i0 = 0; i0 < NI; i0 += BATCH) {
-        float w[BATCH];
-#pragma unroll
-        for (int j = 0; j < BATCH; j++) w[j] = wp[(size_t)(i0 + j) * stride];
-#pragma unroll
-        for (int j = 0; j < BATCH; j++) acc += w[j] * xp[i0 + j];
-    }
-    return acc;
 }
 
 // ---- shared pieces of both kernels; NTH = threads per workgroup
@@ -818,13 +494,10 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
     act.hi = (_Float16*)lds;
     act.lo = act.hi + CH * ROWS16;
     const int count = board_count(n, d_count);
-    act.zero_slots(threadIdx.x, NT16);
+    act.zero_slots(threadIdx.x, NT16, CH);
     for (int i = threadIdx.x; i < 3 * (ROWS - POS); i += NT16)
         sm.planes[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
 
-#ifdef GZ_PV_EXP_PRIO
-    if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
     PV_STAMP(30);  // start of the clock (slot 30 is not a phase)
     for (int b = blockIdx.x; b < count; b += gridDim.x) {
         int tid = threadIdx.x;

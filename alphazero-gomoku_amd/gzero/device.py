@@ -195,3 +195,36 @@ def pv_forward(weights, leaf_rows):
     lg, v, pr = pv_forward_dev(weights, d_b, n, d_probs=d_probs)
     torch.cuda.synchronize()
     return lg.cpu().numpy().reshape(n, 225), v.cpu().numpy(), pr.cpu().numpy().reshape(n, 225)
+
+
+class GNWeights:
+    """BG planner nets (GraphNet + OpponentDQN) blob resident on the device."""
+
+    def __init__(self, blob):
+        lib = require_gpu()
+        blob = np.ascontiguousarray(blob, np.float32)
+        if blob.size != lib.gz_gn_weight_floats():
+            raise ValueError(f"planner blob has {blob.size} floats, kernel expects {lib.gz_gn_weight_floats()}")
+        self.tensor = torch.from_numpy(blob).cuda()
+
+
+def gn_forward_dev(weights, d_boards, n, d_count=None, d_p=None, d_q=None, d_logits=None):
+    lib = require_gpu()
+    if d_p is None:
+        d_p = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    if d_q is None:
+        d_q = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    _lib.check(lib.gz_gn_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_p), ptr(d_q),
+                                 ptr(d_logits), stream()), "gz_gn_forward")
+    return d_p, d_q, d_logits
+
+
+def gn_forward(weights, leaf_rows):
+    """Host convenience: [n,16] uint32 rows -> (p [n,225], q [n,225], logits [n,225])."""
+    rows = np.ascontiguousarray(leaf_rows, np.uint32).reshape(-1, 16)
+    n = rows.shape[0]
+    d_b = torch.from_numpy(rows.view(np.int32).copy()).cuda()
+    d_lg = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    p, q, lg = gn_forward_dev(weights, d_b, n, d_logits=d_lg)
+    torch.cuda.synchronize()
+    return p.cpu().numpy().reshape(n, 225), q.cpu().numpy().reshape(n, 225), lg.cpu().numpy().reshape(n, 225)

@@ -139,9 +139,9 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
  * csrc/gz_pvnet.h / gzero/weights.py).  Boards [n][16] uint32 bit planes.  If
  * d_count is not NULL it holds the number of valid boards on the device
  * (n = capacity).  Outputs: logits [n][225], value [n] (tanh), probs
- * [n][225] (softmax) or NULL.  precision: GZ_PV_FP32 (exact f32 MFMA; needs
- * d_workspace of gz_pv_workspace_bytes(n) bytes) or GZ_PV_F16X3 (3-term fp16
- * split on the fp16 MFMA, ~22-bit operands, f32 accumulation; no workspace). */
+ * [n][225] (softmax) or NULL.  precision: GZ_PV_FP32 (exact f32 MFMA) or
+ * GZ_PV_F16X3 (3-term fp16 split on the fp16 MFMA, ~22-bit operands, f32
+ * accumulation).  d_workspace: gz_pv_workspace_bytes(n) bytes, required. */
 #define GZ_PV_FP32 0
 #define GZ_PV_F16X3 1
 size_t gz_pv_weight_floats(void);
@@ -149,6 +149,15 @@ size_t gz_pv_workspace_bytes(int32_t n);
 int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
                   float* d_logits, float* d_value, float* d_probs, void* d_workspace, int32_t precision,
                   void* stream);
+
+/* ---- K7: BG planner nets (bg_planner.py:22-78, BGPlannerAI.get_move :243-250) ----
+ * d_weights: packed blob of gz_gn_weight_floats() floats (csrc/gz_gnet.h,
+ * gzero/planner_nets.py).  Boards [n][16] uint32 bit planes (d_count as above).
+ * Outputs: p = softmax(GraphNet(planes)) [n][225], q = OpponentDQN(planes)
+ * [n][225], logits [n][225] or NULL.  GraphNet convs in f16x3 (as GZ_PV_F16X3). */
+size_t gz_gn_weight_floats(void);
+int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
+                  float* d_p, float* d_q, float* d_logits, void* stream);
 
 #ifdef __cplusplus
 }
