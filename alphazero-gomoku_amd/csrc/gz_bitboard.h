@@ -370,9 +370,9 @@ GZ_HD int policy_move(const BB& me, const BB& op, const BB& e, const Centre& cb,
     return select_bit(s, (int)below(x, (uint32_t)n));
 }
 
-// Full rollout (_simulate with planner_steps = 0, ai_agent.py:251-285) from a
-// non-terminal position.  `mover` is the colour to move (1/2), `ai` the root AI.
-// Returns the terminal value (ai_agent.py:287-304).
+// Offensive part of _simulate (ai_agent.py:276-285) from a non-terminal position,
+// `steps0` plies already played (the planner's).  `mover` is the colour to move
+// (1/2), `ai` the root AI.  Returns the terminal value (ai_agent.py:287-304).
 struct RolloutResult {
     double value;
     BB black, white;
@@ -381,11 +381,11 @@ struct RolloutResult {
 };
 
 GZ_HD RolloutResult rollout(BB black, BB white, int n_moves, int mover, int ai, int max_depth,
-                            uint64_t key, uint32_t* cnt) {
+                            uint64_t key, uint32_t* cnt, int steps0 = 0) {
     Centre cb = centre_buckets();
     BB me = mover == 1 ? black : white;
     BB op = mover == 1 ? white : black;
-    int over = 0, winner = 0, steps = 0;
+    int over = 0, winner = 0, steps = steps0;
     while (!over && steps < max_depth) {
         BB e = empties(me, op);
         int ne = bb_count(e);

@@ -39,6 +39,20 @@ class SearchParams(ctypes.Structure):  # gz_search_params
                 ("planner_steps", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
+class PlannerParams(ctypes.Structure):  # gz_planner_params
+    _fields_ = [("k", ctypes.c_int32), ("pad", ctypes.c_int32), ("alpha", ctypes.c_double),
+                ("explore", ctypes.c_double)]
+
+
+# BGPlannerAI.params (bg_planner.py:215-219)
+PLANNER = {"easy": (8, 0.5, 0.2), "medium": (12, 0.65, 0.1), "hard": (16, 0.75, 0.05)}
+
+
+def planner_params(difficulty):
+    k, a, e = PLANNER.get(difficulty, PLANNER["medium"])
+    return PlannerParams(k, 0, a, e)
+
+
 class Record(ctypes.Structure):  # gz_record, 80 bytes
     _fields_ = [("black", ctypes.c_uint32 * 8), ("white", ctypes.c_uint32 * 8),
                 ("game_id", ctypes.c_int64), ("ply", ctypes.c_int16), ("move", ctypes.c_int16),
@@ -83,6 +97,10 @@ SIGNATURES = {
     "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _P]),
     "gz_gn_weight_floats": (_SZ, []),
     "gz_gn_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
+    "gz_plan_workspace_bytes": (_SZ, [_I32, _I32]),
+    "gz_plan_search": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _P]),
+    "gz_planner_move_workspace_bytes": (_SZ, [_I32]),
+    "gz_planner_move": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

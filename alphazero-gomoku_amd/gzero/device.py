@@ -228,3 +228,55 @@ def gn_forward(weights, leaf_rows):
     p, q, lg = gn_forward_dev(weights, d_b, n, d_logits=d_lg)
     torch.cuda.synchronize()
     return p.cpu().numpy().reshape(n, 225), q.cpu().numpy().reshape(n, 225), lg.cpu().numpy().reshape(n, 225)
+
+
+def plan_search(states, game_ids, params, pparams, gn_weights, want_trees=False, leaf_cap=0):
+    """AlphaZeroGomokuAI.get_move with BG-planner rollout plies (gz_plan_search).
+    Returns (moves, stats, trees, leaves) like search()."""
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_gids = torch.as_tensor(np.asarray(game_ids, np.int64)).cuda()
+    d_moves = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_stats = torch.zeros(n * ctypes.sizeof(_lib.SearchStats), dtype=torch.uint8, device="cuda")
+    S = params.num_simulations
+    tb = lib.gz_tree_bytes(S)
+    d_trees = torch.zeros(n * tb, dtype=torch.uint8, device="cuda") if want_trees else None
+    gather = (params.flags & _lib.GZ_FLAG_GATHER_LEAVES) != 0
+    d_leaves = torch.zeros(max(1, leaf_cap) * 16, dtype=torch.int32, device="cuda") if gather else None
+    d_lc = torch.zeros(1, dtype=torch.int32, device="cuda") if gather else None
+    ws = torch.empty(lib.gz_plan_workspace_bytes(n, S), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.gz_plan_search(ptr(d_states), ptr(d_gids), n, ctypes.byref(params), ctypes.byref(pparams),
+                                  ptr(gn_weights.tensor), ptr(ws), ptr(d_trees), ptr(d_moves), ptr(d_stats),
+                                  ptr(d_leaves), int(leaf_cap), ptr(d_lc), stream()), "gz_plan_search")
+    torch.cuda.synchronize()
+    st = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=np.dtype(
+        [("n_nodes", "<i4"), ("predicts", "<i4"), ("main_draws", "<i4"), ("pad", "<i4"), ("sim_draws", "<i8")]))
+    trees = None
+    if want_trees:
+        raw = d_trees.cpu().numpy().reshape(n, tb)
+        trees = [parse_tree(raw[i], S, int(st["n_nodes"][i])) for i in range(n)]
+    leaves = None
+    if gather:
+        cnt = int(d_lc.item())
+        leaves = d_leaves.cpu().numpy().view(np.uint32).reshape(-1, 16)[:min(cnt, leaf_cap)]
+    return d_moves.cpu().numpy(), st, trees, leaves
+
+
+def planner_move(states, ais, keys, pparams, gn_weights):
+    """BGPlannerAI.get_move per state (gz_planner_move): returns (moves, draws)."""
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_ai = torch.as_tensor(np.asarray(ais, np.int32)).cuda()
+    d_keys = torch.as_tensor(np.asarray(keys, np.uint64).view(np.int64)).cuda()
+    d_moves = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_draws = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ws = torch.empty(lib.gz_planner_move_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.gz_planner_move(ptr(d_states), ptr(d_ai), ptr(d_keys), n, ctypes.byref(pparams),
+                                   ptr(gn_weights.tensor), ptr(ws), ptr(d_moves), ptr(d_draws), stream()),
+               "gz_planner_move")
+    torch.cuda.synchronize()
+    return d_moves.cpu().numpy(), d_draws.cpu().numpy().view(np.uint32)

@@ -28,6 +28,7 @@ extern "C" {
 #define GZ_ERR_ARG -1
 #define GZ_ERR_HIP -2
 #define GZ_ERR_UNSUPPORTED -3
+#define GZ_ERR_INTERNAL -4
 
 #define GZ_MAX_SIMULATIONS 4095
 #define GZ_MAX_GAME_PLIES 200
@@ -57,6 +58,15 @@ typedef struct gz_search_params {
 } gz_search_params;
 
 #define GZ_FLAG_GATHER_LEAVES 1 /* append every non-terminal node's board for the PV forward */
+
+/* BGPlannerAI.params (bg_planner.py:215-219): easy {8, 0.5, 0.2}, medium
+ * {12, 0.65, 0.1}, hard {16, 0.75, 0.05}. */
+typedef struct gz_planner_params {
+    int32_t k;       /* knowledge-search top-k, 1..16 */
+    int32_t pad;
+    double alpha;    /* mix_alpha */
+    double explore;  /* exploration probability */
+} gz_planner_params;
 
 /* One (s, pi, z) training tuple (training.py:77-97,203-210). 80 bytes. */
 typedef struct gz_record {
@@ -158,6 +168,27 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
 size_t gz_gn_weight_floats(void);
 int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
                   float* d_p, float* d_q, float* d_logits, void* stream);
+
+/* ---- K4+K5+K7: MCTS with BG-planner rollout plies (planner_steps > 0) ----
+ * gz_search's contract (ai_agent.py:109-222) for p->planner_steps >= 0 with the
+ * planner of pp (BGPlannerAI for the searching AI's colour, bg_planner.py:199-269)
+ * and its nets d_gn_weights (gz_gn_forward).  Host-driven: launches on `stream`
+ * and synchronises it once per simulation round.  d_workspace:
+ * gz_plan_workspace_bytes(n, num_simulations) bytes.  d_trees (optional) gets
+ * gz_tree_bytes(num_simulations) bytes per game in gz_search's layout. */
+size_t gz_plan_workspace_bytes(int32_t n, int32_t num_simulations);
+int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
+                   const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
+                   void* d_workspace, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
+                   uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, void* stream);
+
+/* BGPlannerAI.get_move (bg_planner.py:232-269) for each board: d_ai = the
+ * planner's colour P, d_keys = RNG stream; d_moves (-1 = None), d_draws.
+ * d_workspace: gz_planner_move_workspace_bytes(n) bytes. */
+size_t gz_planner_move_workspace_bytes(int32_t n);
+int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_ai, const uint64_t* d_keys, int32_t n,
+                    const gz_planner_params* pp, const float* d_gn_weights, void* d_workspace,
+                    int32_t* d_moves, uint32_t* d_draws, void* stream);
 
 #ifdef __cplusplus
 }

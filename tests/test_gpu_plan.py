@@ -1,0 +1,147 @@
+"""BG planner on the GPU: gz_planner_move (BGPlannerAI.get_move) and
+gz_plan_search (MCTS with planner rollout plies).
+
+Exact checks use the GPU's own net outputs: the C oracle is driven with p / q
+computed by gz_gn_forward for the same boards (the nets are fp32 and only
+tolerance-equal to torch's), so everything else -- knowledge-search scores, top-k,
+compose, RNG draws, trees -- must agree bit for bit.  Against the reference's
+fixtures the moves must agree except where the reference's own composed scores
+are a near-tie (|gap| <= 1e-6) that the nets' rounding can flip.
+"""
+import numpy as np
+import pytest
+
+from conftest import SEED, golden
+from gzero import _lib, boards, planner_nets
+
+pytestmark = pytest.mark.gpu
+
+DIFF = {"easy": (1.4, 0.2), "medium": (1.6, 0.05), "hard": (1.8, 0.01)}
+
+
+def _hexf(hs):
+    return np.array([int(h, 16) for h in hs], dtype=np.uint32).view(np.float32)
+
+
+@pytest.fixture(scope="module")
+def gnw():
+    from gzero import device
+    g = golden("planner")
+    gsd = planner_nets.init_graphnet_state(g["gn_seed"])
+    dsd = planner_nets.init_dqn_state(g["dqn_seed"])
+    return device.GNWeights(planner_nets.pack_planner_weights(gsd, dsd))
+
+
+def _state(oracle, moves):
+    b = oracle.new_board(moves)
+    return b, boards.make_states(b.cells()[None], n_moves=b.n_moves, player=b.player, over=b.over, winner=b.winner)
+
+
+def _rows(cells):
+    bl, wh = boards.cells_to_words(np.asarray(cells, np.int8).reshape(-1, 225))
+    return boards.leaf_words(bl, wh)
+
+
+def test_planner_move_exact_vs_oracle(oracle, gnw):
+    from gzero import device
+    g = golden("planner")
+    cases = g["cases"]
+    sts, ais, keys, obs = [], [], [], []
+    for c in cases:
+        b, st = _state(oracle, c["moves"])
+        obs.append(b)
+        sts.append(st[0])
+        ais.append(c["P"])
+        keys.append(oracle.lib().or_stream_key(g["seed"], c["game_id"], len(c["moves"]), 1))
+    sts = np.array(sts)
+    by_diff = {}
+    for i, c in enumerate(cases):
+        by_diff.setdefault(c["difficulty"], []).append(i)
+    p, q, _ = device.gn_forward(gnw, _rows([b.cells() for b in obs]))
+    for diff, idx in by_diff.items():
+        mv, dr = device.planner_move(sts[idx], [ais[i] for i in idx], [keys[i] for i in idx],
+                                     _lib.planner_params(diff), gnw)
+        for k, i in enumerate(idx):
+            om, od = oracle.planner_move(obs[i], ais[i], diff, p[i], q[i], keys[i])
+            assert (int(mv[k]), int(dr[k])) == (om, od), cases[i]["game_id"]
+
+
+def test_planner_move_vs_reference(oracle, gnw):
+    from gzero import device
+    g = golden("planner")
+    mism = 0
+    for diff in ("easy", "medium", "hard"):
+        cs = [c for c in g["cases"] if c["difficulty"] == diff]
+        sts = np.array([_state(oracle, c["moves"])[1][0] for c in cs])
+        keys = [oracle.lib().or_stream_key(g["seed"], c["game_id"], len(c["moves"]), 1) for c in cs]
+        mv, dr = device.planner_move(sts, [c["P"] for c in cs], keys, _lib.planner_params(diff), gnw)
+        a = _lib.PLANNER[diff][1]
+        for k, c in enumerate(cs):
+            assert int(dr[k]) == c["draws"]
+            if int(mv[k]) == c["move"]:
+                continue
+            mism += 1
+            top = c["top"]
+            comp = {cell: a * float(pp) - (1 - a) * float(qq)
+                    for cell, pp, qq in zip(top, _hexf(c["p"]), _hexf(c["q"]))}
+            assert int(mv[k]) in comp and abs(comp[int(mv[k])] - comp[c["move"]]) <= 1e-6, c["game_id"]
+    assert mism <= 3
+
+
+def _pq_from_gpu(gnw):
+    from gzero import device
+
+    def pq(board, game_id, sim, step):
+        cells = np.frombuffer(bytes(board.cell), dtype=np.int8)
+        p, q, _ = device.gn_forward(gnw, _rows(cells))
+        return p[0], q[0]
+    return pq
+
+
+@pytest.mark.parametrize("idx", range(20))
+def test_plan_search_exact_vs_oracle(oracle, gnw, idx):
+    from gzero import device
+    g = golden("planner_mcts")
+    c = g["cases"][idx]
+    b, st = _state(oracle, c["moves"])
+    cp, ex = DIFF[c["difficulty"]]
+    p = device.search_params(c["sims"], cp, ex, c["beta"], SEED)
+    p.planner_steps = c["planner_steps"]
+    mv, stats, trees, _ = device.plan_search(st, [c["game_id"]], p, _lib.planner_params(c["difficulty"]), gnw,
+                                             want_trees=True)
+    prm = oracle.make_params(c["difficulty"], sims=c["sims"], beta=c["beta"], seed=SEED,
+                             planner_steps=c["planner_steps"], pq=_pq_from_gpu(gnw))
+    om, ot = oracle.get_move(b, b.player, prm, c["game_id"])
+    assert int(mv[0]) == om
+    assert stats[0]["main_draws"] == ot["main_draws"]
+    assert stats[0]["sim_draws"] == ot["sim_draws"]
+    assert stats[0]["predicts"] == ot["predicts"]
+    t = trees[0]
+    n = len(ot["parent"])
+    assert [int(x) for x in t["parent"][:n]] == ot["parent"]
+    assert [int(x) for x in t["move"][1:n]] == ot["move"][1:n]
+    assert [int(x) for x in t["visits"][:n]] == ot["visits"]
+    assert [float(x) for x in t["value"][:n]] == ot["value"]
+
+
+def test_plan_search_vs_reference(oracle, gnw):
+    """All 20 reference searches in one batched call: same move / root statistics
+    unless a planner decision inside was a near-tie of the reference's nets."""
+    from gzero import device
+    g = golden("planner_mcts")
+    same = 0
+    for c in g["cases"]:
+        _, st = _state(oracle, c["moves"])
+        cp, ex = DIFF[c["difficulty"]]
+        p = device.search_params(c["sims"], cp, ex, c["beta"], SEED)
+        p.planner_steps = c["planner_steps"]
+        mv, stats, trees, _ = device.plan_search(st, [c["game_id"]], p, _lib.planner_params(c["difficulty"]), gnw,
+                                                 want_trees=True)
+        ok = int(mv[0]) == c["move"] and stats[0]["sim_draws"] == sum(c["sim_draws"])
+        if ok and "children" in c:
+            t = trees[0]
+            kids = [i for i in range(len(t["move"])) if t["parent"][i] == 0]
+            got = [[int(t["move"][i]), int(t["visits"][i]), float(t["value"][i])] for i in kids]
+            ok = got == c["children"]
+        same += ok
+    assert same >= 18, same
