@@ -592,6 +592,76 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
     }
 }
 
+// The move-application half of selfplay_kernel for searches run elsewhere
+// (gz_plan_search): record, make_move, finish / restart (training.py:141-218).
+__global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int n_slots, const int32_t* moves,
+                                                              gz_record* records, int rec_cap,
+                                                              gz_selfplay_counters* ctr) {
+    const int s = blockIdx.x;
+    if (s >= n_slots) return;
+    const int lane = lane_id();
+    SlotHeader* h = (SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
+    gz_record* rec = (gz_record*)(h + 1);
+    BB black, white;
+    load_bb(black, h->black);
+    load_bb(white, h->white);
+    const int n_moves = h->n_moves, player = h->player;
+    const int mv = moves[s];
+    if (mv < 0) return;  // unreachable: live games always have an empty cell
+    const int bit = cell_to_bit(mv);
+    BB& mine = player == 1 ? black : white;
+    const BB E = empties(black, white);
+    const bool win = bb_test(threats(mine).win, bit);
+    const int ne = bb_count(E);
+    if (lane == 0) {
+        gz_record& r = rec[n_moves];
+        store_bb(r.black, black);
+        store_bb(r.white, white);
+        r.game_id = h->game_id;
+        r.ply = (int16_t)n_moves;
+        r.move = (int16_t)mv;
+        r.player = (int8_t)player;
+        r.z = 0;
+    }
+    bb_set(mine, bit);
+    const int over = win ? player : ((ne == 1 || n_moves + 1 >= 200) ? 3 : 0);
+    __syncthreads();
+    long long games = 0;
+    int64_t game_id = h->game_id;
+    if (over) {
+        const int winner = over == 3 ? 0 : over;
+        const int n = n_moves + 1;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&ctr->records, n);
+        base = __shfl(base, 0);
+        for (int i = lane; i < n; i += WAVE) {
+            if (base + i < rec_cap) {
+                gz_record r = rec[i];
+                r.z = (int8_t)(winner == 0 ? 0 : (r.player == winner ? 1 : -1));
+                records[base + i] = r;
+            }
+        }
+        if (lane == 0 && base + n > rec_cap) {
+            int lost = base + n - (base > rec_cap ? base : rec_cap);
+            atomicAdd(&ctr->records_dropped, lost);
+        }
+        games = 1;
+        game_id += h->game_id_stride;
+        black = bb_zero();
+        white = bb_zero();
+    }
+    if (lane == 0) {
+        store_bb(h->black, black);
+        store_bb(h->white, white);
+        h->game_id = game_id;
+        h->n_moves = over ? 0 : n_moves + 1;
+        h->player = over ? 1 : 3 - player;
+        h->games_done += games;
+        atomicAdd((unsigned long long*)&ctr->moves, 1ull);
+        if (games) atomicAdd((unsigned long long*)&ctr->games, 1ull);
+    }
+}
+
 __global__ void selfplay_boards_kernel(const char* slots, int n_slots, gz_board_state* out, int64_t* gids) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
@@ -737,7 +807,7 @@ int validate_params(const gz_search_params* p) {
     if (p->num_simulations < 0 || p->num_simulations > GZ_MAX_SIMULATIONS)
         return fail(GZ_ERR_ARG, "num_simulations out of range [0, 4095]");
     if (p->planner_steps != 0)
-        return fail(GZ_ERR_UNSUPPORTED, "planner_steps > 0 (BG-planner rollouts) is not implemented on the device yet");
+        return fail(GZ_ERR_UNSUPPORTED, "planner_steps > 0 runs through gz_plan_search / gz_selfplay_plan_run");
     return GZ_OK;
 }
 
@@ -838,6 +908,45 @@ int gz_selfplay_run(void* d_slots, int32_t n_slots, const gz_search_params* p, i
     selfplay_kernel<<<n_slots, WAVE, smem_bytes(p->num_simulations), as_stream(stream)>>>(
         (char*)d_slots, n_slots, *p, n_plies, d_records, record_cap, sink, gather ? 1 : 0, d_counters);
     return check_launch("selfplay_kernel");
+}
+
+size_t gz_selfplay_plan_workspace_bytes(int32_t n_slots, int32_t num_simulations) {
+    size_t a = ((size_t)n_slots * sizeof(gz_board_state) + 255) & ~(size_t)255;
+    size_t b = ((size_t)n_slots * 8 + 255) & ~(size_t)255;
+    size_t c = ((size_t)n_slots * 4 + 255) & ~(size_t)255;
+    return a + b + c + gz_plan_workspace_bytes(n_slots, num_simulations);
+}
+
+int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params* p, const gz_planner_params* pp,
+                         const float* d_gn_weights, void* d_workspace, int32_t n_plies, gz_record* d_records,
+                         int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, gz_selfplay_counters* d_counters,
+                         void* stream) {
+    if (!p || !pp || !d_slots || n_slots <= 0 || n_plies < 0 || !d_counters || !d_records || record_cap < 0 ||
+        !d_workspace || !d_gn_weights)
+        return fail(GZ_ERR_ARG, "gz_selfplay_plan_run: bad arguments");
+    bool gather = (p->flags & GZ_FLAG_GATHER_LEAVES) != 0;
+    if (gather && (!d_leaves || leaf_cap < 0)) return fail(GZ_ERR_ARG, "gz_selfplay_plan_run: leaf buffer missing");
+    char* ws = (char*)d_workspace;
+    gz_board_state* d_boards = (gz_board_state*)ws;
+    ws += ((size_t)n_slots * sizeof(gz_board_state) + 255) & ~(size_t)255;
+    int64_t* d_gids = (int64_t*)ws;
+    ws += ((size_t)n_slots * 8 + 255) & ~(size_t)255;
+    int32_t* d_moves = (int32_t*)ws;
+    ws += ((size_t)n_slots * 4 + 255) & ~(size_t)255;
+    hipStream_t st = as_stream(stream);
+    for (int it = 0; it < n_plies; it++) {
+        selfplay_boards_kernel<<<(n_slots + 255) / 256, 256, 0, st>>>((const char*)d_slots, n_slots, d_boards, d_gids);
+        int rc = check_launch("selfplay_boards_kernel");
+        if (rc) return rc;
+        rc = gz_plan_search(d_boards, d_gids, n_slots, p, pp, d_gn_weights, ws, nullptr, d_moves, nullptr,
+                            gather ? d_leaves : nullptr, leaf_cap, gather ? &d_counters->leaves : nullptr, stream);
+        if (rc) return rc;
+        selfplay_commit_kernel<<<n_slots, WAVE, 0, st>>>((char*)d_slots, n_slots, d_moves, d_records, record_cap,
+                                                         d_counters);
+        rc = check_launch("selfplay_commit_kernel");
+        if (rc) return rc;
+    }
+    return GZ_OK;
 }
 
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations, gz_board_state* d_out,

@@ -16,7 +16,7 @@ import torch
 
 from . import _lib
 from .boards import RECORD_DTYPE, STATE_DTYPE, words_to_cells
-from .device import PVWeights, ptr, require_gpu, search_params, stream
+from .device import GNWeights, PVWeights, ptr, require_gpu, search_params, stream
 
 COUNTER_DTYPE = np.dtype([("records", "<i4"), ("leaves", "<i4"), ("records_dropped", "<i4"),
                           ("leaves_dropped", "<i4"), ("moves", "<i8"), ("games", "<i8")])
@@ -25,14 +25,23 @@ COUNTER_DTYPE = np.dtype([("records", "<i4"), ("leaves", "<i4"), ("records_dropp
 class SelfPlayEngine:
     def __init__(self, n_slots=4096, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2,
                  seed=0, max_depth=100, pv_weights=None, plies_per_step=1, game_id_base=0,
-                 game_id_stride=None, planner_steps=0):
+                 game_id_stride=None, planner_steps=0, planner_difficulty="medium", gn_weights=None):
+        """planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
+        planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights."""
         self.lib = require_gpu()
-        if planner_steps:
-            raise _lib.GzeroError("planner_steps > 0 (BG-planner rollouts) is not implemented on the device yet")
         self.n_slots = int(n_slots)
         self.plies_per_step = int(plies_per_step)
         self.gather = pv_weights is not None
-        self.params = search_params(num_simulations, c_puct, exploration, beta, seed, max_depth, 0, self.gather)
+        self.planner_steps = int(planner_steps)
+        self.params = search_params(num_simulations, c_puct, exploration, beta, seed, max_depth,
+                                    self.planner_steps, self.gather)
+        if self.planner_steps:
+            if gn_weights is None:
+                raise ValueError("planner_steps > 0 needs gn_weights (the planner's GraphNet/DQN)")
+            self.gn_weights = gn_weights if isinstance(gn_weights, GNWeights) else GNWeights(gn_weights)
+            self.pparams = _lib.planner_params(planner_difficulty)
+            self.d_plan_ws = torch.empty(self.lib.gz_selfplay_plan_workspace_bytes(self.n_slots, num_simulations),
+                                         dtype=torch.uint8, device="cuda")
         self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
             else PVWeights(pv_weights)
         S = self.params.num_simulations
@@ -61,6 +70,13 @@ class SelfPlayEngine:
         if n > self.plies_per_step and self.gather:
             raise ValueError("n_plies exceeds the leaf buffer sized for plies_per_step")
         self.d_counters.zero_()
+        if self.planner_steps:
+            _lib.check(self.lib.gz_selfplay_plan_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params),
+                                                     ctypes.byref(self.pparams), ptr(self.gn_weights.tensor),
+                                                     ptr(self.d_plan_ws), n, ptr(self.d_records), self.record_cap,
+                                                     ptr(self.d_leaves), self.leaf_cap, ptr(self.d_counters),
+                                                     stream()), "gz_selfplay_plan_run")
+            return
         _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
                                             self.leaf_cap, ptr(self.d_counters), stream()), "gz_selfplay_run")

@@ -145,3 +145,26 @@ def test_plan_search_vs_reference(oracle, gnw):
             ok = got == c["children"]
         same += ok
     assert same >= 18, same
+
+
+def test_selfplay_planner_games_vs_oracle(oracle, gnw):
+    """gz_selfplay_plan_run: whole games (planner_steps 2, 3 sims) equal the oracle's
+    play_one_game driven by the GPU's net outputs."""
+    from gzero.selfplay import SelfPlayEngine, records_to_games
+    n_slots = 3
+    eng = SelfPlayEngine(n_slots=n_slots, num_simulations=3, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED,
+                         plies_per_step=16, planner_steps=2, planner_difficulty="medium", gn_weights=gnw)
+    games = {}
+    for _ in range(40):
+        eng.step()
+        for gid, g in records_to_games(eng.records()).items():
+            if gid < n_slots:
+                games[gid] = g
+        if len(games) == n_slots:
+            break
+    assert len(games) == n_slots
+    prm = oracle.make_params("medium", sims=3, beta=0.2, seed=SEED, planner_steps=2, pq=_pq_from_gpu(gnw))
+    for gid, g in games.items():
+        ref = oracle.play_game(prm, prm, gid)
+        assert g["moves"] == ref["moves"], gid
+        assert g["z"] == ref["z"], gid
