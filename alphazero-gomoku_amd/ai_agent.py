@@ -12,11 +12,12 @@ irreproducible).  Here every draw comes from counter-based streams keyed by
 a fresh random value, so unseeded AIs are as random as the reference's while a
 fixed (seed, game_id) reproduces a game exactly, on any number of GPUs.
 
-Not yet on the device: BG-planner-guided rollout plies (``planner_steps > 0``).
-Such an AI raises ``GzeroError`` as soon as it needs a search; pass
-``planner_steps=0``.  ``time_limit`` is accepted for compatibility; the GPU
-completes every simulation (200 simulations take well under a millisecond), so
-the reference's wall-clock cut-off (ai_agent.py:183-189) never applies.
+With ``planner_steps > 0`` (the reference's default, 5) every rollout starts
+with that many BG-planner plies (ai_agent.py:265-274): the search runs as the
+batched pipeline of ``gz_plan_search`` with the AI's ``bg_planner`` nets.
+``time_limit`` is accepted for compatibility; the GPU completes every
+simulation, so the reference's wall-clock cut-off (ai_agent.py:183-189) never
+applies.
 """
 import logging
 import random
@@ -25,6 +26,7 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
+from bg_planner import BGPlannerAI
 from gomoku_board import GomokuBoard
 from neural_network import GomokuModel
 from gzero import _lib, device
@@ -45,6 +47,7 @@ class AlphaZeroGomokuAI:
         self.time_reward_factor = float(time_reward_factor)
         self.logger = logging.getLogger(__name__)
         self.model = GomokuModel(model_path=model_path, device=self.device)
+        self.bg_planner = BGPlannerAI(player=self.player, difficulty=self.difficulty, device="cpu")
         # live knobs of the reference's table (ai_agent.py:65-90); bg_weight and
         # planning_steps are kept but, as in the reference, never read
         self.difficulty_params = {
@@ -64,11 +67,9 @@ class AlphaZeroGomokuAI:
         self.last_search_stats = None
 
     def _search_params(self, gather):
-        if self.planner_steps:
-            raise _lib.GzeroError("planner_steps > 0 (BG-planner rollout plies) is not implemented on the device yet; "
-                                  "construct the AI with planner_steps=0")
         return device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
-                                    self.params["exploration"], self.beta, self.seed, 100, 0, gather)
+                                    self.params["exploration"], self.beta, self.seed, 100, self.planner_steps,
+                                    gather)
 
     def get_move(self, board: GomokuBoard) -> Optional[Tuple[int, int]]:
         """ai_agent.py:109-136 (opening book, MCTS, exploration) on the GPU."""
@@ -83,7 +84,12 @@ class AlphaZeroGomokuAI:
             p = device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
                                      self.params["exploration"], self.beta, self.seed, 100, 0, False)
         cap = p.num_simulations + 1 if gather else 0
-        mv, stats, _, leaves = device.search(board.to_state(), [self.game_id], p, leaf_cap=cap)
+        if needs_search and self.planner_steps and p.num_simulations > 0:
+            mv, stats, _, leaves = device.plan_search(board.to_state(), [self.game_id], p,
+                                                      self.bg_planner.planner_params(),
+                                                      self.bg_planner.device_weights(), leaf_cap=cap)
+        else:
+            mv, stats, _, leaves = device.search(board.to_state(), [self.game_id], p, leaf_cap=cap)
         if gather and leaves is not None and len(leaves):
             from gzero import boards
             self.model.predict_batch(boards.words_to_cells(leaves[:, :8], leaves[:, 8:]))
@@ -114,7 +120,6 @@ class AIFactory:
         if ai_type == "alphazero":
             return AlphaZeroGomokuAI(player, difficulty, **kwargs)
         if ai_type == "bg_planner":
-            from bg_planner import BGPlannerAI
             return BGPlannerAI(player, difficulty, device=kwargs.get("device", "cpu"))
         raise ValueError(f"Unsupported ai_type: {ai_type}")
 

@@ -1,15 +1,23 @@
-"""Drop-in ``bg_planner`` module (reference: bg_planner.py:22-269) -- partial.
+"""Drop-in ``bg_planner`` module (reference: bg_planner.py:22-269).
 
-``KnowledgeSearch._pattern_score`` runs on the GPU pattern kernel
-(``gz_pattern_score``, the same LUT the search uses for the UCB's BG term).
-The planner itself (``BGPlannerAI.get_move``: knowledge-scored top-k +
-GraphNet/OpponentDQN composition, bg_planner.py:232-269) is not on the device
-yet; constructing ``BGPlannerAI`` raises ``GzeroError`` rather than silently
-running a CPU version.
+* ``GraphNet`` / ``OpponentDQN`` -- the reference's torch modules (same parameter
+  names, gzero/planner_nets.py); they are the weights' home and training side.
+* ``KnowledgeSearch._pattern_score`` runs on the GPU pattern kernel.
+* ``BGPlannerAI.get_move`` runs on the GPU (``gz_planner_move``): both nets in one
+  batched MFMA kernel (gz_gnet.hip), then the knowledge-search top-k, the
+  alpha-mix with the opponent DQN and the exploration draw in one wavefront.
+
+Randomness: the reference draws from the global ``random`` module.  Here each
+call draws from the counter-based stream (``seed``, ``game_id``, ply, call index).
 """
+import random
+from typing import List, Optional, Tuple
+
 import numpy as np
+import torch
 
 from gzero import _lib
+from gzero.planner_nets import GraphNet, OpponentDQN, pack_planner_weights  # noqa: F401  (re-exported)
 
 
 class KnowledgeSearch:
@@ -28,6 +36,61 @@ class KnowledgeSearch:
 
 
 class BGPlannerAI:
-    def __init__(self, player: int, difficulty: str = "medium", device: str = "cpu"):
-        raise _lib.GzeroError("BGPlannerAI (GraphNet + OpponentDQN + knowledge search) is not implemented on the "
-                              "device yet")
+    """BG-Planner AI (bg_planner.py:199-269) on the GPU."""
+
+    def __init__(self, player: int, difficulty: str = "medium", device: str = "cpu", seed: Optional[int] = None,
+                 game_id: int = 0):
+        self.player = player
+        self.difficulty = difficulty
+        self.device = torch.device(device)
+        self.board_size = 15
+        self.graph_net = GraphNet(self.board_size).to(self.device)
+        self.opp_dqn = OpponentDQN(self.board_size).to(self.device)
+        self.k_search = KnowledgeSearch(self.board_size)
+        self.params = {
+            'easy': {'k': 8, 'mix_alpha': 0.5, 'explore': 0.2},
+            'medium': {'k': 12, 'mix_alpha': 0.65, 'explore': 0.1},
+            'hard': {'k': 16, 'mix_alpha': 0.75, 'explore': 0.05},
+        }[difficulty if difficulty in ['easy', 'medium', 'hard'] else 'medium']
+        self.graph_net.eval()
+        self.opp_dqn.eval()
+        self.seed = random.getrandbits(64) if seed is None else int(seed)
+        self.game_id = int(game_id)
+        self._calls = 0
+        self._packed = None
+        self._packed_key = None
+
+    def _param_key(self):
+        return tuple((p.data_ptr(), p._version) for m in (self.graph_net, self.opp_dqn)
+                     for p in m.state_dict().values())
+
+    def device_weights(self):
+        """Both nets packed on the GPU, repacked after any parameter change."""
+        from gzero.device import GNWeights
+        key = self._param_key()
+        if self._packed is None or key != self._packed_key:
+            self._packed = GNWeights(pack_planner_weights(self.graph_net.state_dict(), self.opp_dqn.state_dict()))
+            self._packed_key = key
+        return self._packed
+
+    def planner_params(self):
+        return _lib.PlannerParams(int(self.params['k']), 0, float(self.params['mix_alpha']),
+                                  float(self.params['explore']))
+
+    def _board_to_planes(self, board_state: np.ndarray) -> np.ndarray:
+        planes = np.zeros((3, self.board_size, self.board_size), dtype=np.float32)
+        planes[0] = (board_state == 1).astype(np.float32)
+        planes[1] = (board_state == 2).astype(np.float32)
+        planes[2] = (board_state == 0).astype(np.float32)
+        return planes
+
+    def get_move(self, board) -> Optional[Tuple[int, int]]:
+        from gzero import device, rng
+        if not board.get_valid_moves():
+            return None
+        self._calls += 1
+        key = rng.stream_key(self.seed, self.game_id, board.get_move_count(), self._calls)
+        mv, _ = device.planner_move(board.to_state(), [self.player], [key], self.planner_params(),
+                                    self.device_weights())
+        m = int(mv[0])
+        return None if m < 0 else (m // 15, m % 15)

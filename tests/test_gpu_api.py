@@ -89,3 +89,41 @@ def test_gomoku_model_predict_and_checkpoint(tmp_path):
         m2.model.policy_fc.bias.add_(1.0)  # uniform shift: softmax unchanged, repack must happen
         m2.model.value_fc2.bias.add_(0.5)
     assert m2.predict(b.get_board_state())[1] != m.predict(b.get_board_state())[1]
+
+
+def _load_planner(ai_or_planner, g):
+    from gzero import planner_nets
+    pl = getattr(ai_or_planner, "bg_planner", ai_or_planner)
+    pl.graph_net.load_state_dict(planner_nets.init_graphnet_state(g["gn_seed"]))
+    pl.opp_dqn.load_state_dict(planner_nets.init_dqn_state(g["dqn_seed"]))
+
+
+def test_bg_planner_ai_golden():
+    """BGPlannerAI.get_move on the GPU against the reference (near-ties of the nets allowed)."""
+    from bg_planner import BGPlannerAI
+    g = golden("planner")
+    same = 0
+    for c in g["cases"][:90]:
+        b = _board(c["moves"])
+        pl = BGPlannerAI(c["P"], c["difficulty"], seed=SEED, game_id=c["game_id"])
+        _load_planner(pl, g)
+        mv = pl.get_move(b)
+        same += (mv[0] * 15 + mv[1]) == c["move"]
+    assert same >= 88
+
+
+def test_ai_with_planner_golden():
+    """AlphaZeroGomokuAI(planner_steps > 0) = the reference's default AI."""
+    from ai_agent import AlphaZeroGomokuAI
+    g = golden("planner_mcts")
+    same = 0
+    for c in g["cases"]:
+        b = _board(c["moves"])
+        ai = AlphaZeroGomokuAI(b.current_player, c["difficulty"], beta=c["beta"], planner_steps=c["planner_steps"],
+                               seed=SEED, game_id=c["game_id"])
+        _load_planner(ai, g)
+        ai.params["num_simulations"] = c["sims"]
+        mv = ai.get_move(b)
+        same += (mv[0] * 15 + mv[1]) == c["move"]
+        assert ai.last_search_stats["predicts"] == c["predicts"]
+    assert same >= 18
