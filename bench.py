@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--no-elided", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--planner-steps", type=int, default=0,
+                    help="BG-planner plies per rollout (BASELINE config 4: 5 with --beta 0.2)")
     args = ap.parse_args()
 
     rank, ws = gdist.init_from_env()
@@ -140,9 +142,14 @@ def main():
     w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision=args.pv_precision)
     base, stride = gdist.shard_ids(rank, ws, args.slots)
     P = args.plies_per_step
+    gnw = None
+    if args.planner_steps:
+        from gzero import planner_nets
+        gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
     eng = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
                          beta=args.beta, seed=args.seed, pv_weights=w, plies_per_step=P,
-                         game_id_base=base, game_id_stride=stride)
+                         game_id_base=base, game_id_stride=stride, planner_steps=args.planner_steps,
+                         planner_difficulty="medium", gn_weights=gnw)
 
     def barrier():
         if ws > 1:
@@ -226,10 +233,11 @@ def main():
             "dtype": "fp32" if args.pv_precision == "fp32" else "f16x3 (fp32-equivalent split, f32 accumulate)",
             "data": "synthetic: self-play from the empty board with random-init weights (numpy default_rng(0))",
             "config": {
-                "workload": (f"BASELINE config 2: {args.slots} concurrent self-play games per GPU, 15x15, "
-                             f"{args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), beta={args.beta}, "
-                             "planner_steps=0, continuous refill; policy-value forward on every non-terminal node "
-                             f"the searches create (reference-work mode, {args.pv_precision})"),
+                "workload": (f"BASELINE config {4 if args.planner_steps else 2}: {args.slots} concurrent self-play "
+                             f"games per GPU, 15x15, {args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), "
+                             f"beta={args.beta}, planner_steps={args.planner_steps}, continuous refill; policy-value "
+                             "forward on every non-terminal node the searches create (reference-work mode, "
+                             f"{args.pv_precision})"),
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,
@@ -242,7 +250,7 @@ def main():
         }
 
     # ---- prior-elided run (same kernel, no PV gather / forward)
-    if not args.no_elided:
+    if not args.no_elided and not args.planner_steps:
         el = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
                             beta=args.beta, seed=args.seed, pv_weights=None, plies_per_step=10,
                             game_id_base=base, game_id_stride=stride)
