@@ -6,7 +6,7 @@
 //   layers 0..7: W then b; even = 3x3 [576][64] (k = tap*64 + cin), odd = 1x1 [64][64]
 //   policy conv W [2][64], b [2](+2); policy fc W^T [450][225], b [225](+3)
 //   dqn fc0 W^T [675][256], b; fc1 W^T [256][256], b; fc2 W^T [256][225], b (+3)
-// fp16 section: embed A fragments hi/lo [4][64][8]; per layer hi then lo in
+// then the fc0 restatement below; fp16 section: embed A fragments hi/lo [4][64][8]; per layer hi then lo in
 // v_mfma_f32_16x16x32_f16 A-fragment order [ks][n-tile 4][lane 64][8]
 // (n = 16*n_tile + lane%16, k = 32*ks + 8*(lane/16) + j).
 #pragma once
@@ -44,5 +44,9 @@ constexpr int h_layer_off(int i) {
     for (int j = 0; j < i; j++) off += ((j % 2 == 0) ? KS3 : KS1) * 4 * 64 * 8;
     return off;
 }
-constexpr int TOTAL = h_layer_off(8);
+// DQN fc0 for one-hot inputs: base [256] = bias + sum of the empty rows;
+// delta [450][256] = (black - empty) rows, then (white - empty) rows
+constexpr int D0_BASE = h_layer_off(8);
+constexpr int D0_DELTA = D0_BASE + DQH;
+constexpr int TOTAL = D0_DELTA + 450 * DQH;
 }  // namespace gzgn

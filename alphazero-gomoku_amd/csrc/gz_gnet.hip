@@ -21,11 +21,29 @@ using namespace gzgn;
 
 namespace {
 
+// Phase stamps (tools/gn_stamps.py only): -DGZ_GN_STAMPS accumulates s_memtime
+// deltas of workgroup 0 / wave 0 per phase; compiled out otherwise.
+#ifdef GZ_GN_STAMPS
+__device__ unsigned long long gz_gn_stamps[32];
+#define GN_STAMP(i)                                                \
+    do {                                                           \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                 \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+            gz_gn_stamps[i] += t_ - gz_gn_stamps[31];              \
+            gz_gn_stamps[31] = t_;                                 \
+        }                                                          \
+    } while (0)
+#else
+#define GN_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 constexpr int NT = 512;
 constexpr int NM = 4;        // M tiles per wave
 constexpr int PROWS = 240;   // fp32 planes [3][240]
 constexpr int ACT_BYTES = 2 * HID * ROWS16 * 2;  // 65536
-constexpr int SMALL_F = 3 * PROWS + 2 * POS + 256 + 2 * 256 + 32 + 2 * DQH + 2 * DQH;
+constexpr int SMALL_F = 3 * PROWS + 2 * POS + 256 + 2 * 256 + 32 + 2 * DQH + 2 * DQH + 256;
 constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
 
 // neighbour of the lane's position in M tile m for tap (dr, dc); POS (a zero plane slot) if off-board
@@ -69,6 +87,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     float* red = part + 2 * 256;                // [32]
     float* da = red + 32;                       // [2][256] dqn partial sums / activations
     float* dc = da + 2 * DQH;                   // [2][256]
+    int* slist = (int*)(dc + 2 * DQH);          // [225] stones (delta rows), row-major
 
     int count = n;
     if (d_count) {
@@ -79,6 +98,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     for (int i = threadIdx.x; i < 3 * (PROWS - POS); i += NT)
         planes[(i / (PROWS - POS)) * PROWS + POS + i % (PROWS - POS)] = 0.f;
 
+    GN_STAMP(30);
     for (int b = blockIdx.x; b < count; b += gridDim.x) {
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
@@ -95,26 +115,51 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             planes[2 * PROWS + p] = (float)(1u - (bl | wh));
         }
         __syncthreads();
+        GN_STAMP(0);
 
-        // ---- OpponentDQN (bg_planner.py:68-78): fc0 over the 225 one-hot inputs that are 1
+        // ---- OpponentDQN (bg_planner.py:68-78).  fc0 on the one-hot planes =
+        // base + the delta rows of the stones (gz_gnet.h), stones listed in
+        // row-major order (a fixed summation order: q is reproducible)
+        if (wave < 4) {
+            const int pos = tid;
+            int code = -1;
+            if (pos < POS) code = planes[pos] != 0.f ? pos : (planes[PROWS + pos] != 0.f ? POS + pos : -1);
+            const uint64_t m = __ballot(code >= 0);
+            if (lane == 0) red[16 + wave] = (float)__popcll(m);
+            __syncthreads();
+            int off = 0;
+            for (int k = 0; k < wave; k++) off += (int)red[16 + k];
+            if (code >= 0) slist[off + __popcll(m & ((1ull << lane) - 1ull))] = code;
+            if (tid == 0) red[24] = red[16] + red[17] + red[18] + red[19];
+        } else {
+            __syncthreads();
+        }
+        __syncthreads();
         {
             const int j = tid & 255, h = tid >> 8;
-            float acc = 0.f;
-            for (int pos = h; pos < POS; pos += 2) {
-                const int plane = planes[pos] != 0.f ? 0 : (planes[PROWS + pos] != 0.f ? 1 : 2);
-                acc += W[D0_WT + (size_t)(plane * POS + pos) * DQH + j];
+            const int ns = (int)red[24];
+            float acc = h == 0 ? W[D0_BASE + j] : 0.f;
+            const float* dt = W + D0_DELTA + j;
+            int i = h;
+            for (; i + 14 < ns; i += 16) {  // 8 independent loads in flight
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = dt[(size_t)slist[i + 2 * u] * DQH];
+#pragma unroll
+                for (int u = 0; u < 8; u++) acc += v[u];
             }
+            for (; i < ns; i += 2) acc += dt[(size_t)slist[i] * DQH];
             da[h * DQH + j] = acc;
         }
         __syncthreads();
         if (tid < DQH) {
-            float a = W[D0_B + tid] + (da[tid] + da[DQH + tid]);
+            float a = da[tid] + da[DQH + tid];
             dc[tid] = a > 0.f ? a : 0.f;
         }
         __syncthreads();
         {  // fc1 256->256 in two input halves
             const int j = tid & 255, h = tid >> 8;
-            da[h * DQH + j] = dot_col<128, 32>(W + D1_WT + (size_t)(h * 128) * DQH + j, DQH, dc + h * 128);
+            da[h * DQH + j] = dot_col<128, 64>(W + D1_WT + (size_t)(h * 128) * DQH + j, DQH, dc + h * 128);
         }
         __syncthreads();
         if (tid < DQH) {
@@ -124,10 +169,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         __syncthreads();
         {  // fc2 256->225 in two input halves
             const int j = tid & 255, h = tid >> 8;
-            if (j < POS) da[h * DQH + j] = dot_col<128, 32>(W + D2_WT + (size_t)(h * 128) * POS + j, POS, dc + DQH + h * 128);
+            if (j < POS) da[h * DQH + j] = dot_col<128, 64>(W + D2_WT + (size_t)(h * 128) * POS + j, POS, dc + DQH + h * 128);
         }
         __syncthreads();
         if (tid < POS) q_out[(size_t)b * POS + tid] = W[D2_B + tid] + (da[tid] + da[DQH + tid]);
+        GN_STAMP(1);
 
         // ---- embed conv 3->64 (K = 27 -> 32): planes are 0/1, so a*w = a*w_hi + a*w_lo
         {
@@ -162,6 +208,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             gn_store(act, acc, W + GE_B, np, m0, lane);
         }
         __syncthreads();
+        GN_STAMP(2);
 
         // ---- 4 x [conv3x3 + ReLU, conv1x1 + ReLU] (bg_planner.py:50-54)
         for (int i = 0; i < 8; i++) {
@@ -176,8 +223,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             else
                 f16_conv<NM, 2, 4, 1>(act, wf, np, m0, lane, acc);
             __syncthreads();  // every wave has read the layer input
+            if (i % 2 == 0) GN_STAMP(3);
+            else GN_STAMP(5);
             gn_store(act, acc, W + layer_bias(i), np, m0, lane);
             __syncthreads();
+            if (i % 2 == 0) GN_STAMP(4);
+            else GN_STAMP(6);
         }
 
         // ---- policy head: conv1x1 64->2 (one thread per position), flatten channel-major
@@ -196,6 +247,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             pc[POS + tid] = p1;
         }
         __syncthreads();
+        GN_STAMP(7);
         {  // Linear 450->225 in two input halves
             const int o = tid & 255, h = tid >> 8;
             if (o < POS) part[h * 256 + o] = dot_col<POS, 45>(W + GF_WT + (size_t)h * POS * POS + o, POS, pc + h * POS);
@@ -203,6 +255,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         __syncthreads();
         if (tid < POS) lg[tid] = W[GF_B + tid] + (part[tid] + part[256 + tid]);
         __syncthreads();
+        GN_STAMP(8);
         // ---- softmax over 225 logits (waves 0..3), torch.softmax(dim=0) semantics in fp32
         if (wave < 4) {
             float x = tid < POS ? lg[tid] : -3.0e38f;
@@ -226,10 +279,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             if (tid < POS) p_out[(size_t)b * POS + tid] = lg[tid] / s;
         }
         __syncthreads();
+        GN_STAMP(9);
     }
 }
 
 }  // namespace
+
+#ifdef GZ_GN_STAMPS
+extern "C" int gz_gn_stamps_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_gn_stamps), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_gn_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 extern "C" void gz_internal_set_error(const char* msg);
 

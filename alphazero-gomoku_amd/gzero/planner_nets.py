@@ -110,7 +110,11 @@ def _h_layer_off(i):
     return off
 
 
-GN_TOTAL = _h_layer_off(8)
+# DQN fc0 restated for one-hot inputs: fc0(x) = base + sum over stones of the
+# (black - empty) or (white - empty) row, base = bias + sum of the empty rows
+D0_BASE = _h_layer_off(8)              # [256]
+D0_DELTA = D0_BASE + DQN_H             # [450][256]: rows 0..224 black - empty, 225..449 white - empty
+GN_TOTAL = D0_DELTA + 450 * DQN_H
 GN_MACS = POS * (27 * HID + 4 * (K3 * HID + HID * HID) + 2 * HID) + 450 * POS
 DQN_MACS = 3 * POS * DQN_H + DQN_H * DQN_H + DQN_H * POS
 
@@ -164,6 +168,10 @@ def pack_planner_weights(gn_sd, dqn_sd):
     blob[D1_B:D1_B + DQN_H] = d["net.2.bias"]
     blob[D2_WT:D2_WT + DQN_H * POS] = d["net.4.weight"].T.reshape(-1)
     blob[D2_B:D2_B + POS] = d["net.4.bias"]
+    w0 = d["net.0.weight"].T.astype(np.float64)  # [675][256]
+    blob[D0_BASE:D0_BASE + DQN_H] = (d["net.0.bias"].astype(np.float64) + w0[2 * POS:].sum(0)).astype(np.float32)
+    delta = np.concatenate([w0[:POS] - w0[2 * POS:], w0[POS:2 * POS] - w0[2 * POS:]])
+    blob[D0_DELTA:D0_DELTA + 450 * DQN_H] = delta.astype(np.float32).reshape(-1)
     return blob
 
 
