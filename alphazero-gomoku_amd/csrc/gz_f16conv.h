@@ -104,14 +104,20 @@ __device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __
     constexpr int HA = (NM + 1) / 2, HB = NM - HA;
     constexpr int KS = TAPS * CQ;
     constexpr int KS_HALVES = NTT * 64 * 8;  // fragments of one k-step, all n-tiles
+    constexpr int KS_BYTES = KS_HALVES * 2, LO_BYTES = KS * KS_BYTES;
     const int li = lane & 15, q = lane >> 4;
-    const _Float16* wh = Wf + ((size_t)(2 * np) * 64 + lane) * 8;
-    const _Float16* wl = wh + (size_t)KS * KS_HALVES;
+    // weight fragments through a buffer resource: one 32-bit lane offset instead of
+    // two 64-bit pointers (the k-step / hi-lo / n-tile parts are wave-uniform)
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = ((2 * np) * 64 + lane) * 16;
+    auto wload = [&](int ks, int n, int lo) -> h8 {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+    };
     h8 b[2][2];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
-        b[n][0] = *(const h8*)(wh + n * 512);
-        b[n][1] = *(const h8*)(wl + n * 512);
+        b[n][0] = wload(0, n, 0);
+        b[n][1] = wload(0, n, 1);
     }
     h8 ah[NM], al[NM];
     int nb[NM];
@@ -140,8 +146,8 @@ __device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __
                 const int ks1 = ks + 1 < KS ? ks + 1 : 0;
 #pragma unroll
                 for (int n = 0; n < 2; n++) {
-                    bn[n][0] = *(const h8*)(wh + ks1 * KS_HALVES + n * 512);
-                    bn[n][1] = *(const h8*)(wl + ks1 * KS_HALVES + n * 512);
+                    bn[n][0] = wload(ks1, n, 0);
+                    bn[n][1] = wload(ks1, n, 1);
                 }
             }
 #pragma unroll

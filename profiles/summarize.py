@@ -39,7 +39,7 @@ summary = {"bench": {k: bench[k] for k in ("value", "unit", "ms_per_step", "step
 for k, v in durs.items():
     # the bench's timed window is the LAST `steps` PV launches (warm-up launches
     # include opening plies with no leaves)
-    timed = v[-steps:] if k == "pv_kernel" else v
+    timed = v[-steps:] if k.startswith("pv_kernel") else v
     summary["kernels"][k] = {"calls": len(v), "avg_ms_all": sum(v) / len(v),
                              "avg_ms_timed_window": sum(timed) / len(timed), "max_ms": max(v)}
 
@@ -55,15 +55,16 @@ def pmc(name, counter):
 
 fetch = pmc("pmc_fetch", "FETCH_SIZE")
 write = pmc("pmc_write", "WRITE_SIZE")
-for k in ("pv_kernel", "selfplay_kernel"):
+PV = next((k for k in durs if k.startswith("pv_kernel")), "pv_kernel")
+for k in (PV, "selfplay_kernel"):
     if k in fetch and k in write:
-        f = fetch[k][-steps:] if k == "pv_kernel" else fetch[k]
-        w = write[k][-steps:] if k == "pv_kernel" else write[k]
+        f = fetch[k][-steps:] if k == PV else fetch[k]
+        w = write[k][-steps:] if k == PV else write[k]
         summary["kernels"].setdefault(k, {})["hbm_bytes_per_launch"] = {
             "fetch_raw": sum(f) / len(f) * 1024, "write": sum(w) / len(w) * 1024,
             "total_raw": (sum(f) / len(f) + sum(w) / len(w)) * 1024,
             "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024; access widths uncalibrated -> raw"}
-pv = summary["kernels"].get("pv_kernel", {})
+pv = summary["kernels"].get(PV, {})
 boards = bench["config"]["pv_boards_per_step"]
 if "hbm_bytes_per_launch" in pv:
     tb = pv["hbm_bytes_per_launch"]["total_raw"]
