@@ -119,6 +119,7 @@ __device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __
         b[n][0] = wload(0, n, 0);
         b[n][1] = wload(0, n, 1);
     }
+
     h8 ah[NM], al[NM];
     int nb[NM];
     int lv = li;

@@ -172,8 +172,58 @@ __device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][N
     }
 }
 
+// last residual layer: y = relu(acc*S + T + skip) is only consumed by the 1x1
+// heads (policy 128->2, value 128->1), so the epilogue reduces it straight into
+// per-wave partial head sums hpart[np][3][256] (32 channels each) instead of
+// storing the map (neural_network.py:132-142)
+template <int NM>
+__device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const float* __restrict__ W,
+                                                const float* __restrict__ S, const float* __restrict__ T,
+                                                const f32x4 (&skip)[2][NM], int np, int m0, int lane,
+                                                float* __restrict__ hpart) {
+    asm volatile("" : "+v"(lane));
+    lane &= 63;
+    float s0[NM], s1[NM], sv[NM];
+#pragma unroll
+    for (int m = 0; m < NM; m++) s0[m] = s1[m] = sv[m] = 0.f;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(S + ch0), t = *(const f32x4*)(T + ch0);
+        const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
+        const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+#pragma unroll
+        for (int m = 0; m < NM; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = acc[n][m][r] * s[r] + t[r] + skip[n][m][r];
+                y = y > 0.f ? y : 0.f;
+                s0[m] += w0[r] * y;
+                s1[m] += w1[r] * y;
+                sv[m] += wv[r] * y;
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < NM; m++) {
+        float a = s0[m], c = s1[m], v = sv[m];
+        a += __shfl_xor(a, 16);
+        c += __shfl_xor(c, 16);
+        v += __shfl_xor(v, 16);
+        a += __shfl_xor(a, 32);
+        c += __shfl_xor(c, 32);
+        v += __shfl_xor(v, 32);
+        const int pos = (m0 + m) * 16 + (lane & 15);
+        if (lane < 16 && pos < POS) {
+            hpart[(np * 3 + 0) * 256 + pos] = a;
+            hpart[(np * 3 + 1) * 256 + pos] = c;
+            hpart[(np * 3 + 2) * 256 + pos] = v;
+        }
+    }
+}
+
 template <int NM, int m0>
-__device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict__ W, int wave, int lane) {
+__device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict__ W, int wave, int lane,
+                                          float* __restrict__ hpart) {
     const int np = wave & 3;
     for (int blk = 0; blk < 2; blk++) {
         f32x4 skip[2][NM];
@@ -195,8 +245,10 @@ __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict
             PV_STAMP(3);
             if (half == 0)
                 f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
-            else
+            else if (blk == 0)
                 f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+            else
+                f16_store_heads<NM>(acc, W, R + RES_S, R + RES_T, skip, np, m0, lane, hpart);
             __syncthreads();
             PV_STAMP(4);
         }
@@ -284,8 +336,9 @@ struct Smem {
     float* lg;      // [256] logits, then exp(logit - max)
     float* part;    // [2][256] policy_fc partial sums
     float* vq;      // [3][64] value_fc1 partial sums
+    float* hpart;   // [4][3][256] fused 1x1 head partial sums (f16x3 kernel)
 };
-constexpr int SMALL_F = 3 * ROWS + 2 * POS + POS + 32 + 256 + 512 + 192;
+constexpr int SMALL_F = 3 * ROWS + 2 * POS + POS + 32 + 256 + 512 + 192 + 4 * 3 * 256;
 constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
 
 __device__ inline Smem smem_layout(char* lds) {
@@ -297,6 +350,7 @@ __device__ inline Smem smem_layout(char* lds) {
     m.lg = m.red + 32;
     m.part = m.lg + 256;
     m.vq = m.part + 512;
+    m.hpart = m.vq + 192;
     return m;
 }
 
@@ -341,13 +395,26 @@ __device__ __forceinline__ void conv0_tile(Act& act, const float* __restrict__ W
 
 // heads (neural_network.py:132-159) + softmax (neural_network.py:240-247) for board b;
 // the tower's output map is in act.  Ends with a barrier.
-template <int NTH, class Act>
+template <int NTH, class Act, bool FUSED>
 __device__ __forceinline__ void heads(const Act& act, const Smem& sm, const float* __restrict__ W, int b, int tid,
                                       float* __restrict__ logits, float* __restrict__ value,
                                       float* __restrict__ probs) {
     const int lane = tid & 63, wave = tid >> 6;
     // 1x1 convs (policy 128->2, value 128->1), one thread per position
-    if (tid < POS) {
+    if (FUSED) {  // partial sums of the 4 channel quarters from the last epilogue
+        if (tid < POS) {
+            float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                p0 += sm.hpart[(q * 3 + 0) * 256 + tid];
+                p1 += sm.hpart[(q * 3 + 1) * 256 + tid];
+                v += sm.hpart[(q * 3 + 2) * 256 + tid];
+            }
+            sm.hp[tid] = p0;
+            sm.hp[POS + tid] = p1;
+            sm.hv[tid] = v;
+        }
+    } else if (tid < POS) {
         const int pos = tid;
         float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
         for (int c0 = 0; c0 < CH; c0 += 8) {
@@ -476,7 +543,7 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
                 __syncthreads();
             }
         }
-        heads<NT32>(act, sm, W, b, tid, logits, value, probs);
+        heads<NT32, ActF32, false>(act, sm, W, b, tid, logits, value, probs);
     }
 }
 
@@ -510,10 +577,10 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
-            f16_tower<7, 8>(act, W, wave, lane);
+            f16_tower<7, 8>(act, W, wave, lane, sm.hpart);
         else
-            f16_tower<8, 0>(act, W, wave, lane);
-        heads<NT16>(act, sm, W, b, tid, logits, value, probs);
+            f16_tower<8, 0>(act, W, wave, lane, sm.hpart);
+        heads<NT16, ActF16x3, true>(act, sm, W, b, tid, logits, value, probs);
     }
 }
 

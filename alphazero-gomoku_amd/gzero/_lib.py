@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgzero.so")
+# GZ_LIBRARY: an alternative build of the same library (A/B kernel experiments, tools/Makefile)
+LIB_PATH = os.environ.get("GZ_LIBRARY") or os.path.join(HERE, "libgzero.so")
 
 GZ_OK = 0
 GZ_FLAG_GATHER_LEAVES = 1
