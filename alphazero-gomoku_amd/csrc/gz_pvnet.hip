@@ -258,7 +258,32 @@ __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict
 // conv0 3->128 + BN + ReLU in f16 (C^T form): the input planes are 0/1, exact in
 // fp16, so a*w = a*w_hi + a*w_lo (2 MFMAs, no a_lo term); K = 27 (k = tap*3 + cin)
 // padded to one 32-deep k-step.  Wave w: N tile w, all 15 M tiles.
-__device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict__ W, const float* planes, int nt,
+// im2col of conv0 for the board in `planes`: col[row][k] (fp16, 0/1 exactly),
+// k = tap*3 + cin (27 -> 32 zero-padded), row = position (rows >= 225 zero).
+// One thread per (row, k-half); built once per board for all 8 waves.
+template <int NTH>
+__device__ __forceinline__ void build_im2col(_Float16* __restrict__ col, const float* __restrict__ planes, int tid) {
+    for (int t = tid; t < 256 * 2; t += NTH) {
+        const int row = t >> 1, k0 = (t & 1) * 16;
+        const int r = row / 15, c = row % 15;
+        h8 v[2];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int k = k0 + j;
+            const int tap = k / 3, cin = k % 3;
+            const int rr = r + tap / 3 - 1, cc = c + tap % 3 - 1;
+            const bool ok = k < 27 && row < POS && rr >= 0 && rr < 15 && cc >= 0 && cc < 15;
+            v[j >> 3][j & 7] = ok ? (_Float16)planes[cin * ROWS + rr * 15 + cc] : (_Float16)0.f;
+        }
+        *(h8*)(col + row * 32 + k0) = v[0];
+        *(h8*)(col + row * 32 + k0 + 8) = v[1];
+    }
+}
+
+// conv0 3->128 + BN + ReLU in f16 (C^T form): the input planes are 0/1, exact in
+// fp16, so a*w = a*w_hi + a*w_lo (2 MFMAs, no a_lo term); K = 27 (k = tap*3 + cin)
+// padded to one 32-deep k-step.  Wave w: N tile w, all 15 M tiles.
+__device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict__ W, const _Float16* col, int nt,
                                           int lane) {
     const int li = lane & 15, q = lane >> 4;
     const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
@@ -266,20 +291,14 @@ __device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict
     const int ch0 = nt * 16 + 4 * q;
     const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
     const f32x4 none = zero4();
-    int lv = li;
-    asm volatile("" : "+v"(lv));
-    for (int m = 0; m < MT; m++) {
-        h8 a;
+    h8 a[MT];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int k = 8 * q + j;  // lane-uniform within each quarter-wave
-            const int tap = k / 3, cin = k % 3;
-            const int idx = k < 27 ? nbr(m, lv, tap / 3 - 1, tap % 3 - 1) : ZERO;
-            a[j] = (_Float16)planes[(k < 27 ? cin : 0) * ROWS + idx];
-        }
+    for (int m = 0; m < MT; m++) a[m] = *(const h8*)(col + (m * 16 + li) * 32 + 8 * q);
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
         f32x4 acc = zero4();
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a[m], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a[m], acc, 0, 0, 0);
         const int pos = m * 16 + li;
         if (pos < POS) f16_put4<false>(act, acc, s, t, none, ch0, pos);
     }
@@ -338,6 +357,8 @@ struct Smem {
     float* vq;      // [3][64] value_fc1 partial sums
     float* hpart;   // [4][3][256] fused 1x1 head partial sums (f16x3 kernel)
 };
+// the f16x3 kernel's conv0 im2col (256 x 32 halves) reuses hp..hpart
+static_assert((2 * POS + POS + 32 + 256 + 512 + 192 + 4 * 3 * 256) * 4 >= 256 * 32 * 2, "im2col space");
 constexpr int SMALL_F = 3 * ROWS + 2 * POS + POS + 32 + 256 + 512 + 192 + 4 * 3 * 256;
 constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
 
@@ -573,7 +594,11 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         load_planes<NT16>(sm.planes, boards + (size_t)b * 16, tid);
         __syncthreads();
         PV_STAMP(0);
-        conv0_f16(act, W, sm.planes, wave, lane);
+        // im2col in the heads' scratch area (dead until this board's heads)
+        _Float16* col = (_Float16*)sm.hp;
+        build_im2col<NT16>(col, sm.planes, tid);
+        __syncthreads();
+        conv0_f16(act, W, col, wave, lane);
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
