@@ -175,10 +175,32 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         if (tid < POS) q_out[(size_t)b * POS + tid] = W[D2_B + tid] + (da[tid] + da[DQH + tid]);
         GN_STAMP(1);
 
-        // ---- embed conv 3->64 (K = 27 -> 32): planes are 0/1, so a*w = a*w_hi + a*w_lo
+        // ---- embed conv 3->64 (K = 27 -> 32): planes are 0/1, so a*w = a*w_hi + a*w_lo.
+        // im2col (256 rows x 32 halves, built once per board) lives in the activation
+        // area, k-chunk q of row r at channel-group slot (q, r) so the zero rows
+        // POS..255 stay zero, until every wave holds its fragments in registers.
         {
+            _Float16* col = act.hi;
+            for (int t = tid; t < 256 * 2; t += NT) {
+                const int row = t >> 1, k0 = (t & 1) * 16;
+                const int r = row / 15, c = row % 15;
+                h8 v[2];
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const int k = k0 + j;
+                    const int tap = k / 3, cin = k % 3;
+                    const int rr = r + tap / 3 - 1, cc = c + tap % 3 - 1;
+                    const bool ok = k < 27 && row < POS && rr >= 0 && rr < 15 && cc >= 0 && cc < 15;
+                    v[j >> 3][j & 7] = ok ? (_Float16)planes[cin * PROWS + rr * 15 + cc] : (_Float16)0.f;
+                }
+                *(h8*)(col + ((k0 >> 3) * ROWS16 + row) * 8) = v[0];
+                *(h8*)(col + ((k0 >> 3) * ROWS16 + ROWS16 + row) * 8) = v[1];
+            }
+            __syncthreads();
             const int li = lane & 15, q = lane >> 4;
-            f32x4 acc[2][NM];
+            h8 a[NM];
+#pragma unroll
+            for (int m = 0; m < NM; m++) a[m] = *(const h8*)(col + (q * ROWS16 + (m0 + m) * 16 + li) * 8);
             h8 wa[2][2];
 #pragma unroll
             for (int nn = 0; nn < 2; nn++) {
@@ -186,25 +208,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
                 wa[nn][0] = *(const h8*)wf;
                 wa[nn][1] = *(const h8*)(wf + 4 * 64 * 8);
             }
-            int lv = li;
-            asm volatile("" : "+v"(lv));
+            f32x4 acc[2][NM];
 #pragma unroll
-            for (int m = 0; m < NM; m++) {
-                h8 a;
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int k = 8 * q + j;
-                    const int tap = k / 3, cin = k % 3;
-                    const int idx = k < 27 ? pnbr(m0 + m, lv, tap / 3 - 1, tap % 3 - 1) : POS;
-                    a[j] = (_Float16)planes[(k < 27 ? cin : 0) * PROWS + idx];
-                }
+            for (int m = 0; m < NM; m++)
 #pragma unroll
                 for (int nn = 0; nn < 2; nn++) {
                     acc[nn][m] = zero4();
-                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][0], a, acc[nn][m], 0, 0, 0);
-                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][1], a, acc[nn][m], 0, 0, 0);
+                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][0], a[m], acc[nn][m], 0, 0, 0);
+                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][1], a[m], acc[nn][m], 0, 0, 0);
                 }
-            }
+            __syncthreads();  // every wave has its im2col fragments
             gn_store(act, acc, W + GE_B, np, m0, lane);
         }
         __syncthreads();
