@@ -572,6 +572,9 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
 // (one wave per SIMD with 512 registers and all 15 M tiles per wave measured 37%
 // slower: the compiler serialises the A-fragment reads of a single stream)
 constexpr int NT16 = 512;
+#ifndef PV_SPLIT
+#define PV_SPLIT 8  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
+#endif
 __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restrict__ W,
                                                          const uint32_t* __restrict__ boards, int n,
                                                          const int32_t* d_count, float* __restrict__ logits,
@@ -602,9 +605,9 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
-            f16_tower<7, 8>(act, W, wave, lane, sm.hpart);
+            f16_tower<15 - PV_SPLIT, PV_SPLIT>(act, W, wave, lane, sm.hpart);
         else
-            f16_tower<8, 0>(act, W, wave, lane, sm.hpart);
+            f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart);
         heads<NT16, ActF16x3, true>(act, sm, W, b, tid, logits, value, probs);
     }
 }
