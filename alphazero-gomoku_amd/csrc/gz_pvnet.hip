@@ -608,7 +608,9 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
             f16_tower<15 - PV_SPLIT, PV_SPLIT>(act, W, wave, lane, sm.hpart);
         else
             f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart);
-        heads<NT16, ActF16x3, true>(act, sm, W, b, tid, logits, value, probs);
+        int tid_h = threadIdx.x;  // re-read: a pinned tid kept live across the tower is spilled
+        asm volatile("" : "+v"(tid_h));
+        heads<NT16, ActF16x3, true>(act, sm, W, b, tid_h, logits, value, probs);
     }
 }
 

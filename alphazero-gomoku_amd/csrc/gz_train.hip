@@ -1,0 +1,164 @@
+// gz_train.hip -- training-set materialisation on the device.
+//
+// GomokuSelfPlayDataset (training.py:104-134) turns the replay into
+//   samples [0, n)           : every record as is
+//   samples n + 8j + 2k + f  : record sel[j] under rot90^k then (f) a horizontal flip
+//                              (augment_sample, training.py:63-71: k = 0..3, flip F/T)
+// with planes [black, white, empty] float32 [3][15][15] (the model input),
+// the label move index and the value float(z).  The planes follow np.rot90
+// (counter-clockwise, axes (1, 2)) and np.flip(axis=2) (training.py:44-51);
+// the label follows the reference's _transform_index (training.py:53-61),
+// which rotates the other way -- kept bit for bit unless GZ_AUG_FIX_LABELS.
+//
+// HBM-bound byte work: one thread writes 4 consecutive floats of the flat
+// [S][675] plane array (16-B coalesced stores); the 80-byte record of a sample
+// is read by the ~169 threads that cover it (L1/L2 hits).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/gzero.h"
+
+namespace {
+
+constexpr int N = 15;
+constexpr int POS = N * N;
+constexpr int SAMPLE_F = 3 * POS;  // 675 floats
+
+// source cell (row-major) of output cell (i, j) under flip(rot90^k(x))
+__device__ __forceinline__ int aug_source(int i, int j, int k, int flip) {
+    if (flip) j = N - 1 - j;
+    for (int t = 0; t < k; t++) {  // y = rot90(x): y[i][j] = x[j][N-1-i]
+        const int a = j, b = N - 1 - i;
+        i = a;
+        j = b;
+    }
+    return i * N + j;
+}
+
+// label of a move under the same symmetry (training.py:53-61, or the corrected map)
+__device__ __forceinline__ int aug_label(int idx, int k, int flip, int fix) {
+    int r = idx / N, c = idx % N;
+    for (int t = 0; t < k; t++) {
+        const int a = fix ? N - 1 - c : c, b = fix ? r : N - 1 - r;
+        r = a;
+        c = b;
+    }
+    if (flip) c = N - 1 - c;
+    return r * N + c;
+}
+
+struct SampleRef {
+    int rec, k, flip;
+};
+
+__device__ __forceinline__ SampleRef sample_ref(long long s, int n, const int32_t* __restrict__ sel) {
+    if (s < n) return {(int)s, 0, 0};
+    const long long a = s - n;
+    return {sel[a >> 3], (int)((a & 7) >> 1), (int)(a & 1)};
+}
+
+__device__ __forceinline__ float plane_value(const gz_record* __restrict__ rec, int plane, int cell) {
+    const int bit = (cell / N) * 16 + cell % N;
+    const uint32_t b = (rec->black[bit >> 5] >> (bit & 31)) & 1u;
+    const uint32_t w = (rec->white[bit >> 5] >> (bit & 31)) & 1u;
+    const uint32_t v = plane == 0 ? b : (plane == 1 ? w : 1u - (b | w));
+    return (float)v;
+}
+
+__global__ void dataset_planes_kernel(const gz_record* __restrict__ recs, int n, const int32_t* __restrict__ sel,
+                                      const int64_t* __restrict__ ids, long long n_all, long long total_f,
+                                      float* __restrict__ x) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long e0 = t * 4;
+    if (e0 >= total_f) return;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const long long e = e0 + u;
+        v[u] = 0.f;
+        if (e < total_f) {
+            const long long so = e / SAMPLE_F;
+            const int rem = (int)(e - so * SAMPLE_F);
+            const int plane = rem / POS, cell = rem % POS;
+            const long long s = ids ? ids[so] : so;
+            const SampleRef r = (unsigned long long)s < (unsigned long long)n_all ? sample_ref(s, n, sel)
+                                                                                 : SampleRef{-1, 0, 0};
+            if ((unsigned)r.rec < (unsigned)n)  // out-of-range selections give zero planes, label -1
+                v[u] = plane_value(recs + r.rec, plane, aug_source(cell / N, cell % N, r.k, r.flip));
+        }
+    }
+    if (e0 + 4 <= total_f) {
+        *(float4*)(x + e0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int u = 0; u < 4 && e0 + u < total_f; u++) x[e0 + u] = v[u];
+    }
+}
+
+__global__ void dataset_labels_kernel(const gz_record* __restrict__ recs, int n, const int32_t* __restrict__ sel,
+                                      const int64_t* __restrict__ ids, long long n_all, long long count, int fix,
+                                      int64_t* __restrict__ y, float* __restrict__ val) {
+    const long long so = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (so >= count) return;
+    const long long s = ids ? ids[so] : so;
+    const SampleRef r = (unsigned long long)s < (unsigned long long)n_all ? sample_ref(s, n, sel) : SampleRef{-1, 0, 0};
+    if ((unsigned)r.rec >= (unsigned)n) {
+        y[so] = -1;
+        val[so] = 0.f;
+        return;
+    }
+    const gz_record* rec = recs + r.rec;
+    y[so] = aug_label(rec->move, r.k, r.flip, fix);
+    val[so] = (float)rec->z;
+}
+
+
+}  // namespace
+
+extern "C" void gz_internal_set_error(const char* msg);
+
+namespace {
+int launch(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m, const int64_t* d_ids,
+           long long count, int32_t flags, float* d_x, int64_t* d_y, float* d_v, hipStream_t st, const char* who) {
+    if (n < 0 || m < 0 || count < 0 || (n > 0 && !d_records) || (m > 0 && !d_sel) ||
+        (count > 0 && (!d_x || !d_y || !d_v)) || (flags & ~GZ_AUG_FIX_LABELS)) {
+        gz_internal_set_error((std::string(who) + ": bad arguments").c_str());
+        return GZ_ERR_ARG;
+    }
+    if (m > 0 && n == 0) {
+        gz_internal_set_error((std::string(who) + ": augmentation of an empty replay").c_str());
+        return GZ_ERR_ARG;
+    }
+    if (count == 0) return GZ_OK;
+    const long long n_all = (long long)n + 8LL * m;
+    const long long total_f = count * SAMPLE_F;
+    const int bs = 256;
+    const long long th = (total_f + 3) / 4;
+    dataset_planes_kernel<<<(unsigned)((th + bs - 1) / bs), bs, 0, st>>>(d_records, n, d_sel, d_ids, n_all, total_f, d_x);
+    dataset_labels_kernel<<<(unsigned)((count + bs - 1) / bs), bs, 0, st>>>(
+        d_records, n, d_sel, d_ids, n_all, count, (flags & GZ_AUG_FIX_LABELS) ? 1 : 0, d_y, d_v);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string(who) + ": " + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+}  // namespace
+
+extern "C" int gz_dataset_build(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m, int32_t flags,
+                                float* d_x, int64_t* d_y, float* d_v, void* stream) {
+    return launch(d_records, n, d_sel, m, nullptr, (long long)n + 8LL * (m > 0 ? m : 0), flags, d_x, d_y, d_v,
+                  (hipStream_t)stream, "gz_dataset_build");
+}
+
+extern "C" int gz_dataset_gather(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m,
+                                 const int64_t* d_ids, int64_t count, int32_t flags, float* d_x, int64_t* d_y,
+                                 float* d_v, void* stream) {
+    if (count > 0 && !d_ids) {
+        gz_internal_set_error("gz_dataset_gather: d_ids is required");
+        return GZ_ERR_ARG;
+    }
+    return launch(d_records, n, d_sel, m, d_ids, count, flags, d_x, d_y, d_v, (hipStream_t)stream,
+                  "gz_dataset_gather");
+}

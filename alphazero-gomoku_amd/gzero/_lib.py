@@ -17,6 +17,7 @@ GZ_MAX_SIMULATIONS = 4095
 GZ_MAX_GAME_PLIES = 200
 GZ_PV_FP32 = 0
 GZ_PV_F16X3 = 1
+GZ_AUG_FIX_LABELS = 1
 
 
 class GzeroUnavailable(RuntimeError):
@@ -104,6 +105,8 @@ SIGNATURES = {
     "gz_selfplay_plan_workspace_bytes": (_SZ, [_I32, _I32]),
     "gz_selfplay_plan_run": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I32, _P, _I32, _P, _I32, _P, _P]),
     "gz_planner_move": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
+    "gz_dataset_build": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P]),
+    "gz_dataset_gather": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _I64, _I32, _P, _P, _P, _P]),
 }
 
 _lib = None

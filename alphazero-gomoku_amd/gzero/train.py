@@ -1,0 +1,243 @@
+"""Device-resident training step: the replay stays on
+the GPU as 80-byte records, batches are materialised by the gz_dataset_gather
+kernel (augmentation included), and the policy-value SGD step runs data-parallel
+with one RCCL all-reduce of the flat gradient per step.
+
+Semantics follow the reference's training loop:
+
+* ``DeviceDataset`` = ``GomokuSelfPlayDataset`` (training.py:104-134): every
+  record, then the 8 symmetries of ``random.sample(range(n), max(1, int(n *
+  augment_ratio)))`` drawn from the same ``random`` module, sample order
+  identical (originals, then 8 per chosen record in (k_rot, flip) order).
+* ``loader_order`` = the index order of ``DataLoader(ds, batch_size,
+  shuffle)`` (training.py:453-454), produced by torch's own sampler over an index
+  set so the torch RNG is consumed exactly as the reference's loader does.
+* ``DeviceTrainer.train_epoch`` / ``validate_epoch`` = training.py:277-337:
+  CrossEntropy(logits, move) + MSE(value, z), ``clip_grad_norm_`` at
+  ``grad_clip``, Adam(lr 8e-4, wd 1e-5) and StepLR(2, 0.85) as in main()
+  (training.py:387-388,379-381); the loss is the mean of per-batch float
+  losses (accumulated on the device in float64, one host sync per epoch).
+
+Data parallel (world size N): every rank holds the same dataset (records are
+all-gathered at episode end, gzero.dist) and the same permutation; global batch
+k is ``batch_size * N`` consecutive permutation entries and rank r trains on
+its ``batch_size`` slice.  Each rank's loss is weighted by its share of the
+global batch and the gradients are SUM-all-reduced, so the update is the
+global-batch mean (BatchNorm statistics stay per rank, as in DDP).  N = 1 is the
+reference's loop exactly.
+"""
+import ctypes
+import random as _random
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.distributed as dist
+from torch.utils.data import DataLoader, Dataset
+
+from . import _lib
+from .boards import RECORD_DTYPE
+
+SAMPLE_SHAPE = (3, 15, 15)
+
+
+def _dev_ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def records_to_device(records):
+    """numpy RECORD_DTYPE array -> device uint8 tensor (80 B per record)."""
+    raw = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
+    return torch.from_numpy(raw.copy()).to("cuda")
+
+
+class DeviceDataset(Dataset):
+    """GomokuSelfPlayDataset over device records (training.py:104-134)."""
+
+    def __init__(self, records, use_augmentation=True, augment_ratio=0.5, fix_labels=False, rng=None,
+                 n_records=None):
+        if isinstance(records, torch.Tensor):
+            self.d_records = records
+            n = int(n_records if n_records is not None else records.numel() // RECORD_DTYPE.itemsize)
+        else:
+            records = np.asarray(records, RECORD_DTYPE)
+            n = len(records)
+            self.d_records = records_to_device(records)
+        rng = _random if rng is None else rng
+        sel = rng.sample(range(n), k=max(1, int(n * augment_ratio))) if (use_augmentation and n > 0) else []
+        self.n = n
+        self.m = len(sel)
+        self.flags = _lib.GZ_AUG_FIX_LABELS if fix_labels else 0
+        self.d_sel = torch.tensor(sel if sel else [0], dtype=torch.int32, device="cuda")
+
+    def __len__(self):
+        return self.n + 8 * self.m
+
+    def gather(self, d_ids, out=None):
+        """Samples d_ids (device int64) -> (x [B,3,15,15] f32, y [B] int64, v [B,1] f32) on the device."""
+        b = int(d_ids.numel())
+        if out is None:
+            out = (torch.empty((b,) + SAMPLE_SHAPE, dtype=torch.float32, device="cuda"),
+                   torch.empty(b, dtype=torch.int64, device="cuda"),
+                   torch.empty((b, 1), dtype=torch.float32, device="cuda"))
+        x, y, v = out
+        L = _lib.load()
+        _lib.check(L.gz_dataset_gather(_dev_ptr(self.d_records), self.n, _dev_ptr(self.d_sel), self.m,
+                                       _dev_ptr(d_ids), b, self.flags, _dev_ptr(x), _dev_ptr(y), _dev_ptr(v),
+                                       _stream()), "gz_dataset_gather")
+        return x, y, v
+
+    def materialize(self):
+        """The whole dataset (gz_dataset_build)."""
+        s = len(self)
+        x = torch.empty((s,) + SAMPLE_SHAPE, dtype=torch.float32, device="cuda")
+        y = torch.empty(s, dtype=torch.int64, device="cuda")
+        v = torch.empty((s, 1), dtype=torch.float32, device="cuda")
+        L = _lib.load()
+        _lib.check(L.gz_dataset_build(_dev_ptr(self.d_records), self.n, _dev_ptr(self.d_sel), self.m, self.flags,
+                                      _dev_ptr(x), _dev_ptr(y), _dev_ptr(v), _stream()), "gz_dataset_build")
+        return x, y, v
+
+    def __getitem__(self, i):
+        x, y, v = self.gather(torch.tensor([int(i)], dtype=torch.int64, device="cuda"))
+        return x[0], y[0], v[0]
+
+
+class _IndexSet(Dataset):
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return i
+
+
+def loader_order(n, batch_size=128, shuffle=True):
+    """Index batches of DataLoader(<n samples>, batch_size, shuffle) with the same torch-RNG use."""
+    return [b for b in DataLoader(_IndexSet(n), batch_size=batch_size, shuffle=shuffle)]
+
+
+def _world(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+class DeviceTrainer:
+    """Adam + StepLR policy-value SGD of training.main (training.py:379-388) on the device."""
+
+    def __init__(self, model, lr=8e-4, weight_decay=1e-5, grad_clip=0.8, step_size=2, gamma=0.85, group=None,
+                 device="cuda"):
+        self.gm = model
+        self.net = model.model if hasattr(model, "model") else model
+        self.device = torch.device(device)
+        self.net.to(self.device)
+        if hasattr(model, "device"):
+            model.device = self.device
+        self.grad_clip = grad_clip
+        self.group = group
+        self.world, self.rank = _world(group)
+        self.params = [p for p in self.net.parameters()]
+        self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay)
+        self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=step_size, gamma=gamma)
+        self.ce, self.mse = nn.CrossEntropyLoss(), nn.MSELoss()
+        if self.world > 1:
+            # identical replicas: rank 0's parameters and BatchNorm buffers everywhere
+            for t in list(self.net.state_dict().values()):
+                dist.broadcast(t, 0, group=group)
+            n = sum(p.numel() for p in self.params)
+            self.flat = torch.zeros(n, dtype=torch.float32, device=self.device)
+
+    def _allreduce_grads(self):
+        """One bucket: the whole gradient (2.85 MB) in a single SUM all-reduce."""
+        off = 0
+        views = []
+        for p in self.params:
+            k = p.numel()
+            g = self.flat[off:off + k]
+            if p.grad is None:
+                g.zero_()
+            else:
+                g.copy_(p.grad.reshape(-1))
+            views.append((p, g))
+            off += k
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        for p, g in views:
+            if p.grad is None:
+                p.grad = torch.empty_like(p)
+            p.grad.copy_(g.view_as(p))
+
+    def _slices(self, order, batch_size):
+        """Per-step (this rank's ids, local count, global count) of a permutation."""
+        B = batch_size * self.world
+        for k in range(0, len(order), B):
+            glob = order[k:k + B]
+            gcount = len(glob)
+            # remainder batches: split as evenly as possible, rank r keeps slice r
+            per = -(-gcount // self.world) if gcount < B else batch_size
+            mine = glob[self.rank * per:(self.rank + 1) * per]
+            yield mine, len(mine), gcount
+
+    def _ids(self, indices, order):
+        return order if indices is None else indices[order]
+
+    def train_epoch(self, ds, batch_size=128, indices=None, shuffle=True):
+        """One epoch over ds (or the subset ``indices``, a device int64 tensor); returns the mean batch loss."""
+        self.net.train()
+        n = len(ds) if indices is None else int(indices.numel())
+        order = torch.cat(loader_order(n, batch_size * self.world if self.world > 1 else batch_size, shuffle)) \
+            if n else torch.zeros(0, dtype=torch.int64)
+        order = order.to(self.device)
+        ids_all = self._ids(indices, order)
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        batches = 0
+        for mine, local, gcount in self._slices(ids_all, batch_size):
+            self.optimizer.zero_grad(set_to_none=False)
+            if local > 0:
+                x, y, v = ds.gather(mine)
+                logits, val = self.net(x)
+                loss = self.ce(logits, y) + self.mse(val, v)
+                (loss * (local / gcount) if self.world > 1 else loss).backward()
+                lval = loss.detach()
+            else:
+                lval = torch.zeros((), device=self.device)
+            if self.world > 1:
+                # the global-batch loss (for reporting) rides along with the gradient
+                self._allreduce_grads()
+                lval = lval * (local / gcount)
+                dist.all_reduce(lval, group=self.group)
+            if self.grad_clip is not None and self.grad_clip > 0:
+                nn.utils.clip_grad_norm_(self.params, self.grad_clip)
+            self.optimizer.step()
+            total += lval.double()
+            batches += 1
+        if self.world > 1:
+            for t in self.net.buffers():  # BatchNorm running stats: rank 0's, as DDP's broadcast_buffers
+                dist.broadcast(t, 0, group=self.group)
+        return float(total.item()) / max(1, batches)
+
+    @torch.no_grad()
+    def validate_epoch(self, ds, batch_size=128, indices=None):
+        self.net.eval()
+        n = len(ds) if indices is None else int(indices.numel())
+        # iterate an (unshuffled) DataLoader as the reference does: it draws one torch seed
+        order = loader_order(n, batch_size, shuffle=False)
+        order = (torch.cat(order) if order else torch.zeros(0, dtype=torch.int64)).to(self.device)
+        ids_all = self._ids(indices, order)
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        batches = 0
+        for k in range(0, n, batch_size):
+            x, y, v = ds.gather(ids_all[k:k + batch_size])
+            logits, val = self.net(x)
+            total += (self.ce(logits, y) + self.mse(val, v)).double()
+            batches += 1
+        return float(total.item()) / max(1, batches)
+
+    def step_scheduler(self):
+        self.scheduler.step()

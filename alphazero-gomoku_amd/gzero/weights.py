@@ -24,9 +24,10 @@ class _Block(nn.Module):
 
     def __init__(self, ch):
         super().__init__()
+        # registration order of the reference (parameters() order feeds clip_grad_norm_'s sum)
         self.conv1 = nn.Conv2d(ch, ch, 3, padding=1)
-        self.bn1 = nn.BatchNorm2d(ch)
         self.conv2 = nn.Conv2d(ch, ch, 3, padding=1)
+        self.bn1 = nn.BatchNorm2d(ch)
         self.bn2 = nn.BatchNorm2d(ch)
 
     def forward(self, x):
@@ -59,6 +60,22 @@ class PolicyValueNet(nn.Module):
         return logits, torch.tanh(self.value_fc2(v))
 
 
+def _init_order(state):
+    """Draw order of init_state_dict: residual blocks as conv1, bn1, conv2, bn2 (the
+    order the fixtures were generated in), whatever the module registration order."""
+    rank = {"conv1": 0, "bn1": 1, "conv2": 2, "bn2": 3}
+    items = list(state.items())
+    first = {}
+    keys = []
+    for i, (name, _) in enumerate(items):
+        p = name.split(".")
+        if p[0] == "residual_tower":
+            keys.append((first.setdefault(p[1], i), rank[p[2]], i))
+        else:
+            keys.append((i, 0, i))
+    return [items[k[2]] for k in sorted(keys)]
+
+
 def init_state_dict(seed=0, bn_noise=True):
     """Deterministic weights from numpy's default_rng(seed), identical on every
     machine (torch's CPU RNG is not used).  Uniform(+-1/sqrt(fan_in)) like
@@ -67,7 +84,7 @@ def init_state_dict(seed=0, bn_noise=True):
     rng = np.random.default_rng(seed)
     net = PolicyValueNet()
     sd = {}
-    for name, t in net.state_dict().items():
+    for name, t in _init_order(net.state_dict()):
         shape = tuple(t.shape)
         if name.endswith("num_batches_tracked"):
             sd[name] = torch.zeros((), dtype=torch.long)

@@ -53,7 +53,7 @@ typedef struct gz_search_params {
     double exploration;      /* params["exploration"] */
     double beta;             /* constructor beta: weight of tanh(pattern/1e4) in UCB */
     uint64_t seed;           /* RNG streams (gzero/rng.py) */
-    int32_t planner_steps;   /* BG-planner plies per rollout: only 0 is implemented */
+    int32_t planner_steps;   /* BG-planner plies per rollout (> 0: gz_plan_search / gz_selfplay_plan_run) */
     int32_t flags;           /* GZ_FLAG_* */
 } gz_search_params;
 
@@ -198,6 +198,22 @@ size_t gz_planner_move_workspace_bytes(int32_t n);
 int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_ai, const uint64_t* d_keys, int32_t n,
                     const gz_planner_params* pp, const float* d_gn_weights, void* d_workspace,
                     int32_t* d_moves, uint32_t* d_draws, void* stream);
+
+/* ---- K8 training-set materialisation (GomokuSelfPlayDataset, training.py:104-134;
+ * augment_sample, training.py:44-71).  Samples [0, n) are the records as is;
+ * sample n + 8j + 2k + f is record d_sel[j] under rot90^k (np.rot90, axes (1,2))
+ * then, if f, np.flip(axis=2).  Outputs: d_x float32 [n+8m][3][15][15] planes
+ * [black, white, empty]; d_y int64 move labels (the reference's label map, which
+ * rotates the other way, unless GZ_AUG_FIX_LABELS); d_v float32 z.  d_sel values
+ * must lie in [0, n) (others give zero planes and label -1). */
+#define GZ_AUG_FIX_LABELS 1
+int gz_dataset_build(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m, int32_t flags,
+                     float* d_x, int64_t* d_y, float* d_v, void* stream);
+/* The samples d_ids[0..count) of that dataset (a training batch, e.g. a DataLoader
+ * permutation slice) without materialising the rest: outputs [count][...].
+ * Ids outside [0, n+8m) give zero planes and label -1. */
+int gz_dataset_gather(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m, const int64_t* d_ids,
+                      int64_t count, int32_t flags, float* d_x, int64_t* d_y, float* d_v, void* stream);
 
 #ifdef __cplusplus
 }

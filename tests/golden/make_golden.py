@@ -872,9 +872,90 @@ def part_planner_mcts():
     dump("planner_mcts", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
 
 
+# ---------------------------------------------------------------------------
+# G9 dataset + SGD (training.py:104-134,277-337,430-454): the dataset's sample
+# order / labels / planes, and two epochs of training.main's optimiser loop
+# ---------------------------------------------------------------------------
+
+SGD_SEED = 31
+
+
+def sgd_records(n=200):
+    """Seeded replay records: (cells before the move, move, player, z)."""
+    import random as pyrandom
+    rng = pyrandom.Random(SGD_SEED)
+    recs = []
+    while len(recs) < n:
+        L = rng.randint(0, 120)
+        mv = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.5) if L else []
+        cells = [0] * 225
+        for i, m in enumerate(mv):
+            cells[m] = 1 + (i % 2)
+        empty = [i for i in range(225) if cells[i] == 0]
+        recs.append({"cells": "".join(map(str, cells)), "move": rng.choice(empty), "player": 1 + (L % 2),
+                     "z": rng.choice([-1, 0, 1])})
+    return recs
+
+
+def part_sgd():
+    import base64
+    import random as pyrandom
+    import numpy as np
+    import torch
+    from torch.utils.data import DataLoader, Subset
+    from gzero import weights
+    h = ref()
+    recs = sgd_records()
+    replay = h.tr.SimpleReplay()
+    for r in recs:
+        c = np.array([int(ch) for ch in r["cells"]], np.int64).reshape(15, 15)
+        planes = np.stack([(c == 1), (c == 2), (c == 0)]).astype(np.float32)
+        replay.add(planes, r["move"], r["player"])
+        replay.outcomes.append(r["z"])
+    rnd = pyrandom.Random(SGD_SEED + 1)
+    h.tr.random = rnd
+    ds = h.tr.GomokuSelfPlayDataset(replay, use_augmentation=True, augment_ratio=0.35)
+    labels = [int(s[1]) for s in ds.samples]
+    values = [float(s[2]) for s in ds.samples]
+    planes_crc = zlib.crc32(b"".join(np.ascontiguousarray(s[0], np.float32).tobytes() for s in ds.samples))
+    n = len(ds)
+    idx = list(range(n))
+    rnd.shuffle(idx)
+    split = int(n * 0.9)
+    train_idx, val_idx = idx[:split], idx[split:]
+    sd = weights.init_state_dict(seed=7)
+    path = os.path.join(os.getcwd(), "pv_sgd.pth")
+    torch.save({"model_state_dict": sd, "model_type": "alphazero_gomoku", "board_size": 15, "device": "cpu"}, path)
+    model = h.nn.GomokuModel(model_path=path, board_size=15, device="cpu")
+    torch.manual_seed(SGD_SEED + 2)
+    train_loader = DataLoader(Subset(ds, train_idx), batch_size=128, shuffle=True)
+    val_loader = DataLoader(Subset(ds, val_idx), batch_size=128, shuffle=False)
+    opt = torch.optim.Adam(model.model.parameters(), lr=8e-4, weight_decay=1e-5)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=2, gamma=0.85)
+    import io
+    import contextlib
+    tl, vl = [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for ep in range(2):
+            tl.append(h.tr.train_epoch(model, train_loader, opt, torch.device("cpu"), grad_clip=0.8))
+            vl.append(h.tr.validate_epoch(model, val_loader, torch.device("cpu")))
+    sched.step()
+    stats = {}
+    sample = {}
+    for k, t in model.model.state_dict().items():
+        a = t.detach().double().numpy().reshape(-1)
+        stats[k] = [float(a.sum()), float((a * a).sum())]
+        sample[k] = base64.b64encode(t.detach().float().numpy().reshape(-1)[::max(1, a.size // 64)][:64].tobytes()).decode()
+    dump("sgd", {"seed": SGD_SEED, "records": recs, "sel_seed": SGD_SEED + 1, "torch_seed": SGD_SEED + 2,
+                 "n_samples": n, "labels": labels, "values": values, "planes_crc32": planes_crc,
+                 "train_idx": train_idx, "val_idx": val_idx, "train_loss": tl, "val_loss": vl,
+                 "param_stats": stats, "param_sample_f32_b64": sample, "lr_after": sched.get_last_lr()})
+
+
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
          "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "augment": part_augment,
-         "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts}
+         "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
+         "sgd": part_sgd}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(PARTS)

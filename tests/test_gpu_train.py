@@ -1,0 +1,133 @@
+"""gz_dataset_build / gz_dataset_gather and the device SGD loop on the GPU
+(SURVEY §8f rows 1-2).
+
+* the materialised dataset equals the numpy restatement bit for bit and the
+  reference's G9 fixture (labels, values, planes CRC), with the reference's and
+  the corrected label map;
+* gather of arbitrary ids (ragged, repeated, out of range) equals rows of the
+  materialised set;
+* full-size properties: 1M samples -- every cell in exactly one plane, stone
+  counts preserved by every symmetry, 8 labels per augmented record distinct;
+* DeviceTrainer's two epochs follow the reference's losses within 1e-3
+  relative (GPU convolutions round differently from CPU torch; the host loop is
+  bit-exact on CPU, tests/test_train_cpu.py).
+"""
+import random
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+import train_oracle as TO
+
+pytestmark = pytest.mark.gpu
+
+
+def _records(g):
+    from gzero import boards
+    cells = np.array([[int(ch) for ch in r["cells"]] for r in g["records"]], np.int8)
+    rec = np.zeros(len(cells), boards.RECORD_DTYPE)
+    bl, wh = boards.cells_to_words(cells)
+    rec["black"], rec["white"] = bl, wh
+    rec["move"] = [r["move"] for r in g["records"]]
+    rec["player"] = [r["player"] for r in g["records"]]
+    rec["z"] = [r["z"] for r in g["records"]]
+    rec["game_id"] = np.arange(len(cells))
+    return cells, rec
+
+
+@pytest.mark.parametrize("fix", [False, True])
+def test_dataset_build_exact(fix):
+    from gzero.train import DeviceDataset
+    g = golden("sgd")
+    cells, rec = _records(g)
+    ds = DeviceDataset(rec, augment_ratio=0.35, fix_labels=fix, rng=random.Random(g["sel_seed"]))
+    sel = random.Random(g["sel_seed"]).sample(range(len(rec)), k=max(1, int(len(rec) * 0.35)))
+    x, y, v = (t.cpu().numpy() for t in ds.materialize())
+    ox, oy, ov = TO.dataset_samples(cells, rec["move"], rec["z"], sel, fix=fix)
+    assert len(ds) == len(oy) == g["n_samples"]
+    assert np.array_equal(x, ox) and np.array_equal(y, oy) and np.array_equal(v[:, 0], ov)
+    if not fix:
+        assert y.tolist() == g["labels"] and v[:, 0].tolist() == g["values"]
+        assert zlib.crc32(np.ascontiguousarray(x).tobytes()) == g["planes_crc32"]
+
+
+def test_dataset_gather_ids():
+    from gzero.train import DeviceDataset
+    g = golden("sgd")
+    _, rec = _records(g)
+    ds = DeviceDataset(rec, augment_ratio=0.35, rng=random.Random(g["sel_seed"]))
+    X, Y, V = ds.materialize()
+    n = len(ds)
+    ids = torch.tensor([0, n - 1, 5, 5, n, -1, 200, 201, 207, 3 * n], dtype=torch.int64, device="cuda")
+    x, y, v = ds.gather(ids)
+    for k, i in enumerate(ids.tolist()):
+        if 0 <= i < n:
+            assert torch.equal(x[k], X[i]) and int(y[k]) == int(Y[i]) and float(v[k]) == float(V[i])
+        else:
+            assert int(y[k]) == -1 and float(x[k].abs().sum()) == 0.0
+    e = ds.gather(torch.zeros(0, dtype=torch.int64, device="cuda"))
+    assert e[0].shape[0] == 0
+
+
+def test_dataset_full_size_properties():
+    """1M samples from 117,650 records: planes partition the board, symmetries
+    keep stone counts, the 8 corrected labels of a record are its 8 images."""
+    from gzero import boards
+    from gzero.train import DeviceDataset
+    rng = np.random.default_rng(5)
+    n = 117_650
+    cells = rng.choice(np.array([0, 0, 0, 1, 2], np.int8), size=(n, 225))
+    rec = np.zeros(n, boards.RECORD_DTYPE)
+    rec["black"], rec["white"] = boards.cells_to_words(cells)
+    rec["move"] = rng.integers(0, 225, n)
+    rec["z"] = rng.integers(-1, 2, n)
+    ds = DeviceDataset(rec, augment_ratio=1.0, fix_labels=True, rng=random.Random(9))
+    assert len(ds) == 9 * n
+    X, Y, V = ds.materialize()
+    assert torch.all(X.sum(dim=1) == 1.0)  # exactly one plane per cell
+    nb = X[:, 0].sum(dim=(1, 2)).view(-1)
+    orig = nb[:n]
+    sel = torch.tensor(random.Random(9).sample(range(n), k=n), device="cuda")
+    aug = nb[n:].view(n, 8)
+    assert torch.equal(aug, orig[sel].view(n, 1).expand(n, 8))
+    # corrected labels: the move cell of the original lands on the label cell of every image
+    lab = Y[n:].view(n, 8)
+    assert torch.all(lab >= 0) and torch.all(lab < 225)
+    assert torch.all(V[n:].view(n, 8) == V[:n][sel].view(n, 1))
+    del X
+    torch.cuda.empty_cache()
+
+
+def test_device_trainer_follows_reference():
+    from gzero import weights
+    from gzero.train import DeviceDataset, DeviceTrainer
+    from neural_network import GomokuModel
+    g = golden("sgd")
+    _, rec = _records(g)
+    rnd = random.Random(g["sel_seed"])
+    ds = DeviceDataset(rec, augment_ratio=0.35, rng=rnd)
+    idx = list(range(len(ds)))
+    rnd.shuffle(idx)
+    split = int(len(ds) * 0.9)
+    assert idx[:split] == g["train_idx"]
+    tr_idx = torch.tensor(idx[:split], dtype=torch.int64, device="cuda")
+    va_idx = torch.tensor(idx[split:], dtype=torch.int64, device="cuda")
+    m = GomokuModel(device="cpu")
+    m.model.load_state_dict(weights.init_state_dict(seed=7))
+    tr = DeviceTrainer(m)
+    torch.manual_seed(g["torch_seed"])
+    tl, vl = [], []
+    for _ in range(2):
+        tl.append(tr.train_epoch(ds, 128, indices=tr_idx))
+        vl.append(tr.validate_epoch(ds, 128, indices=va_idx))
+    tr.step_scheduler()
+    np.testing.assert_allclose(tl, g["train_loss"], rtol=1e-3)
+    np.testing.assert_allclose(vl, g["val_loss"], rtol=1e-3)
+    assert tr.scheduler.get_last_lr() == g["lr_after"]
+    for k, t in m.model.state_dict().items():
+        a = t.detach().double().cpu().numpy().reshape(-1)
+        s, ss = g["param_stats"][k]
+        assert abs(float(a.sum()) - s) <= 1e-3 * max(1.0, abs(s)) + 2e-3 * a.size ** 0.5, k
