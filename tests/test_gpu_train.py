@@ -7,7 +7,7 @@
 * gather of arbitrary ids (ragged, repeated, out of range) equals rows of the
   materialised set;
 * full-size properties: 1M samples -- every cell in exactly one plane, stone
-  counts preserved by every symmetry, 8 labels per augmented record distinct;
+  counts and values preserved by every symmetry, corrected labels on sampled rows;
 * DeviceTrainer's two epochs follow the reference's losses within 1e-3
   relative (GPU convolutions round differently from CPU torch; the host loop is
   bit-exact on CPU, tests/test_train_cpu.py).
@@ -74,7 +74,7 @@ def test_dataset_gather_ids():
 
 def test_dataset_full_size_properties():
     """1M samples from 117,650 records: planes partition the board, symmetries
-    keep stone counts, the 8 corrected labels of a record are its 8 images."""
+    keep stone counts and values, corrected labels are the move's 8 images."""
     from gzero import boards
     from gzero.train import DeviceDataset
     rng = np.random.default_rng(5)
@@ -93,9 +93,12 @@ def test_dataset_full_size_properties():
     sel = torch.tensor(random.Random(9).sample(range(n), k=n), device="cuda")
     aug = nb[n:].view(n, 8)
     assert torch.equal(aug, orig[sel].view(n, 1).expand(n, 8))
-    # corrected labels: the move cell of the original lands on the label cell of every image
-    lab = Y[n:].view(n, 8)
-    assert torch.all(lab >= 0) and torch.all(lab < 225)
+    # corrected labels = the image of the move cell under each symmetry (sampled rows)
+    lab = Y[n:].view(n, 8).cpu().numpy()
+    sel_h = sel.cpu().numpy()
+    for j in np.random.default_rng(6).integers(0, n, 2000):
+        mv = int(rec["move"][sel_h[j]])
+        assert [TO.transform_index(mv, k, f, fix=True) for k in range(4) for f in (False, True)] == lab[j].tolist()
     assert torch.all(V[n:].view(n, 8) == V[:n][sel].view(n, 1))
     del X
     torch.cuda.empty_cache()
