@@ -73,31 +73,43 @@ class AlphaZeroGomokuAI:
 
     def get_move(self, board: GomokuBoard) -> Optional[Tuple[int, int]]:
         """ai_agent.py:109-136 (opening book, MCTS, exploration) on the GPU."""
-        if not board.get_valid_moves():
-            return None
+        return self.get_moves([board], [self.game_id])[0]
+
+    def get_moves(self, boards: List[GomokuBoard], game_ids: List[int]) -> List[Optional[Tuple[int, int]]]:
+        """get_move for many boards in one batched search: board i draws from the
+        streams of (self.seed, game_ids[i]), so the result equals get_move on each
+        board with ``game_id = game_ids[i]``."""
         t0 = time.time()
-        needs_search = board.get_move_count() >= 6
-        gather = self.compute_priors and needs_search
-        if needs_search:
-            p = self._search_params(gather)
-        else:  # openings draw no simulation
-            p = device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
-                                     self.params["exploration"], self.beta, self.seed, 100, 0, False)
-        cap = p.num_simulations + 1 if gather else 0
-        if needs_search and self.planner_steps and p.num_simulations > 0:
-            mv, stats, _, leaves = device.plan_search(board.to_state(), [self.game_id], p,
-                                                      self.bg_planner.planner_params(),
-                                                      self.bg_planner.device_weights(), leaf_cap=cap)
-        else:
-            mv, stats, _, leaves = device.search(board.to_state(), [self.game_id], p, leaf_cap=cap)
-        if gather and leaves is not None and len(leaves):
-            from gzero import boards
-            self.model.predict_batch(boards.words_to_cells(leaves[:, :8], leaves[:, 8:]))
+        out = [None] * len(boards)
+        groups = {}  # openings (< 6 plies) draw no simulation; the rest search
+        for i, b in enumerate(boards):
+            if b.get_valid_moves():
+                groups.setdefault(b.get_move_count() >= 6, []).append(i)
+        for needs_search, idx in sorted(groups.items()):
+            gather = self.compute_priors and needs_search
+            if needs_search:
+                p = self._search_params(gather)
+            else:
+                p = device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
+                                         self.params["exploration"], self.beta, self.seed, 100, 0, False)
+            cap = (p.num_simulations + 1) * len(idx) if gather else 0
+            states = np.concatenate([boards[i].to_state() for i in idx])
+            gids = [int(game_ids[i]) for i in idx]
+            if needs_search and self.planner_steps and p.num_simulations > 0:
+                mv, stats, _, leaves = device.plan_search(states, gids, p, self.bg_planner.planner_params(),
+                                                          self.bg_planner.device_weights(), leaf_cap=cap)
+            else:
+                mv, stats, _, leaves = device.search(states, gids, p, leaf_cap=cap)
+            if gather and leaves is not None and len(leaves):
+                from gzero import boards as gb
+                self.model.predict_batch(gb.words_to_cells(leaves[:, :8], leaves[:, 8:]))
+            for k, i in enumerate(idx):
+                m = int(mv[k])
+                out[i] = None if m < 0 else (m // 15, m % 15)
+            self.last_search_stats = stats[-1]
         self._last_decision_time = time.time() - t0
-        self.last_search_stats = stats[0]
-        self.games_played += 1
-        m = int(mv[0])
-        return None if m < 0 else (m // 15, m % 15)
+        self.games_played += len(boards)
+        return out
 
     def evaluate_position(self, board: GomokuBoard) -> float:
         if board.game_over:

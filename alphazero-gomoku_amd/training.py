@@ -185,6 +185,88 @@ def selfplay(n_games: int, num_simulations: int = 200, difficulty: str = "medium
                     "game_slices": slices}
 
 
+# ---------------------------------------------------------------- arena (training.py:221-270)
+
+
+class RandomAgent:
+    """evaluate_model's opponent when there is no baseline: random.choice(valid),
+    drawn from the (seed, game_id, ply, 0) stream."""
+
+    def __init__(self, seed: int = 0, game_id: int = 0):
+        self.seed, self.game_id = int(seed), int(game_id)
+
+    def get_move(self, board: GomokuBoard):
+        from gzero import rng
+        v = board.get_valid_moves()
+        if not v:
+            return None
+        return rng.Stream(rng.stream_key(self.seed, self.game_id, board.get_move_count(), 0)).choice(v)
+
+
+def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficulty: str = "easy",
+                   eval_num_sim: int = 60, eval_plans: int = 2, seed: Optional[int] = None,
+                   return_games: bool = False, alternate: bool = True):
+    """training.py:221-270 with all ``games`` played at once: every ply, the games
+    whose side to move belongs to the same agent are searched in ONE batched GPU
+    call (AlphaZeroGomokuAI.get_moves).  As in the reference the evaluated model
+    alternates colours (black in even games), its AI uses ``eval_num_sim``
+    simulations only when there is no baseline (otherwise the difficulty's own
+    count; the baseline's AI uses ``eval_num_sim``), both with ``eval_plans``
+    planner plies, and a missing move ends the game as a draw.  Game g draws from
+    the streams of (seed_a / seed_b, g): the result equals playing the games one
+    by one with per-game AIs of those seeds and ``game_id = g``.  ``alternate=False``
+    keeps the evaluated model on black in every game -- what training.main's six
+    ``evaluate_model(..., games=1)`` calls amount to (training.py:484-492)."""
+    from ai_agent import AlphaZeroGomokuAI
+    seed = random.getrandbits(64) if seed is None else int(seed)
+    seed_a, seed_b = seed, (seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
+    # one AI object per (agent, colour): the colour is the AI's player in the search
+    ai_a, ai_b = {}, {}
+    for color in (GomokuBoard.BLACK, GomokuBoard.WHITE):
+        a = AlphaZeroGomokuAI(color, difficulty=eval_difficulty, planner_steps=eval_plans, seed=seed_a)
+        a.model = current
+        if baseline is None:
+            a.params = dict(a.params, num_simulations=eval_num_sim)
+            b = RandomAgent(seed_b)
+        else:
+            b = AlphaZeroGomokuAI(color, difficulty=eval_difficulty, planner_steps=eval_plans, seed=seed_b)
+            b.params = dict(b.params, num_simulations=eval_num_sim)
+            b.model = baseline
+        ai_a[color], ai_b[color] = a, b
+    boards = [GomokuBoard() for _ in range(games)]
+    color_a = [GomokuBoard.BLACK if (g % 2 == 0 or not alternate) else GomokuBoard.WHITE for g in range(games)]
+    active = list(range(games))
+    moves = [[] for _ in range(games)]
+    while active:
+        groups = {}
+        for g in active:
+            cp = boards[g].current_player
+            who = "a" if cp == color_a[g] else "b"
+            groups.setdefault((who, cp), []).append(g)
+        stopped = set()
+        for (who, cp), gs in groups.items():
+            agent = (ai_a if who == "a" else ai_b)[cp]
+            if isinstance(agent, RandomAgent):
+                mv = [RandomAgent(agent.seed, g).get_move(boards[g]) for g in gs]
+            else:
+                mv = agent.get_moves([boards[g] for g in gs], gs)
+            for g, m in zip(gs, mv):
+                if m is None:
+                    stopped.add(g)
+                    continue
+                boards[g].make_move(*m)
+                moves[g].append(m[0] * 15 + m[1])
+        active = [g for g in active if g not in stopped and not boards[g].game_over]
+    wins = sum(1 for g in range(games) if boards[g].winner is not None and boards[g].winner == color_a[g])
+    draws = sum(1 for g in range(games) if boards[g].winner is None)
+    losses = games - wins - draws
+    out = {"wins": wins, "losses": losses, "draws": draws, "win_rate": wins / max(1, games)}
+    if return_games:
+        out["games"] = [{"moves": moves[g], "winner": boards[g].winner, "color_a": color_a[g]} for g in range(games)]
+        out["seeds"] = (seed_a, seed_b)
+    return out
+
+
 # ---------------------------------------------------------------- SGD (training.py:277-337)
 
 
@@ -218,3 +300,147 @@ def validate_epoch(model, loader, device, epoch_index: int = 1, num_epochs: int 
             total += float((ce(logits, y_p) + mse(v, y_v)).item())
             batches += 1
     return total / max(1, batches)
+
+
+# ---------------------------------------------------------------- training.main (training.py:361-537)
+
+
+def _render_bar(pct: float, width: int = 20) -> str:
+    k = int(round(max(0.0, min(1.0, pct)) * width))
+    return "[" + "#" * k + "-" * (width - k) + "]"
+
+
+def _fmt_duration(seconds: float) -> str:
+    seconds = int(max(0, seconds))
+    h, r = divmod(seconds, 3600)
+    m, s = divmod(r, 60)
+    return f"{h}h{m:02d}m{s:02d}s" if h else (f"{m}m{s:02d}s" if m else f"{s}s")
+
+
+def run_iteration(model, trainer, it: int, games_per_iteration: int = 10, num_simulations: int = 200,
+                  difficulty: str = "medium", beta: float = 0.2, planner_steps: int = 5, seed: int = 0,
+                  train_split: float = 0.9, batch_size: int = 128, epochs: int = 2, augment_ratio: float = 0.35,
+                  planner=None, verbose: bool = True) -> dict:
+    """One iteration of training.main on the device (training.py:399-480):
+    self-play of ``games_per_iteration`` games per rank (ids sharded by rank,
+    records all-gathered so every rank holds the same replay), the dataset with
+    35 % 8-fold augmentation, a 90/10 split drawn from ``random``, ``epochs``
+    epochs of the data-parallel SGD step and the StepLR step."""
+    from gzero import dist as gdist
+    from gzero.train import DeviceDataset, records_to_device
+    rank, ws = gdist.world()
+    t0 = time.time()
+    replay_base = (it * ws + rank) * games_per_iteration
+    rep, st = selfplay(games_per_iteration, num_simulations=num_simulations, difficulty=difficulty, beta=beta,
+                       seed=seed, game_id_base=replay_base, model=model, planner_steps=planner_steps,
+                       planner=planner)
+    recs = _replay_records(rep)
+    d = records_to_device(recs) if len(recs) else torch.zeros(0, dtype=torch.uint8, device="cuda")
+    if ws > 1:
+        d = gdist.all_gather_records(d, len(recs))
+    n_rec = d.numel() // 80
+    t1 = time.time()
+    out = {"iteration": it, "records": n_rec, "selfplay_s": t1 - t0, "moves_played": st["moves_played"] * ws}
+    if n_rec == 0:
+        return dict(out, skipped=True)
+    ds = DeviceDataset(d, use_augmentation=True, augment_ratio=augment_ratio, n_records=n_rec)
+    if len(ds) < 8:  # training.py:431-433
+        return dict(out, skipped=True)
+    n = len(ds)
+    idx = list(range(n))
+    random.shuffle(idx)
+    split = int(n * train_split)
+    tr_idx = torch.tensor(idx[:split], dtype=torch.int64, device="cuda")
+    va_idx = torch.tensor(idx[split:], dtype=torch.int64, device="cuda")
+    tl, vl = [], []
+    for ep in range(epochs):
+        tl.append(trainer.train_epoch(ds, batch_size, indices=tr_idx))
+        vl.append(trainer.validate_epoch(ds, batch_size, indices=va_idx))
+        if verbose and rank == 0:
+            print(f"    ├── 模型训练: {_render_bar((ep + 1) / epochs, 12)} epoch {ep + 1}/{epochs} "
+                  f"train {tl[-1]:.3f} val {vl[-1]:.3f}")
+    trainer.step_scheduler()
+    model.eval_mode()
+    t2 = time.time()
+    return dict(out, samples=n, train_loss=float(np.mean(tl)), val_loss=float(np.mean(vl)), sgd_s=t2 - t1)
+
+
+def _replay_records(rep: "SimpleReplay"):
+    """SimpleReplay -> device record layout (gzero.boards.RECORD_DTYPE)."""
+    from gzero import boards
+    n = len(rep)
+    rec = np.zeros(n, boards.RECORD_DTYPE)
+    if n:
+        planes = np.stack(rep.states)
+        cells = (planes[:, 0] > 0.5).astype(np.int8) + 2 * (planes[:, 1] > 0.5).astype(np.int8)
+        rec["black"], rec["white"] = boards.cells_to_words(cells.reshape(n, 225))
+        rec["move"] = rep.move_indices
+        rec["player"] = rep.players
+        rec["z"] = rep.outcomes
+    return rec
+
+
+def main(iterations: int = 6, games_per_iteration: int = 10, seed: Optional[int] = None, models_dir: str = "models",
+         num_simulations: int = 200, planner_steps: int = 5, eval_games: int = 6):
+    """training.main (training.py:361-537) on the MI355X engine: same loop, the
+    same hyper-parameters (Adam 8e-4 / wd 1e-5, StepLR(2, 0.85), clip 0.8,
+    batch 128, 2 epochs, 35 % augmentation, 90/10 split, patience 3, 6 arena
+    games) and the same checkpoint names.  Under torchrun every rank plays its
+    own games and trains data-parallel (gzero.train.DeviceTrainer)."""
+    import math
+    import os
+    from gzero import dist as gdist
+    from gzero.train import DeviceTrainer
+    from neural_network import GomokuModel
+    rank, ws = gdist.init_from_env()
+    seed = int(seed if seed is not None else 20240101)
+    random.seed(seed)  # every rank draws the same dataset / split / shuffles
+    torch.manual_seed(seed)
+    if rank == 0:
+        os.makedirs(models_dir, exist_ok=True)
+    model = GomokuModel(model_path=None, board_size=15, device="cuda")
+    trainer = DeviceTrainer(model)
+    best_val, patience, patience_count = math.inf, 3, 0
+    best_snapshot = None
+    t0 = time.time()
+    history = []
+    for it in range(1, iterations + 1):
+        res = run_iteration(model, trainer, it, games_per_iteration, num_simulations=num_simulations,
+                            planner_steps=planner_steps, seed=seed, verbose=rank == 0)
+        if res.get("skipped"):
+            if rank == 0:
+                print("自我对弈样本过少，跳过本轮训练。")
+            continue
+        if rank == 0:
+            model.save_model(os.path.join(models_dir, f"alphazero_gomoku_iter_{it}.pth"))
+        improved = res["val_loss"] < best_val
+        if improved:
+            best_val, patience_count = res["val_loss"], 0
+            best_path = os.path.join(models_dir, "alphazero_gomoku_best.pth")
+            if rank == 0:
+                model.save_model(best_path)
+            best_snapshot = GomokuModel(board_size=15, device="cuda")
+            best_snapshot.model.load_state_dict(model.model.state_dict())
+            best_snapshot.eval_mode()
+        else:
+            patience_count += 1
+        stats = evaluate_model(model, best_snapshot, games=eval_games, seed=seed + it, alternate=False) \
+            if rank == 0 else {}
+        res.update(eval=stats, elapsed=time.time() - t0)
+        history.append(res)
+        if rank == 0:
+            pct = it / iterations
+            print(f"📊 {_render_bar(pct)} {int(pct * 100)}% | {_fmt_duration(res['elapsed'])} | "
+                  f"records {res['records']} | loss {res['val_loss']:.3f} | win rate "
+                  f"{100.0 * stats.get('win_rate', 0.0):.1f}%")
+        if patience_count >= patience:
+            if rank == 0:
+                print("触发早停条件，结束训练。")
+            break
+    if rank == 0:
+        model.save_model(os.path.join(models_dir, "alphazero_gomoku_final.pth"))
+    return history
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,66 @@
+"""Batched arena (training.evaluate_model, training.py:221-270).
+
+evaluate_model plays all games at once, one batched search per (agent, colour)
+per ply.  Each game must equal the same game played alone through the
+one-board API (AlphaZeroGomokuAI.get_move, pinned to the oracle and the
+reference's fixtures by test_gpu_api / test_gpu_plan) with per-game AIs of the
+same seeds and ``game_id = g`` -- which pins the batching: grouping, stream
+keys, colours, simulation counts and the draw / stop rules.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 77
+
+
+def _play_alone(current, baseline, g, seeds, sims_a, sims_b, plans=2):
+    from ai_agent import AlphaZeroGomokuAI
+    from gomoku_board import GomokuBoard
+    from training import RandomAgent
+    color_a = GomokuBoard.BLACK if g % 2 == 0 else GomokuBoard.WHITE
+    other = GomokuBoard.WHITE if color_a == GomokuBoard.BLACK else GomokuBoard.BLACK
+    a = AlphaZeroGomokuAI(color_a, "easy", planner_steps=plans, seed=seeds[0], game_id=g)
+    a.model = current
+    a.params = dict(a.params, num_simulations=sims_a)
+    if baseline is None:
+        b = RandomAgent(seeds[1], g)
+    else:
+        b = AlphaZeroGomokuAI(other, "easy", planner_steps=plans, seed=seeds[1], game_id=g)
+        b.model = baseline
+        b.params = dict(b.params, num_simulations=sims_b)
+    board = GomokuBoard()
+    moves = []
+    while not board.game_over:
+        agent = a if board.current_player == color_a else b
+        m = agent.get_move(board)
+        if m is None:
+            break
+        board.make_move(*m)
+        moves.append(m[0] * 15 + m[1])
+    return moves, board.winner
+
+
+def test_arena_vs_random_equals_games_alone():
+    from neural_network import GomokuModel
+    from training import evaluate_model
+    cur = GomokuModel(device="cpu")
+    res = evaluate_model(cur, None, games=4, eval_num_sim=12, seed=SEED, return_games=True)
+    for g, rec in enumerate(res["games"]):
+        mv, w = _play_alone(cur, None, g, res["seeds"], 12, None)
+        assert rec["moves"] == mv and rec["winner"] == w, g
+        assert len(mv) >= 9 and w is not None  # five in a row needs 9 plies; random play loses
+    assert res["wins"] + res["losses"] + res["draws"] == 4
+
+
+def test_arena_vs_baseline_equals_games_alone():
+    """With a baseline the evaluated AI keeps the difficulty's simulation count
+    (easy: 100) and only the baseline's AI runs eval_num_sim (training.py:238-247)."""
+    from neural_network import GomokuModel
+    from training import evaluate_model
+    cur, base = GomokuModel(device="cpu"), GomokuModel(device="cpu")
+    res = evaluate_model(cur, base, games=2, eval_num_sim=10, seed=SEED + 1, return_games=True)
+    for g, rec in enumerate(res["games"]):
+        mv, w = _play_alone(cur, base, g, res["seeds"], 100, 10)
+        assert rec["moves"] == mv and rec["winner"] == w, g
+        assert len(mv) >= 9, g
