@@ -321,10 +321,8 @@ extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, i
     }
     if (n == 0) return GZ_OK;
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-    }
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
     int grid = n < 2 * cus ? n : 2 * cus;
     gn_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(d_weights, d_boards, n, d_count, d_p, d_q, d_logits);
     hipError_t e = hipGetLastError();

@@ -633,10 +633,8 @@ extern "C" size_t gz_pv_weight_floats(void) { return (size_t)TOTAL; }
 
 static int pv_grid(int n) {
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-    }
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
     return n < cus ? n : cus;
 }
 

@@ -10,9 +10,12 @@
 // the label follows the reference's _transform_index (training.py:53-61),
 // which rotates the other way -- kept bit for bit unless GZ_AUG_FIX_LABELS.
 //
-// HBM-bound byte work: one thread writes 4 consecutive floats of the flat
-// [S][675] plane array (16-B coalesced stores); the 80-byte record of a sample
-// is read by the ~169 threads that cover it (L1/L2 hits).
+// HBM-bound byte work (2,712 B written per sample): one thread per output cell
+// writes its three plane values; the 80-byte record of a sample is read by the
+// 225 threads that cover it (L1/L2 hits).  Measured 2.85 TB/s for the whole-set
+// build (nontemporal stores; plain stores 2.3 TB/s).  Slower, kept out: a
+// bounded grid-stride grid (1.9), 16-byte stores over 4-sample groups (2.2), a
+// wave per sample (2.2), 4 samples per thread with all loads first (2.3).
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -25,15 +28,14 @@ constexpr int N = 15;
 constexpr int POS = N * N;
 constexpr int SAMPLE_F = 3 * POS;  // 675 floats
 
-// source cell (row-major) of output cell (i, j) under flip(rot90^k(x))
+// source cell (row-major) of output cell (i, j) under flip(rot90^k(x));
+// y = rot90(x) reads y[i][j] = x[j][N-1-i], so rot90^k reads x at
+// k=0 (i, j), k=1 (j, N-1-i), k=2 (N-1-i, N-1-j), k=3 (N-1-j, i)
 __device__ __forceinline__ int aug_source(int i, int j, int k, int flip) {
     if (flip) j = N - 1 - j;
-    for (int t = 0; t < k; t++) {  // y = rot90(x): y[i][j] = x[j][N-1-i]
-        const int a = j, b = N - 1 - i;
-        i = a;
-        j = b;
-    }
-    return i * N + j;
+    const int a = (k == 0) ? i : (k == 1) ? j : (k == 2) ? N - 1 - i : N - 1 - j;
+    const int b = (k == 0) ? j : (k == 1) ? N - 1 - i : (k == 2) ? N - 1 - j : i;
+    return a * N + b;
 }
 
 // label of a move under the same symmetry (training.py:53-61, or the corrected map)
@@ -58,40 +60,44 @@ __device__ __forceinline__ SampleRef sample_ref(long long s, int n, const int32_
     return {sel[a >> 3], (int)((a & 7) >> 1), (int)(a & 1)};
 }
 
-__device__ __forceinline__ float plane_value(const gz_record* __restrict__ rec, int plane, int cell) {
-    const int bit = (cell / N) * 16 + cell % N;
-    const uint32_t b = (rec->black[bit >> 5] >> (bit & 31)) & 1u;
-    const uint32_t w = (rec->white[bit >> 5] >> (bit & 31)) & 1u;
-    const uint32_t v = plane == 0 ? b : (plane == 1 ? w : 1u - (b | w));
-    return (float)v;
-}
-
+// one thread per (sample, output cell): the source cell's two bits give the
+// three plane values, stored at cell, 225 + cell and 450 + cell of the sample
+// (consecutive lanes -> consecutive cells: coalesced 4-byte stores).  NT: the
+// whole-set build streams past the caches; a batch gather stays in L2 for the
+// forward that reads it next.
+template <bool NT>
 __global__ void dataset_planes_kernel(const gz_record* __restrict__ recs, int n, const int32_t* __restrict__ sel,
-                                      const int64_t* __restrict__ ids, long long n_all, long long total_f,
+                                      const int64_t* __restrict__ ids, long long n_all, long long count,
                                       float* __restrict__ x) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long e0 = t * 4;
-    if (e0 >= total_f) return;
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const long long e = e0 + u;
-        v[u] = 0.f;
-        if (e < total_f) {
-            const long long so = e / SAMPLE_F;
-            const int rem = (int)(e - so * SAMPLE_F);
-            const int plane = rem / POS, cell = rem % POS;
-            const long long s = ids ? ids[so] : so;
-            const SampleRef r = (unsigned long long)s < (unsigned long long)n_all ? sample_ref(s, n, sel)
-                                                                                 : SampleRef{-1, 0, 0};
-            if ((unsigned)r.rec < (unsigned)n)  // out-of-range selections give zero planes, label -1
-                v[u] = plane_value(recs + r.rec, plane, aug_source(cell / N, cell % N, r.k, r.flip));
+    const long long total = count * POS;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const long long so = t / POS;
+        const int cell = (int)(t - so * POS);
+        const long long s = ids ? ids[so] : so;
+        const SampleRef r =
+            (unsigned long long)s < (unsigned long long)n_all ? sample_ref(s, n, sel) : SampleRef{-1, 0, 0};
+        float b = 0.f, w = 0.f, e = 0.f;
+        if ((unsigned)r.rec < (unsigned)n) {  // out-of-range selections give zero planes, label -1
+            const int src = aug_source(cell / N, cell % N, r.k, r.flip);
+            const int bit = (src / N) * 16 + src % N;
+            const gz_record* rec = recs + r.rec;
+            const uint32_t bb = (rec->black[bit >> 5] >> (bit & 31)) & 1u;
+            const uint32_t ww = (rec->white[bit >> 5] >> (bit & 31)) & 1u;
+            b = (float)bb;
+            w = (float)ww;
+            e = (float)(1u - (bb | ww));
         }
-    }
-    if (e0 + 4 <= total_f) {
-        *(float4*)(x + e0) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-        for (int u = 0; u < 4 && e0 + u < total_f; u++) x[e0 + u] = v[u];
+        float* o = x + so * SAMPLE_F + cell;
+        if (NT) {
+            __builtin_nontemporal_store(b, o);
+            __builtin_nontemporal_store(w, o + POS);
+            __builtin_nontemporal_store(e, o + 2 * POS);
+        } else {
+            o[0] = b;
+            o[POS] = w;
+            o[2 * POS] = e;
+        }
     }
 }
 
@@ -112,7 +118,6 @@ __global__ void dataset_labels_kernel(const gz_record* __restrict__ recs, int n,
     val[so] = (float)rec->z;
 }
 
-
 }  // namespace
 
 extern "C" void gz_internal_set_error(const char* msg);
@@ -131,10 +136,15 @@ int launch(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t 
     }
     if (count == 0) return GZ_OK;
     const long long n_all = (long long)n + 8LL * m;
-    const long long total_f = count * SAMPLE_F;
     const int bs = 256;
-    const long long th = (total_f + 3) / 4;
-    dataset_planes_kernel<<<(unsigned)((th + bs - 1) / bs), bs, 0, st>>>(d_records, n, d_sel, d_ids, n_all, total_f, d_x);
+    long long th = count * POS;
+    if (th > (1LL << 30)) th = 1LL << 30;  // one thread per cell up to 4M blocks, grid-stride beyond
+    if (d_ids)
+        dataset_planes_kernel<false><<<(unsigned)((th + bs - 1) / bs), bs, 0, st>>>(d_records, n, d_sel, d_ids, n_all,
+                                                                                   count, d_x);
+    else
+        dataset_planes_kernel<true><<<(unsigned)((th + bs - 1) / bs), bs, 0, st>>>(d_records, n, d_sel, d_ids, n_all,
+                                                                                  count, d_x);
     dataset_labels_kernel<<<(unsigned)((count + bs - 1) / bs), bs, 0, st>>>(
         d_records, n, d_sel, d_ids, n_all, count, (flags & GZ_AUG_FIX_LABELS) ? 1 : 0, d_y, d_v);
     hipError_t e = hipGetLastError();

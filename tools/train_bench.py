@@ -22,6 +22,35 @@ sys.path[:0] = [os.path.join(REPO, "alphazero-gomoku_amd"), REPO]
 import torch  # noqa: E402
 
 
+def dataset_bench(n, reps=5):
+    """gz_dataset_build over n records with every record augmented (9n samples):
+    HBM-bound writes, 2,712 B out per sample (planes 2,700 + label 8 + value 4)."""
+    import random
+    import numpy as np
+    from gzero import boards
+    from gzero.train import DeviceDataset
+    rng = np.random.default_rng(1)
+    cells = rng.choice(np.array([0, 0, 0, 1, 2], np.int8), size=(n, 225))
+    rec = np.zeros(n, boards.RECORD_DTYPE)
+    rec["black"], rec["white"] = boards.cells_to_words(cells)
+    rec["move"] = rng.integers(0, 225, n)
+    ds = DeviceDataset(rec, augment_ratio=1.0, rng=random.Random(0))
+    ds.materialize()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = ds.materialize()
+        del out
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    s = len(ds)
+    byts = s * (2700 + 8 + 4) + n * 80
+    return {"records": n, "samples": s, "ms": ms, "GB_per_s": byts / ms / 1e6, "bytes": byts,
+            "note": "materialize() allocates its outputs inside the timed loop (caching allocator, no sync)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--games", type=int, default=256, help="self-play games per rank per iteration")
@@ -30,6 +59,8 @@ def main():
     ap.add_argument("--planner-steps", type=int, default=5)
     ap.add_argument("--eval-games", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dataset-records", type=int, default=0,
+                    help="also time gz_dataset_build on this many random records (x4.5 samples at ratio 0.35*10)")
     a = ap.parse_args()
     import random
     from gzero import dist as gdist
@@ -57,6 +88,7 @@ def main():
         if rank == 0:
             print(json.dumps({"progress": it, **{k: v for k, v in r.items() if not isinstance(v, dict)}}),
                   file=sys.stderr, flush=True)
+    dsb = dataset_bench(a.dataset_records) if a.dataset_records and rank == 0 else None
     ev = None
     if a.eval_games and rank == 0:
         t = time.time()
@@ -75,7 +107,7 @@ def main():
             "samples_per_iteration": sum(r.get("samples", 0) for r in its) / len(its),
             "config": {"games_per_rank": a.games, "sims": a.sims, "planner_steps": a.planner_steps,
                        "batch_per_rank": 128, "epochs": 2, "augment_ratio": 0.35},
-            "eval": ev, "dtype": "fp32 SGD (MIOpen), f16x3 self-play forwards",
+            "eval": ev, "dataset_kernel": dsb, "dtype": "fp32 SGD (MIOpen), f16x3 self-play forwards",
             "data": "synthetic: self-play from the empty board, random-init weights"}), flush=True)
 
 
