@@ -5,7 +5,8 @@
 // boards; two workgroups share a CU (LDS 76 KB each).  GraphNet's 64x225 map
 // stays in LDS as f16x3 hi/lo planes (gz_f16conv.h); every conv is an implicit
 // GEMM on v_mfma_f32_16x16x32_f16 in C^T form.  Wave w owns n-tiles
-// {2(w&1), 2(w&1)+1} x M tiles [4(w>>1), 4(w>>1)+4) (tile 15 = zero rows, unused).
+// {2(w&1), 2(w&1)+1} x M tiles [4(w>>1), 4(w>>1)+4), waves 6-7 three tiles (tile 15
+// would be zero rows only).
 // The embed conv reads 0/1 planes, exact in fp16, so it takes 2 MFMAs (w_hi, w_lo).
 // Heads (policy conv 1x1, FC 450->225, softmax) and the DQN MLP run on VALU.
 #include <hip/hip_runtime.h>
@@ -54,8 +55,9 @@ __device__ inline int pnbr(int m, int li, int dr, int dc) {
     return ok ? r * 15 + c : POS;
 }
 
-// epilogue: y = relu(acc + bias) for the wave's 2 n-tiles x NM M tiles
-__device__ __forceinline__ void gn_store(ActF16x3& act, const f32x4 (&acc)[2][NM], const float* __restrict__ bias,
+// epilogue: y = relu(acc + bias) for the wave's 2 n-tiles x NMW M tiles
+template <int NMW>
+__device__ __forceinline__ void gn_store(ActF16x3& act, const f32x4 (&acc)[2][NMW], const float* __restrict__ bias,
                                          int np, int m0, int lane) {
     asm volatile("" : "+v"(lane));
     lane &= 63;
@@ -66,10 +68,64 @@ __device__ __forceinline__ void gn_store(ActF16x3& act, const f32x4 (&acc)[2][NM
         const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
         const f32x4 t = *(const f32x4*)(bias + ch0);
 #pragma unroll
-        for (int m = 0; m < NM; m++) {
+        for (int m = 0; m < NMW; m++) {
             const int pos = (m0 + m) * 16 + (lane & 15);
             if (pos < POS) f16_put4<false>(act, acc[n][m], one, t, none, ch0, pos);
         }
+    }
+}
+
+// embed conv MFMAs (fragments from the im2col in act.hi) and the 8 tower layers
+// for a wave owning NMW M tiles from m0; every barrier of the board's tower is here
+template <int NMW>
+__device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict__ W, int np, int m0, int lane) {
+    {
+        const _Float16* col = act.hi;
+        const int li = lane & 15, q = lane >> 4;
+        h8 a[NMW];
+#pragma unroll
+        for (int m = 0; m < NMW; m++) a[m] = *(const h8*)(col + (q * ROWS16 + (m0 + m) * 16 + li) * 8);
+        h8 wa[2][2];
+#pragma unroll
+        for (int nn = 0; nn < 2; nn++) {
+            const _Float16* wf = (const _Float16*)(W + GH_E) + ((size_t)(2 * np + nn) * 64 + lane) * 8;
+            wa[nn][0] = *(const h8*)wf;
+            wa[nn][1] = *(const h8*)(wf + 4 * 64 * 8);
+        }
+        f32x4 acc[2][NMW];
+#pragma unroll
+        for (int m = 0; m < NMW; m++)
+#pragma unroll
+            for (int nn = 0; nn < 2; nn++) {
+                acc[nn][m] = zero4();
+                acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][0], a[m], acc[nn][m], 0, 0, 0);
+                acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][1], a[m], acc[nn][m], 0, 0, 0);
+            }
+        __syncthreads();  // every wave has its im2col fragments
+        gn_store<NMW>(act, acc, W + GE_B, np, m0, lane);
+    }
+    __syncthreads();
+    GN_STAMP(2);
+
+    // ---- 4 x [conv3x3 + ReLU, conv1x1 + ReLU] (bg_planner.py:50-54)
+    for (int i = 0; i < 8; i++) {
+        f32x4 acc[2][NMW];
+#pragma unroll
+        for (int nn = 0; nn < 2; nn++)
+#pragma unroll
+            for (int m = 0; m < NMW; m++) acc[nn][m] = zero4();
+        const _Float16* wf = (const _Float16*)(W + h_layer_off(i));
+        if (i % 2 == 0)
+            f16_conv<NMW, 2, 4, 9>(act, wf, np, m0, lane, acc);
+        else
+            f16_conv<NMW, 2, 4, 1>(act, wf, np, m0, lane, acc);
+        __syncthreads();  // every wave has read the layer input
+        if (i % 2 == 0) GN_STAMP(3);
+        else GN_STAMP(5);
+        gn_store<NMW>(act, acc, W + layer_bias(i), np, m0, lane);
+        __syncthreads();
+        if (i % 2 == 0) GN_STAMP(4);
+        else GN_STAMP(6);
     }
 }
 
@@ -197,52 +253,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
                 *(h8*)(col + ((k0 >> 3) * ROWS16 + ROWS16 + row) * 8) = v[1];
             }
             __syncthreads();
-            const int li = lane & 15, q = lane >> 4;
-            h8 a[NM];
-#pragma unroll
-            for (int m = 0; m < NM; m++) a[m] = *(const h8*)(col + (q * ROWS16 + (m0 + m) * 16 + li) * 8);
-            h8 wa[2][2];
-#pragma unroll
-            for (int nn = 0; nn < 2; nn++) {
-                const _Float16* wf = (const _Float16*)(W + GH_E) + ((size_t)(2 * np + nn) * 64 + lane) * 8;
-                wa[nn][0] = *(const h8*)wf;
-                wa[nn][1] = *(const h8*)(wf + 4 * 64 * 8);
-            }
-            f32x4 acc[2][NM];
-#pragma unroll
-            for (int m = 0; m < NM; m++)
-#pragma unroll
-                for (int nn = 0; nn < 2; nn++) {
-                    acc[nn][m] = zero4();
-                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][0], a[m], acc[nn][m], 0, 0, 0);
-                    acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nn][1], a[m], acc[nn][m], 0, 0, 0);
-                }
-            __syncthreads();  // every wave has its im2col fragments
-            gn_store(act, acc, W + GE_B, np, m0, lane);
         }
-        __syncthreads();
-        GN_STAMP(2);
-
-        // ---- 4 x [conv3x3 + ReLU, conv1x1 + ReLU] (bg_planner.py:50-54)
-        for (int i = 0; i < 8; i++) {
-            f32x4 acc[2][NM];
-#pragma unroll
-            for (int nn = 0; nn < 2; nn++)
-#pragma unroll
-                for (int m = 0; m < NM; m++) acc[nn][m] = zero4();
-            const _Float16* wf = (const _Float16*)(W + h_layer_off(i));
-            if (i % 2 == 0)
-                f16_conv<NM, 2, 4, 9>(act, wf, np, m0, lane, acc);
-            else
-                f16_conv<NM, 2, 4, 1>(act, wf, np, m0, lane, acc);
-            __syncthreads();  // every wave has read the layer input
-            if (i % 2 == 0) GN_STAMP(3);
-            else GN_STAMP(5);
-            gn_store(act, acc, W + layer_bias(i), np, m0, lane);
-            __syncthreads();
-            if (i % 2 == 0) GN_STAMP(4);
-            else GN_STAMP(6);
-        }
+        // waves 6-7 own M tiles 12-14 only (tile 15 is all zero rows): 15 tiles, not 16
+        if ((wave >> 1) == 3)
+            gn_tower<NM - 1>(act, W, np, m0, lane);
+        else
+            gn_tower<NM>(act, W, np, m0, lane);
 
         // ---- policy head: conv1x1 64->2 (one thread per position), flatten channel-major
         if (tid < POS) {

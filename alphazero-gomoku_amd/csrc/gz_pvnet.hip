@@ -575,6 +575,9 @@ constexpr int NT16 = 512;
 #ifndef PV_SPLIT
 #define PV_SPLIT 8  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
 #endif
+#ifndef PV_YOUNG_TILES
+#define PV_YOUNG_TILES (15 - PV_SPLIT)
+#endif
 __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restrict__ W,
                                                          const uint32_t* __restrict__ boards, int n,
                                                          const int32_t* d_count, float* __restrict__ logits,
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
-            f16_tower<15 - PV_SPLIT, PV_SPLIT>(act, W, wave, lane, sm.hpart);
+            f16_tower<PV_YOUNG_TILES, PV_SPLIT>(act, W, wave, lane, sm.hpart);
         else
             f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart);
         int tid_h = threadIdx.x;  // re-read: a pinned tid kept live across the tower is spilled
