@@ -416,26 +416,13 @@ __device__ __forceinline__ void conv0_tile(Act& act, const float* __restrict__ W
 
 // heads (neural_network.py:132-159) + softmax (neural_network.py:240-247) for board b;
 // the tower's output map is in act.  Ends with a barrier.
-template <int NTH, class Act, bool FUSED>
+template <int NTH, class Act>
 __device__ __forceinline__ void heads(const Act& act, const Smem& sm, const float* __restrict__ W, int b, int tid,
                                       float* __restrict__ logits, float* __restrict__ value,
                                       float* __restrict__ probs) {
     const int lane = tid & 63, wave = tid >> 6;
     // 1x1 convs (policy 128->2, value 128->1), one thread per position
-    if (FUSED) {  // partial sums of the 4 channel quarters from the last epilogue
-        if (tid < POS) {
-            float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                p0 += sm.hpart[(q * 3 + 0) * 256 + tid];
-                p1 += sm.hpart[(q * 3 + 1) * 256 + tid];
-                v += sm.hpart[(q * 3 + 2) * 256 + tid];
-            }
-            sm.hp[tid] = p0;
-            sm.hp[POS + tid] = p1;
-            sm.hv[tid] = v;
-        }
-    } else if (tid < POS) {
+    if (tid < POS) {
         const int pos = tid;
         float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
         for (int c0 = 0; c0 < CH; c0 += 8) {
@@ -564,7 +551,7 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
                 __syncthreads();
             }
         }
-        heads<NT32, ActF32, false>(act, sm, W, b, tid, logits, value, probs);
+        heads<NT32, ActF32>(act, sm, W, b, tid, logits, value, probs);
     }
 }
 
@@ -572,6 +559,9 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
 // (one wave per SIMD with 512 registers and all 15 M tiles per wave measured 37%
 // slower: the compiler serialises the A-fragment reads of a single stream)
 constexpr int NT16 = 512;
+// per-board record of the 1x1 head convs' outputs between the tower and the FC heads:
+// hp [0, 450) channel-major, zero to HP_K; hv [HV_OFF, HV_OFF + 225), zero to HSTRIDE
+constexpr int HP_K = 464, HV_OFF = HP_K, HV_K = 240, HSTRIDE = HV_OFF + HV_K;
 #ifndef PV_SPLIT
 #define PV_SPLIT 8  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
 #endif
@@ -580,8 +570,7 @@ constexpr int NT16 = 512;
 #endif
 __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restrict__ W,
                                                          const uint32_t* __restrict__ boards, int n,
-                                                         const int32_t* d_count, float* __restrict__ logits,
-                                                         float* __restrict__ value, float* __restrict__ probs) {
+                                                         const int32_t* d_count, float* __restrict__ hbuf) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const Smem sm = smem_layout(lds);
     ActF16x3 act;
@@ -613,7 +602,169 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
             f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart);
         int tid_h = threadIdx.x;  // re-read: a pinned tid kept live across the tower is spilled
         asm volatile("" : "+v"(tid_h));
-        heads<NT16, ActF16x3, true>(act, sm, W, b, tid_h, logits, value, probs);
+        // the 1x1 head convs' outputs go to HBM; the FC heads run batched over boards
+        // in pv_heads_kernel.  hpart is next written in the next board's last epilogue,
+        // many barriers later, so no barrier is needed here.
+        if (tid_h < POS) {
+            float p0 = W[P_B], p1 = W[P_B + 1], v = W[V_B];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                p0 += sm.hpart[(q * 3 + 0) * 256 + tid_h];
+                p1 += sm.hpart[(q * 3 + 1) * 256 + tid_h];
+                v += sm.hpart[(q * 3 + 2) * 256 + tid_h];
+            }
+            float* h = hbuf + (size_t)b * HSTRIDE;
+            h[tid_h] = p0;  // flatten order: channel-major (policy.view(B, -1))
+            h[POS + tid_h] = p1;
+            h[HV_OFF + tid_h] = v;
+        } else if (tid_h < POS + (HV_OFF - 2 * POS)) {
+            hbuf[(size_t)b * HSTRIDE + 2 * POS + (tid_h - POS)] = 0.f;  // hp k-padding
+        } else if (tid_h < POS + (HV_OFF - 2 * POS) + (HSTRIDE - HV_OFF - POS)) {
+            hbuf[(size_t)b * HSTRIDE + HV_OFF + POS + (tid_h - POS - (HV_OFF - 2 * POS))] = 0.f;  // hv padding
+        }
+    }
+}
+
+// ============================================================ batched FC heads (f16x3 path)
+// policy_fc 450->225 and value_fc1 225->64 for HB = 64 boards per workgroup as fp32
+// MFMA GEMMs (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation) over
+// the 1x1-conv outputs the tower kernel left in hbuf, then value_fc2 + tanh and the
+// softmax (neural_network.py:146-159, 240-247).  K is taken in blocks of 16: in the
+// t-th k-step of block j, lane group g multiplies k = 16j + 4g + t, so a lane's A
+// operand for 4 k-steps is one 16-byte load.  Wave w: policy n-tiles {w, w+4, w+8,
+// w+12} (< 15) and value n-tile w, all 4 board tiles.
+constexpr int HB = 64;
+constexpr int NTH_H = 256;
+constexpr int LG_STRIDE = 228;
+static_assert(HP_K % 16 == 0 && HV_K % 16 == 0 && HV_OFF % 4 == 0 && HSTRIDE % 4 == 0, "16-B A loads");
+
+__device__ __forceinline__ void heads_gemm_block(const float* __restrict__ Wt,
+                                                 int ldw, int kmax, int nmax, int kb, int lane, const int (&nt)[4],
+                                                 int ntn, f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
+    const int li = lane & 15, g = lane >> 4;
+    f32x4 a[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        int k = 16 * kb + 4 * g + t;
+        k = k < kmax ? k : kmax - 1;  // A is zero there
+        float bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int n = 16 * nt[q] + li;
+            n = n < nmax ? n : nmax - 1;
+            bv[q] = q < ntn ? Wt[(size_t)k * ldw + n] : 0.f;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][t], bv[q], acc[m][q], 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restrict__ W, const float* __restrict__ hbuf,
+                                                           int n, const int32_t* d_count, float* __restrict__ logits,
+                                                           float* __restrict__ value, float* __restrict__ probs) {
+    __shared__ float lg[HB * LG_STRIDE];
+    __shared__ float h1[HB * 64];
+    const int count = board_count(n, d_count);
+    const int b0 = blockIdx.x * HB;
+    if (b0 >= count) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, g = lane >> 4;
+    // board rows of the lane (row li of each of the 4 board tiles); rows past count
+    // re-read the last board and their outputs are dropped
+    const float* arow[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const int b = b0 + 16 * m + li;
+        arow[m] = hbuf + (size_t)(b < count ? b : count - 1) * HSTRIDE;
+    }
+    {  // policy_fc
+        int nt[4];
+        int ntn = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            nt[q] = wave + 4 * q;
+            ntn += nt[q] < 15;
+        }
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[m][q] = zero4();
+        for (int kb = 0; kb < HP_K / 16; kb++)
+            heads_gemm_block(W + PF_WT, POS, 2 * POS, POS, kb, lane, nt, ntn, acc, arow);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (q >= ntn) continue;
+            const int o = 16 * nt[q] + li;
+            if (o >= POS) continue;
+            const float bias = W[PF_B + o];
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) lg[(16 * m + 4 * g + r) * LG_STRIDE + o] = acc[m][q][r] + bias;
+        }
+    }
+    {  // value_fc1 (+ bias, ReLU)
+        const float* arv[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) arv[m] = arow[m] + HV_OFF;
+        int nt[4] = {wave, 0, 0, 0};
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[m][0] = zero4();
+        for (int kb = 0; kb < HV_K / 16; kb++)
+            heads_gemm_block(W + V1_WT, 64, POS, 64, kb, lane, nt, 1, acc, arv);
+        const int j = 16 * wave + li;
+        const float bias = W[V1_B + j];
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float y = acc[m][0][r] + bias;
+                h1[(16 * m + 4 * g + r) * 64 + j] = y > 0.f ? y : 0.f;
+            }
+    }
+    __syncthreads();
+    // value_fc2 + tanh: one thread per board
+    if (tid < HB && b0 + tid < count) {
+        float tot = 0.f;
+        for (int j = 0; j < 64; j++) tot += W[V2_W + j] * h1[tid * 64 + j];
+        value[b0 + tid] = tanhf(tot + W[V2_B]);
+    }
+    // softmax: wave w handles boards w, w+4, ...; lane covers outputs lane + 64u
+    for (int bb = wave; bb < HB && b0 + bb < count; bb += 4) {
+        const float* l = lg + bb * LG_STRIDE;
+        float x[4];
+        float mx = -3.0e38f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            x[u] = o < POS ? l[o] : -3.0e38f;
+            mx = fmaxf(mx, x[u]);
+        }
+        mx = wave_max(mx);
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            e[u] = o < POS ? __expf(x[u] - mx) : 0.f;
+            sum += e[u];
+        }
+        sum = wave_sum(sum);
+        const size_t base = (size_t)(b0 + bb) * POS;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            if (o < POS) {
+                logits[base + o] = x[u];
+                if (probs) probs[base + o] = e[u] / sum;
+            }
+        }
     }
 }
 
@@ -642,8 +793,10 @@ static int pv_grid(int n) {
 }
 
 extern "C" size_t gz_pv_workspace_bytes(int32_t n) {
-    int grid = pv_grid(n < 1 ? 1 : n);
-    return (size_t)grid * (NT32 / 64) * SLAB_F * sizeof(float);
+    const int grid = pv_grid(n < 1 ? 1 : n);
+    const size_t slab = (size_t)grid * (NT32 / 64) * SLAB_F * sizeof(float);  // fp32 kernel
+    const size_t heads = (size_t)(n < 1 ? 1 : n) * HSTRIDE * sizeof(float);    // f16x3: tower -> heads
+    return slab > heads ? slab : heads;
 }
 
 extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
@@ -668,7 +821,11 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
         pv_kernel_f32<<<grid, NT32, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs,
                                             (float*)d_workspace);
     else
-        pv_kernel_f16x3<<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, d_logits, d_value, d_probs);
+    {
+        pv_kernel_f16x3<<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace);
+        pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count,
+                                                           d_logits, d_value, d_probs);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_kernel: ") + hipGetErrorString(e)).c_str());

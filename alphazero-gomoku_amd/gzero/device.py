@@ -169,8 +169,15 @@ class PVWeights:
         if blob.size != lib.gz_pv_weight_floats():
             raise ValueError(f"weight blob has {blob.size} floats, kernel expects {lib.gz_pv_weight_floats()}")
         self.tensor = torch.from_numpy(blob).cuda()
-        ws = lib.gz_pv_workspace_bytes(1 << 30)
-        self.workspace = torch.empty(ws, dtype=torch.uint8, device="cuda")
+        self.workspace = torch.empty(0, dtype=torch.uint8, device="cuda")
+
+    def workspace_for(self, n):
+        """gz_pv_workspace_bytes(n) bytes of scratch (the fp32 kernel's slabs, or the f16x3
+        tower -> FC-heads records), grown on demand and kept."""
+        need = _lib.load().gz_pv_workspace_bytes(int(max(1, n)))
+        if self.workspace.numel() < need:
+            self.workspace = torch.empty(need, dtype=torch.uint8, device="cuda")
+        return self.workspace
 
 
 def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=None, d_probs=None):
@@ -181,7 +188,7 @@ def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=No
     if d_value is None:
         d_value = torch.empty(n, dtype=torch.float32, device="cuda")
     _lib.check(lib.gz_pv_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_logits),
-                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace), weights.mode, stream()),
+                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace_for(n)), weights.mode, stream()),
                "gz_pv_forward")
     return d_logits, d_value, d_probs
 

@@ -87,7 +87,7 @@ class SelfPlayEngine:
         d_count = self.d_counters[4:8]  # counters.leaves
         _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
                                           ptr(d_count), ptr(self.d_logits), ptr(self.d_value),
-                                          ptr(self.d_probs), ptr(self.pv_weights.workspace),
+                                          ptr(self.d_probs), ptr(self.pv_weights.workspace_for(self.leaf_cap)),
                                           self.pv_weights.mode, stream()), "gz_pv_forward")
 
     def step(self, n_plies=None):

@@ -160,7 +160,9 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
  * (n = capacity).  Outputs: logits [n][225], value [n] (tanh), probs
  * [n][225] (softmax) or NULL.  precision: GZ_PV_FP32 (exact f32 MFMA) or
  * GZ_PV_F16X3 (3-term fp16 split on the fp16 MFMA, ~22-bit operands, f32
- * accumulation).  d_workspace: gz_pv_workspace_bytes(n) bytes, required. */
+ * accumulation).  d_workspace: gz_pv_workspace_bytes(n) bytes, required (fp32:
+ * per-wave slabs; f16x3: the 1x1 head convs' outputs of every board, 2,816 B
+ * each, passed from the tower kernel to the batched FC-heads kernel). */
 #define GZ_PV_FP32 0
 #define GZ_PV_F16X3 1
 size_t gz_pv_weight_floats(void);
