@@ -205,7 +205,9 @@ def main():
         note = ("3-term fp16 split on v_mfma_f32_16x16x32_f16 (f32 accumulate): peak = dense fp16 MFMA "
                 "peak / 3 products per fp32-equivalent multiply")
     roofline = {
-        "kernel": f"pv_kernel<{args.pv_precision}> (AlphaZeroGomokuNet forward)",
+        "kernel": (f"gz_pv_forward<{args.pv_precision}> (AlphaZeroGomokuNet forward"
+                   + (": pv_kernel_f16x3 tower + pv_heads_kernel FC heads)" if args.pv_precision == "f16x3"
+                      else ": pv_kernel_f32)")),
         "bound": "mfma",
         "achieved": round(achieved, 3),
         "peak": round(peak, 1),

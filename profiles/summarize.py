@@ -5,9 +5,13 @@ FETCH_SIZE / WRITE_SIZE passes.
 
 Bytes: rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md
 (HBM section) FETCH_SIZE reads 1/2 of the bytes of a WIDE (16 B/lane) coalesced
-stream on gfx950; the PV kernel's weight loads are 4 B/lane and the self-play
-kernel's accesses are mixed, i.e. uncalibrated widths, so the raw counter is
-reported (corrected = raw, flagged) rather than guessing a factor.
+stream on gfx950; the PV forward's HBM reads are a mix of 16-B weight-fragment
+loads (L2 hits after the first board), 4-B board and 16-B head-record loads, and
+the self-play kernel's accesses are mixed too, i.e. uncalibrated widths, so the
+raw counter is reported (corrected = raw, flagged) rather than guessing a factor.
+
+The PV forward (one gz_pv_forward) is two kernels for f16x3: pv_kernel_f16x3
+(tower) and pv_heads_kernel (batched FC heads); both are summed as "pv_forward".
 
 Usage: python profiles/summarize.py gpurun_out/prof_r01 profiles/r01
 """
@@ -39,7 +43,7 @@ summary = {"bench": {k: bench[k] for k in ("value", "unit", "ms_per_step", "step
 for k, v in durs.items():
     # the bench's timed window is the LAST `steps` PV launches (warm-up launches
     # include opening plies with no leaves)
-    timed = v[-steps:] if k.startswith("pv_kernel") else v
+    timed = v[-steps:] if k.startswith("pv_") else v
     summary["kernels"][k] = {"calls": len(v), "avg_ms_all": sum(v) / len(v),
                              "avg_ms_timed_window": sum(timed) / len(timed), "max_ms": max(v)}
 
@@ -55,22 +59,27 @@ def pmc(name, counter):
 
 fetch = pmc("pmc_fetch", "FETCH_SIZE")
 write = pmc("pmc_write", "WRITE_SIZE")
-PV = next((k for k in durs if k.startswith("pv_kernel")), "pv_kernel")
-for k in (PV, "selfplay_kernel"):
+PVK = [k for k in durs if k.startswith("pv_")]
+for k in PVK + ["selfplay_kernel"]:
     if k in fetch and k in write:
-        f = fetch[k][-steps:] if k == PV else fetch[k]
-        w = write[k][-steps:] if k == PV else write[k]
+        f = fetch[k][-steps:] if k in PVK else fetch[k]
+        w = write[k][-steps:] if k in PVK else write[k]
         summary["kernels"].setdefault(k, {})["hbm_bytes_per_launch"] = {
             "fetch_raw": sum(f) / len(f) * 1024, "write": sum(w) / len(w) * 1024,
             "total_raw": (sum(f) / len(f) + sum(w) / len(w)) * 1024,
             "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024; access widths uncalibrated -> raw"}
-pv = summary["kernels"].get(PV, {})
 boards = bench["config"]["pv_boards_per_step"]
-if "hbm_bytes_per_launch" in pv:
-    tb = pv["hbm_bytes_per_launch"]["total_raw"]
+pvf = {"kernels": PVK,
+       "avg_ms_timed_window": sum(summary["kernels"][k]["avg_ms_timed_window"] for k in PVK)}
+if PVK and all("hbm_bytes_per_launch" in summary["kernels"][k] for k in PVK):
+    tb = sum(summary["kernels"][k]["hbm_bytes_per_launch"]["total_raw"] for k in PVK)
+    pvf["hbm_bytes_per_launch"] = tb
     json.dump({"bytes_per_launch": tb, "boards_per_launch": boards, "bytes_per_board": tb / boards,
                "algorithmic_bytes_per_board": 64 + 225 * 4 * 2 + 4,
-               "source": src}, open(os.path.join(os.path.dirname(dst.rstrip("/")), "pv_traffic.json"), "w"), indent=1)
+               "note": "f16x3: includes the tower -> heads record (2,816 B written and read per board)",
+               "kernels": PVK, "source": src},
+              open(os.path.join(os.path.dirname(dst.rstrip("/")), "pv_traffic.json"), "w"), indent=1)
+summary["pv_forward"] = pvf
 json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
 for f in ("trace/run_kernel_stats.csv", "pmc_fetch/run_counter_collection.csv",
           "pmc_write/run_counter_collection.csv", "bench_trace.json"):
