@@ -4,6 +4,6 @@ cmd=$1; shift
 for rep in 1 2; do
   for lib in "$@"; do
     echo -n "$(basename $lib): "
-    GZ_LIBRARY=$lib timeout -k 10 120 $cmd 2>/dev/null | tail -1 || exit 1
+    GZ_LIBRARY=$lib timeout -k 10 120 $cmd 2>/dev/null | tail -2 | tr "\n" " "; echo || exit 1
   done
 done

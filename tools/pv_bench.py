@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--precision", default="f16x3")
+ap.add_argument("--check", type=int, default=256, help="boards checked against the torch fp32 forward")
 a = ap.parse_args()
 w = device.PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision=a.precision)
 rng = np.random.default_rng(0)
@@ -39,3 +40,9 @@ for _ in range(a.iters):
 t = float(np.median(ts))
 print(f"pv_kernel[{a.precision}] n={a.n}: {t*1e3:.1f} ms, {a.n/t:.0f} boards/s, {a.n*weights.PV_FLOPS/t/1e12:.1f} TFLOP/s "
       f"({a.n*weights.PV_FLOPS/t/1e12/157.3*100:.1f}% of fp32 MFMA peak)")
+if a.check:
+    sd = weights.init_state_dict(0)
+    ref_lg, ref_v = weights.reference_forward(sd, boards.planes_from_cells(cells[: a.check]))
+    dl = np.abs(lg.view(a.n, 225)[: a.check].cpu().numpy() - ref_lg).max()
+    dv = np.abs(v[: a.check].cpu().numpy() - ref_v.reshape(-1)).max()
+    print(f"  check {a.check} boards vs torch fp32: max |dlogit| {dl:.2e}, max |dvalue| {dv:.2e}", "OK" if max(dl, dv) < 1e-4 else "FAIL")
