@@ -49,4 +49,11 @@ constexpr int h_layer_off(int i) {
 constexpr int D0_BASE = h_layer_off(8);
 constexpr int D0_DELTA = D0_BASE + DQH;
 constexpr int TOTAL = D0_DELTA + 450 * DQH;
+
+// per-board record between gn_kernel (GraphNet tower + policy conv 1x1) and
+// gn_heads_kernel (policy FC + softmax, OpponentDQN): floats
+//   [0, 450) policy conv output (channel-major flatten), zero to REC_X;
+//   [REC_X, REC_X + 450) the one-hot stone inputs [black 225 | white 225], zero to REC
+constexpr int REC_X = 464;
+constexpr int REC = 928;
 }  // namespace gzgn

@@ -8,7 +8,10 @@
 // {2(w&1), 2(w&1)+1} x M tiles [4(w>>1), 4(w>>1)+4), waves 6-7 three tiles (tile 15
 // would be zero rows only).
 // The embed conv reads 0/1 planes, exact in fp16, so it takes 2 MFMAs (w_hi, w_lo).
-// Heads (policy conv 1x1, FC 450->225, softmax) and the DQN MLP run on VALU.
+// The policy conv 1x1 (64->2) runs on VALU at the end of the tower and goes to a
+// per-board record in the workspace with the stone inputs; gn_heads_kernel then runs
+// the policy FC 450->225 + softmax and the OpponentDQN MLP for 64 boards per
+// workgroup as fp32-MFMA GEMMs (weights read once per 64 boards, not per board).
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -44,7 +47,7 @@ constexpr int NT = 512;
 constexpr int NM = 4;        // M tiles per wave
 constexpr int PROWS = 240;   // fp32 planes [3][240]
 constexpr int ACT_BYTES = 2 * HID * ROWS16 * 2;  // 65536
-constexpr int SMALL_F = 3 * PROWS + 2 * POS + 256 + 2 * 256 + 32 + 2 * DQH + 2 * DQH + 256;
+constexpr int SMALL_F = 3 * PROWS;
 constexpr int LDS_BYTES = ACT_BYTES + SMALL_F * 4;
 
 // neighbour of the lane's position in M tile m for tap (dr, dc); POS (a zero plane slot) if off-board
@@ -129,21 +132,14 @@ __device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict_
     }
 }
 
-__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void gn_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards,
-                                                   int n, const int32_t* d_count, float* __restrict__ p_out,
-                                                   float* __restrict__ q_out, float* __restrict__ logits_out) {
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void gn_kernel(
+    const float* __restrict__ W, const uint32_t* __restrict__ boards, int n, const int32_t* d_count,
+    float* __restrict__ rec) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     ActF16x3 act;
     act.hi = (_Float16*)lds;
     act.lo = act.hi + HID * ROWS16;
     float* planes = (float*)(lds + ACT_BYTES);  // [3][240]
-    float* pc = planes + 3 * PROWS;             // [450] policy conv output, channel-major
-    float* lg = pc + 2 * POS;                   // [256]
-    float* part = lg + 256;                     // [2][256]
-    float* red = part + 2 * 256;                // [32]
-    float* da = red + 32;                       // [2][256] dqn partial sums / activations
-    float* dc = da + 2 * DQH;                   // [2][256]
-    int* slist = (int*)(dc + 2 * DQH);          // [225] stones (delta rows), row-major
 
     int count = n;
     if (d_count) {
@@ -160,7 +156,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         asm volatile("" : "+v"(tid));
         const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int np = wave & 1, m0 = (wave >> 1) * NM;
-        // ---- input planes [black, white, empty] (bg_planner.py:225-230)
+        float* rb = rec + (size_t)b * REC;
+        // ---- input planes [black, white, empty] (bg_planner.py:225-230); the stone
+        // planes also go to the record (the DQN's one-hot inputs, gn_heads_kernel)
         const uint32_t* bd = boards + (size_t)b * 16;
         for (int p = tid; p < POS; p += NT) {
             int bit = (p / 15) * 16 + (p % 15);
@@ -169,67 +167,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             planes[p] = (float)bl;
             planes[PROWS + p] = (float)wh;
             planes[2 * PROWS + p] = (float)(1u - (bl | wh));
+            rb[REC_X + p] = (float)bl;
+            rb[REC_X + POS + p] = (float)wh;
+        }
+        if (tid < (REC_X - 2 * POS) + (REC - REC_X - 2 * POS)) {  // record padding (A rows past K are zero)
+            const int z = tid < REC_X - 2 * POS ? 2 * POS + tid : REC_X + 2 * POS + (tid - (REC_X - 2 * POS));
+            rb[z] = 0.f;
         }
         __syncthreads();
         GN_STAMP(0);
-
-        // ---- OpponentDQN (bg_planner.py:68-78).  fc0 on the one-hot planes =
-        // base + the delta rows of the stones (gz_gnet.h), stones listed in
-        // row-major order (a fixed summation order: q is reproducible)
-        if (wave < 4) {
-            const int pos = tid;
-            int code = -1;
-            if (pos < POS) code = planes[pos] != 0.f ? pos : (planes[PROWS + pos] != 0.f ? POS + pos : -1);
-            const uint64_t m = __ballot(code >= 0);
-            if (lane == 0) red[16 + wave] = (float)__popcll(m);
-            __syncthreads();
-            int off = 0;
-            for (int k = 0; k < wave; k++) off += (int)red[16 + k];
-            if (code >= 0) slist[off + __popcll(m & ((1ull << lane) - 1ull))] = code;
-            if (tid == 0) red[24] = red[16] + red[17] + red[18] + red[19];
-        } else {
-            __syncthreads();
-        }
-        __syncthreads();
-        {
-            const int j = tid & 255, h = tid >> 8;
-            const int ns = (int)red[24];
-            float acc = h == 0 ? W[D0_BASE + j] : 0.f;
-            const float* dt = W + D0_DELTA + j;
-            int i = h;
-            for (; i + 14 < ns; i += 16) {  // 8 independent loads in flight
-                float v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = dt[(size_t)slist[i + 2 * u] * DQH];
-#pragma unroll
-                for (int u = 0; u < 8; u++) acc += v[u];
-            }
-            for (; i < ns; i += 2) acc += dt[(size_t)slist[i] * DQH];
-            da[h * DQH + j] = acc;
-        }
-        __syncthreads();
-        if (tid < DQH) {
-            float a = da[tid] + da[DQH + tid];
-            dc[tid] = a > 0.f ? a : 0.f;
-        }
-        __syncthreads();
-        {  // fc1 256->256 in two input halves
-            const int j = tid & 255, h = tid >> 8;
-            da[h * DQH + j] = dot_col<128, 64>(W + D1_WT + (size_t)(h * 128) * DQH + j, DQH, dc + h * 128);
-        }
-        __syncthreads();
-        if (tid < DQH) {
-            float a = W[D1_B + tid] + (da[tid] + da[DQH + tid]);
-            dc[DQH + tid] = a > 0.f ? a : 0.f;
-        }
-        __syncthreads();
-        {  // fc2 256->225 in two input halves
-            const int j = tid & 255, h = tid >> 8;
-            if (j < POS) da[h * DQH + j] = dot_col<128, 64>(W + D2_WT + (size_t)(h * 128) * POS + j, POS, dc + DQH + h * 128);
-        }
-        __syncthreads();
-        if (tid < POS) q_out[(size_t)b * POS + tid] = W[D2_B + tid] + (da[tid] + da[DQH + tid]);
-        GN_STAMP(1);
 
         // ---- embed conv 3->64 (K = 27 -> 32): planes are 0/1, so a*w = a*w_hi + a*w_lo.
         // im2col (256 rows x 32 halves, built once per board) lives in the activation
@@ -260,55 +206,170 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         else
             gn_tower<NM>(act, W, np, m0, lane);
 
-        // ---- policy head: conv1x1 64->2 (one thread per position), flatten channel-major
-        if (tid < POS) {
+        // ---- policy head conv1x1 64->2 (one thread per position), flattened
+        // channel-major into the record.  The next board's first LDS write that
+        // could clobber the map (its im2col) comes after a barrier, so none here.
+        int tid_h = threadIdx.x;  // re-read (not kept live across the tower)
+        asm volatile("" : "+v"(tid_h));
+        if (tid_h < POS) {
             float p0 = W[GP_B], p1 = W[GP_B + 1];
             for (int c0 = 0; c0 < HID; c0 += 8) {
                 float a[8];
-                act.get8(c0, tid, a);
+                act.get8(c0, tid_h, a);
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     p0 += W[GP_W + c0 + j] * a[j];
                     p1 += W[GP_W + HID + c0 + j] * a[j];
                 }
             }
-            pc[tid] = p0;
-            pc[POS + tid] = p1;
+            rb[tid_h] = p0;
+            rb[POS + tid_h] = p1;
         }
-        __syncthreads();
         GN_STAMP(7);
-        {  // Linear 450->225 in two input halves
-            const int o = tid & 255, h = tid >> 8;
-            if (o < POS) part[h * 256 + o] = dot_col<POS, 45>(W + GF_WT + (size_t)h * POS * POS + o, POS, pc + h * POS);
+    }
+}
+
+// ============================================================ batched heads
+// policy FC 450->225 + softmax (bg_planner.py:55-56, 243-246) and OpponentDQN
+// (bg_planner.py:68-78) for HB = 64 boards per workgroup as fp32-MFMA GEMMs over
+// the records gn_kernel left (heads_gemm_block, gz_f16conv.h).  DQN fc0 on the one-hot
+// planes = base + the (colour - empty) delta rows of the stones (gz_gnet.h): a GEMM
+// with K = 450 over the record's stone inputs.  Wave w: n-tiles {w, w+4, w+8, w+12}.
+constexpr int HB = 64;
+constexpr int NTH_H = 256;
+constexpr int LG_STRIDE = 228;   // logits rows
+constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
+static_assert(REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
+
+template <int KB>
+__device__ __forceinline__ void heads_gemm(const float* __restrict__ Wt, int ldw, int kmax, int nmax, int lane,
+                                           const int (&nt)[4], int ntn, f32x4 (&acc)[4][4],
+                                           const float* __restrict__ arow[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[m][q] = zero4();
+    for (int kb = 0; kb < KB; kb++) heads_gemm_block(Wt, ldw, kmax, nmax, kb, lane, nt, ntn, acc, arow);
+}
+
+// acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles
+template <bool RELU>
+__device__ __forceinline__ void heads_put(const f32x4 (&acc)[4][4], const float* __restrict__ bias, int nmax,
+                                          const int (&nt)[4], int ntn, int lane, float* dst, int stride) {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (q >= ntn) continue;
+        const int o = 16 * nt[q] + li;
+        if (o >= nmax) continue;
+        const float bv = bias[o];
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = acc[m][q][r] + bv;
+                if (RELU) y = y > 0.f ? y : 0.f;
+                dst[(16 * m + 4 * g + r) * stride + o] = y;
+            }
+    }
+}
+
+__global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restrict__ W, const float* __restrict__ rec,
+                                                           int n, const int32_t* d_count, float* __restrict__ p_out,
+                                                           float* __restrict__ q_out, float* __restrict__ logits_out) {
+    __shared__ __attribute__((aligned(16))) float ra[HB * H_STRIDE];  // logits, then DQN hidden 2
+    __shared__ __attribute__((aligned(16))) float rb[HB * H_STRIDE];  // DQN hidden 1
+    int count = n;
+    if (d_count) {
+        int c = *d_count;
+        count = c < n ? c : n;
+    }
+    const int b0 = blockIdx.x * HB;
+    if (b0 >= count) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, g = lane >> 4;
+    // board rows of the lane (row li of each of the 4 board tiles); rows past count
+    // re-read the last board and their outputs are dropped
+    const float* arow[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const int b = b0 + 16 * m + li;
+        arow[m] = rec + (size_t)(b < count ? b : count - 1) * REC;
+    }
+    int nt[4];
+    int ntn_p = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        nt[q] = wave + 4 * q;
+        ntn_p += nt[q] < 15;
+    }
+    f32x4 acc[4][4];
+    // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
+    heads_gemm<REC_X / 16>(W + GF_WT, POS, 2 * POS, POS, lane, nt, ntn_p, acc, arow);
+    heads_put<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
+    __syncthreads();
+    for (int bb = wave; bb < HB && b0 + bb < count; bb += 4) {  // wave w: boards w, w+4, ...
+        const float* l = ra + bb * LG_STRIDE;
+        float x[4];
+        float mx = -3.0e38f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            x[u] = o < POS ? l[o] : -3.0e38f;
+            mx = fmaxf(mx, x[u]);
         }
-        __syncthreads();
-        if (tid < POS) lg[tid] = W[GF_B + tid] + (part[tid] + part[256 + tid]);
-        __syncthreads();
-        GN_STAMP(8);
-        // ---- softmax over 225 logits (waves 0..3), torch.softmax(dim=0) semantics in fp32
-        if (wave < 4) {
-            float x = tid < POS ? lg[tid] : -3.0e38f;
-            float mx = wave_max(x);
-            if (lane == 0) red[wave] = mx;
+        mx = wave_max(mx);
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            e[u] = o < POS ? __expf(x[u] - mx) : 0.f;
+            sum += e[u];
         }
-        __syncthreads();
-        if (wave < 4) {
-            const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-            float e = tid < POS ? __expf(lg[tid] - mx) : 0.f;
-            float s = wave_sum(e);
-            if (lane == 0) red[8 + wave] = s;
-            if (tid < POS) {
-                if (logits_out) logits_out[(size_t)b * POS + tid] = lg[tid];
-                lg[tid] = e;
+        sum = wave_sum(sum);
+        const size_t base = (size_t)(b0 + bb) * POS;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            if (o < POS) {
+                p_out[base + o] = e[u] / sum;
+                if (logits_out) logits_out[base + o] = x[u];
             }
         }
-        __syncthreads();
-        if (wave < 4) {
-            const float s = (red[8] + red[9]) + (red[10] + red[11]);
-            if (tid < POS) p_out[(size_t)b * POS + tid] = lg[tid] / s;
-        }
-        __syncthreads();
-        GN_STAMP(9);
+    }
+    // ---- DQN fc0 (one-hot planes -> 256) + ReLU into rb
+    {
+        const float* ax[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) ax[m] = arow[m] + REC_X;
+        heads_gemm<(REC - REC_X) / 16>(W + D0_DELTA, DQH, 2 * POS, DQH, lane, nt, 4, acc, ax);
+        heads_put<true>(acc, W + D0_BASE, DQH, nt, 4, lane, rb, H_STRIDE);
+    }
+    __syncthreads();  // rb complete; ra (logits) no longer read
+    const float* ah[4];
+    // ---- fc1 256 -> 256 + ReLU into ra
+#pragma unroll
+    for (int m = 0; m < 4; m++) ah[m] = rb + (16 * m + li) * H_STRIDE;
+    heads_gemm<DQH / 16>(W + D1_WT, DQH, DQH, DQH, lane, nt, 4, acc, ah);
+    heads_put<true>(acc, W + D1_B, DQH, nt, 4, lane, ra, H_STRIDE);
+    __syncthreads();
+    // ---- fc2 256 -> 225: q
+#pragma unroll
+    for (int m = 0; m < 4; m++) ah[m] = ra + (16 * m + li) * H_STRIDE;
+    heads_gemm<DQH / 16>(W + D2_WT, POS, DQH, POS, lane, nt, ntn_p, acc, ah);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (q >= ntn_p) continue;
+        const int o = 16 * nt[q] + li;
+        if (o >= POS) continue;
+        const float bv = W[D2_B + o];
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int b = b0 + 16 * m + 4 * g + r;
+                if (b < count) q_out[(size_t)b * POS + o] = acc[m][q][r] + bv;
+            }
     }
 }
 
@@ -329,10 +390,12 @@ extern "C" void gz_internal_set_error(const char* msg);
 
 extern "C" size_t gz_gn_weight_floats(void) { return (size_t)TOTAL; }
 
+extern "C" size_t gz_gn_workspace_bytes(int32_t n) { return (size_t)(n < 1 ? 1 : n) * REC * sizeof(float); }
+
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                             float* d_p, float* d_q, float* d_logits, void* stream) {
-    if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_p || !d_q))) {
-        gz_internal_set_error("gz_gn_forward: bad arguments");
+                             float* d_p, float* d_q, float* d_logits, void* d_workspace, void* stream) {
+    if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_p || !d_q || !d_workspace))) {
+        gz_internal_set_error("gz_gn_forward: bad arguments (d_workspace: gz_gn_workspace_bytes(n))");
         return GZ_ERR_ARG;
     }
     if (n == 0) return GZ_OK;
@@ -340,7 +403,10 @@ extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, i
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     int grid = n < 2 * cus ? n : 2 * cus;
-    gn_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(d_weights, d_boards, n, d_count, d_p, d_q, d_logits);
+    hipStream_t s = (hipStream_t)stream;
+    gn_kernel<<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace);
+    gn_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count, d_p, d_q,
+                                                        d_logits);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("gn_kernel: ") + hipGetErrorString(e)).c_str());

@@ -72,12 +72,15 @@ struct Counters {
 
 __host__ __device__ inline size_t ctx_stride(int S) { return sizeof(PlanCtx) + tree_bytes_for(S); }
 
+constexpr size_t GN_REC_BYTES = 928 * 4;  // = gz_gn_workspace_bytes(1) (gz_gnet.h REC), checked at run time
+
 struct Workspace {
     char* ctx;
     PlanJob* jobs;
     uint32_t* gn_in;   // [n*S][16]
     float* gn_p;       // [n*S][225]
     float* gn_q;
+    float* gn_rec;     // gz_gn_forward's workspace for n*S rows
     int32_t* rows;     // row -> job
     Counters* ctr;
 };
@@ -100,6 +103,8 @@ __host__ __device__ inline Workspace carve(void* base, int n, int S) {
     p += align256(nj * 225 * 4);
     w.gn_q = (float*)p;
     p += align256(nj * 225 * 4);
+    w.gn_rec = (float*)p;
+    p += align256(nj * GN_REC_BYTES);
     w.rows = (int32_t*)p;
     p += align256(nj * 4);
     return w;
@@ -740,7 +745,8 @@ __global__ void boards_to_rows_kernel(const gz_board_state* boards, int n, uint3
 
 extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                             float* d_p, float* d_q, float* d_logits, void* stream);
+                             float* d_p, float* d_q, float* d_logits, void* d_workspace, void* stream);
+extern "C" size_t gz_gn_workspace_bytes(int32_t n);
 
 static int plan_fail(int code, const char* msg) {
     gz_internal_set_error(msg);
@@ -772,6 +778,8 @@ extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_g
     if (gather && (!d_leaves || !d_leaf_count || leaf_cap < 0))
         return plan_fail(GZ_ERR_ARG, "gz_plan_search: leaf gathering needs d_leaves and d_leaf_count");
     if (n == 0) return GZ_OK;
+    if (gz_gn_workspace_bytes(1) != GN_REC_BYTES)
+        return plan_fail(GZ_ERR_INTERNAL, "gz_plan_search: planner-net record size mismatch");
     hipStream_t s = (hipStream_t)stream;
     const int S = p->num_simulations;
     Workspace w = carve(d_workspace, n, S);
@@ -798,7 +806,8 @@ extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_g
             if (hipMemsetAsync(&w.ctr->rows, 0, 4, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
             plan_collect_kernel<<<jb, 256, 0, s>>>(w, n_jobs, p->planner_steps, 0);
             if ((rc = plan_check("plan_collect_kernel"))) return rc;
-            if ((rc = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, stream)))
+            if ((rc = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
+                                    stream)))
                 return rc;
             plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp);
             if ((rc = plan_check("plan_step_kernel"))) return rc;
@@ -828,14 +837,16 @@ extern "C" int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_
     uint32_t* rows = (uint32_t*)base;
     float* gp = (float*)(base + align256((size_t)n * 64));
     float* gq = gp + (size_t)n * 225;
+    float* rec = (float*)((char*)base + align256((size_t)n * 64) + align256((size_t)n * 225 * 4 * 2));
     boards_to_rows_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_boards, n, rows);
     int rc;
     if ((rc = plan_check("boards_to_rows_kernel"))) return rc;
-    if ((rc = gz_gn_forward(d_gn_weights, rows, n, nullptr, gp, gq, nullptr, stream))) return rc;
+    if ((rc = gz_gn_forward(d_gn_weights, rows, n, nullptr, gp, gq, nullptr, rec, stream))) return rc;
     planner_move_kernel<<<n, WAVE, 0, s>>>(d_boards, d_ai, d_keys, n, *pp, gp, gq, d_moves, d_draws);
     return plan_check("planner_move_kernel");
 }
 
 extern "C" size_t gz_planner_move_workspace_bytes(int32_t n) {
-    return align256((size_t)(n < 1 ? 1 : n) * 64) + (size_t)(n < 1 ? 1 : n) * 225 * 4 * 2;
+    const size_t m = (size_t)(n < 1 ? 1 : n);
+    return align256(m * 64) + align256(m * 225 * 4 * 2) + gz_gn_workspace_bytes((int32_t)m);
 }

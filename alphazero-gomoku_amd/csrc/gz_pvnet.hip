@@ -638,32 +638,6 @@ constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;
 static_assert(HP_K % 16 == 0 && HV_K % 16 == 0 && HV_OFF % 4 == 0 && HSTRIDE % 4 == 0, "16-B A loads");
 
-__device__ __forceinline__ void heads_gemm_block(const float* __restrict__ Wt,
-                                                 int ldw, int kmax, int nmax, int kb, int lane, const int (&nt)[4],
-                                                 int ntn, f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
-    const int li = lane & 15, g = lane >> 4;
-    f32x4 a[4];
-#pragma unroll
-    for (int m = 0; m < 4; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        int k = 16 * kb + 4 * g + t;
-        k = k < kmax ? k : kmax - 1;  // A is zero there
-        float bv[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            int n = 16 * nt[q] + li;
-            n = n < nmax ? n : nmax - 1;
-            bv[q] = q < ntn ? Wt[(size_t)k * ldw + n] : 0.f;
-        }
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][t], bv[q], acc[m][q], 0, 0, 0);
-    }
-}
-
 __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restrict__ W, const float* __restrict__ hbuf,
                                                            int n, const int32_t* d_count, float* __restrict__ logits,
                                                            float* __restrict__ value, float* __restrict__ probs) {

@@ -213,6 +213,14 @@ class GNWeights:
         if blob.size != lib.gz_gn_weight_floats():
             raise ValueError(f"planner blob has {blob.size} floats, kernel expects {lib.gz_gn_weight_floats()}")
         self.tensor = torch.from_numpy(blob).cuda()
+        self._ws = None
+
+    def workspace_for(self, n):
+        """Device workspace of gz_gn_forward for n boards (grown on demand, kept)."""
+        need = int(require_gpu().gz_gn_workspace_bytes(max(1, int(n))))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+        return self._ws
 
 
 def gn_forward_dev(weights, d_boards, n, d_count=None, d_p=None, d_q=None, d_logits=None):
@@ -222,7 +230,7 @@ def gn_forward_dev(weights, d_boards, n, d_count=None, d_p=None, d_q=None, d_log
     if d_q is None:
         d_q = torch.empty(n * 225, dtype=torch.float32, device="cuda")
     _lib.check(lib.gz_gn_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_p), ptr(d_q),
-                                 ptr(d_logits), stream()), "gz_gn_forward")
+                                 ptr(d_logits), ptr(weights.workspace_for(n)), stream()), "gz_gn_forward")
     return d_p, d_q, d_logits
 
 

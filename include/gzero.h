@@ -175,10 +175,13 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
  * d_weights: packed blob of gz_gn_weight_floats() floats (csrc/gz_gnet.h,
  * gzero/planner_nets.py).  Boards [n][16] uint32 bit planes (d_count as above).
  * Outputs: p = softmax(GraphNet(planes)) [n][225], q = OpponentDQN(planes)
- * [n][225], logits [n][225] or NULL.  GraphNet convs in f16x3 (as GZ_PV_F16X3). */
+ * [n][225], logits [n][225] or NULL.  GraphNet convs in f16x3 (as GZ_PV_F16X3);
+ * the policy FC and the DQN run batched over 64 boards (fp32 MFMA).
+ * d_workspace: gz_gn_workspace_bytes(n) bytes, required. */
 size_t gz_gn_weight_floats(void);
+size_t gz_gn_workspace_bytes(int32_t n);
 int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                  float* d_p, float* d_q, float* d_logits, void* stream);
+                  float* d_p, float* d_q, float* d_logits, void* d_workspace, void* stream);
 
 /* ---- K4+K5+K7: MCTS with BG-planner rollout plies (planner_steps > 0) ----
  * gz_search's contract (ai_agent.py:109-222) for p->planner_steps >= 0 with the

@@ -14,6 +14,7 @@ from gzero import boards, device, planner_nets  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--check", type=int, default=256, help="boards checked against the torch fp32 nets")
 a = ap.parse_args()
 w = device.GNWeights(planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0),
                                                        planner_nets.init_dqn_state(1)))
@@ -36,3 +37,10 @@ for _ in range(a.iters):
 t = float(np.median(ts))
 fl = 2 * (planner_nets.GN_MACS + planner_nets.DQN_MACS)
 print(f"gn_kernel n={a.n}: {t*1e3:.2f} ms, {a.n/t:.0f} boards/s, {a.n*fl/t/1e12:.1f} TFLOP/s (fp32-equivalent)")
+if a.check:
+    ref_lg, ref_p, ref_q = planner_nets.reference_forward(
+        planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1), boards.planes_from_cells(cells[: a.check]))
+    dp = np.abs(p.view(a.n, 225)[: a.check].cpu().numpy() - ref_p).max()
+    dq = np.abs(q.view(a.n, 225)[: a.check].cpu().numpy() - ref_q).max()
+    print(f"  check {a.check} boards vs torch fp32: max |dp| {dp:.2e}, max |dq| {dq:.2e}",
+          "OK" if dp < 1e-6 and dq < 1e-4 else "FAIL")
