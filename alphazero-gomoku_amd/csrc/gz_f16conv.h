@@ -238,33 +238,28 @@ __device__ __forceinline__ float dot_col(const float* __restrict__ wp, int strid
 // One 16-deep K block of a batched fp32-MFMA GEMM over 4 tiles of 16 rows
 // (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation): in the t-th k-step
 // of block kb, lane group g multiplies k = 16kb + 4g + t, so a lane's A operand for
-// the 4 k-steps is one 16-byte load from its row arow[m] (rows zero past kmax).
-// B = Wt[k][n] (K-major, leading dimension ldw), n-tiles nt[0..ntn) of the wave.
+// the 4 k-steps is one 16-byte load from its row arow[m] (rows zero past K), and its
+// B operand is one 16-byte load from the packed weights
+//   Wp[kb][n-tile][lane 64][t 4] = W^T[16kb + 4(lane/16) + t][16 n-tile + lane%16]
+// (zero past K and N; gzero/weights.py pack_mfma_b).  n-tiles nt[0..ntn) of the wave.
 // Used by the batched FC heads of the PV and planner nets.
-__device__ __forceinline__ void heads_gemm_block(const float* __restrict__ Wt,
-                                                 int ldw, int kmax, int nmax, int kb, int lane, const int (&nt)[4],
-                                                 int ntn, f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
-    const int li = lane & 15, g = lane >> 4;
-    f32x4 a[4];
+__device__ __forceinline__ void heads_gemm_block(const float* __restrict__ Wp, int ntiles, int kb, int lane,
+                                                 const int (&nt)[4], int ntn, f32x4 (&acc)[4][4],
+                                                 const float* __restrict__ arow[4]) {
+    const int g = lane >> 4;
+    f32x4 a[4], b[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        int k = 16 * kb + 4 * g + t;
-        k = k < kmax ? k : kmax - 1;  // A is zero there
-        float bv[4];
+    for (int q = 0; q < 4; q++)
+        b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * ntiles + nt[q]) * 64 + lane) * 4) : zero4();
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            int n = 16 * nt[q] + li;
-            n = n < nmax ? n : nmax - 1;
-            bv[q] = q < ntn ? Wt[(size_t)k * ldw + n] : 0.f;
-        }
+    for (int t = 0; t < 4; t++)
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][t], bv[q], acc[m][q], 0, 0, 0);
-    }
+                if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][t], b[q][t], acc[m][q], 0, 0, 0);
 }
 
 }  // namespace gzc

@@ -48,7 +48,14 @@ constexpr int h_layer_off(int i) {
 // delta [450][256] = (black - empty) rows, then (white - empty) rows
 constexpr int D0_BASE = h_layer_off(8);
 constexpr int D0_DELTA = D0_BASE + DQH;
-constexpr int TOTAL = D0_DELTA + 450 * DQH;
+// the batched heads' GEMMs in MFMA B-fragment order (gz_f16conv.h heads_gemm_block):
+// [k-blocks of 16][n-tiles][64][4] of policy fc (450->225), the fc0 delta rows
+// (450->256), fc1 (256->256), fc2 (256->225)
+constexpr int GF_P = D0_DELTA + 450 * DQH;
+constexpr int D0_P = GF_P + 29 * 15 * 256;
+constexpr int D1_P = D0_P + 29 * 16 * 256;
+constexpr int D2_P = D1_P + 16 * 16 * 256;
+constexpr int TOTAL = D2_P + 16 * 15 * 256;
 
 // per-board record between gn_kernel (GraphNet tower + policy conv 1x1) and
 // gn_heads_kernel (policy FC + softmax, OpponentDQN): floats

@@ -239,17 +239,16 @@ constexpr int HB = 64;
 constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;   // logits rows
 constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
-static_assert(REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
+static_assert(REC_X == 29 * 16 && REC - REC_X == 29 * 16 && REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
 
-template <int KB>
-__device__ __forceinline__ void heads_gemm(const float* __restrict__ Wt, int ldw, int kmax, int nmax, int lane,
-                                           const int (&nt)[4], int ntn, f32x4 (&acc)[4][4],
-                                           const float* __restrict__ arow[4]) {
+template <int KB, int NTILES>
+__device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lane, const int (&nt)[4], int ntn,
+                                           f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
 #pragma unroll
     for (int m = 0; m < 4; m++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[m][q] = zero4();
-    for (int kb = 0; kb < KB; kb++) heads_gemm_block(Wt, ldw, kmax, nmax, kb, lane, nt, ntn, acc, arow);
+    for (int kb = 0; kb < KB; kb++) heads_gemm_block(Wp, NTILES, kb, lane, nt, ntn, acc, arow);
 }
 
 // acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles
@@ -305,7 +304,7 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
     }
     f32x4 acc[4][4];
     // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
-    heads_gemm<REC_X / 16>(W + GF_WT, POS, 2 * POS, POS, lane, nt, ntn_p, acc, arow);
+    heads_gemm<REC_X / 16, 15>(W + GF_P, lane, nt, ntn_p, acc, arow);
     heads_put<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
     __syncthreads();
     for (int bb = wave; bb < HB && b0 + bb < count; bb += 4) {  // wave w: boards w, w+4, ...
@@ -342,7 +341,7 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
         const float* ax[4];
 #pragma unroll
         for (int m = 0; m < 4; m++) ax[m] = arow[m] + REC_X;
-        heads_gemm<(REC - REC_X) / 16>(W + D0_DELTA, DQH, 2 * POS, DQH, lane, nt, 4, acc, ax);
+        heads_gemm<(REC - REC_X) / 16, 16>(W + D0_P, lane, nt, 4, acc, ax);
         heads_put<true>(acc, W + D0_BASE, DQH, nt, 4, lane, rb, H_STRIDE);
     }
     __syncthreads();  // rb complete; ra (logits) no longer read
@@ -350,13 +349,13 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
     // ---- fc1 256 -> 256 + ReLU into ra
 #pragma unroll
     for (int m = 0; m < 4; m++) ah[m] = rb + (16 * m + li) * H_STRIDE;
-    heads_gemm<DQH / 16>(W + D1_WT, DQH, DQH, DQH, lane, nt, 4, acc, ah);
+    heads_gemm<DQH / 16, 16>(W + D1_P, lane, nt, 4, acc, ah);
     heads_put<true>(acc, W + D1_B, DQH, nt, 4, lane, ra, H_STRIDE);
     __syncthreads();
     // ---- fc2 256 -> 225: q
 #pragma unroll
     for (int m = 0; m < 4; m++) ah[m] = ra + (16 * m + li) * H_STRIDE;
-    heads_gemm<DQH / 16>(W + D2_WT, POS, DQH, POS, lane, nt, ntn_p, acc, ah);
+    heads_gemm<DQH / 16, 15>(W + D2_P, lane, nt, ntn_p, acc, ah);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if (q >= ntn_p) continue;

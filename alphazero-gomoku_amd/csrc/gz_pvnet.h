@@ -42,7 +42,13 @@ constexpr int F16_STRIDE = K * CH;           // floats: K*CH halves hi + K*CH ha
 // conv0 in fp16 MFMA A-fragment order [n-tile 8][lane 64][8]: n = 16*n_tile + lane%16,
 // k = 8*(lane/16) + j (k >= 27 zero); hi then lo
 constexpr int F16_C0 = F16_RES0 + 4 * F16_STRIDE;
-constexpr int TOTAL = F16_C0 + 8 * 64 * 8;
+// FC heads in MFMA B-fragment order for the batched heads kernel (gz_f16conv.h
+// heads_gemm_block): policy_fc [29 k-blocks][15 n-tiles][64][4], value_fc1 [15][4][64][4]
+constexpr int PF_P = F16_C0 + 8 * 64 * 8;
+constexpr int PF_KB = 29, PF_NT = 15;
+constexpr int V1_P = PF_P + PF_KB * PF_NT * 256;
+constexpr int V1_KB = 15, V1_NT = 4;
+constexpr int TOTAL = V1_P + V1_KB * V1_NT * 256;
 
 // algorithmic work of one forward (neural_network.py:132-159), MACs
 constexpr long long MACS = 133690114LL;

@@ -636,7 +636,7 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
 constexpr int HB = 64;
 constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;
-static_assert(HP_K % 16 == 0 && HV_K % 16 == 0 && HV_OFF % 4 == 0 && HSTRIDE % 4 == 0, "16-B A loads");
+static_assert(HP_K == 16 * PF_KB && HV_K == 16 * V1_KB && HP_K % 16 == 0 && HV_K % 16 == 0 && HV_OFF % 4 == 0 && HSTRIDE % 4 == 0, "16-B A loads");
 
 __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restrict__ W, const float* __restrict__ hbuf,
                                                            int n, const int32_t* d_count, float* __restrict__ logits,
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
 #pragma unroll
             for (int q = 0; q < 4; q++) acc[m][q] = zero4();
         for (int kb = 0; kb < HP_K / 16; kb++)
-            heads_gemm_block(W + PF_WT, POS, 2 * POS, POS, kb, lane, nt, ntn, acc, arow);
+            heads_gemm_block(W + PF_P, PF_NT, kb, lane, nt, ntn, acc, arow);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (q >= ntn) continue;
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
 #pragma unroll
         for (int m = 0; m < 4; m++) acc[m][0] = zero4();
         for (int kb = 0; kb < HV_K / 16; kb++)
-            heads_gemm_block(W + V1_WT, 64, POS, 64, kb, lane, nt, 1, acc, arv);
+            heads_gemm_block(W + V1_P, V1_NT, kb, lane, nt, 1, acc, arv);
         const int j = 16 * wave + li;
         const float bias = W[V1_B + j];
 #pragma unroll

@@ -11,6 +11,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .weights import pack_mfma_b
+
 N = 15
 POS = N * N
 HID = 64
@@ -114,7 +116,11 @@ def _h_layer_off(i):
 # (black - empty) or (white - empty) row, base = bias + sum of the empty rows
 D0_BASE = _h_layer_off(8)              # [256]
 D0_DELTA = D0_BASE + DQN_H             # [450][256]: rows 0..224 black - empty, 225..449 white - empty
-GN_TOTAL = D0_DELTA + 450 * DQN_H
+GF_P = D0_DELTA + 450 * DQN_H          # batched heads, MFMA B-fragment order (weights.pack_mfma_b)
+D0_P = GF_P + 29 * 15 * 256
+D1_P = D0_P + 29 * 16 * 256
+D2_P = D1_P + 16 * 16 * 256
+GN_TOTAL = D2_P + 16 * 15 * 256
 GN_MACS = POS * (27 * HID + 4 * (K3 * HID + HID * HID) + 2 * HID) + 450 * POS
 DQN_MACS = 3 * POS * DQN_H + DQN_H * DQN_H + DQN_H * POS
 
@@ -172,6 +178,10 @@ def pack_planner_weights(gn_sd, dqn_sd):
     blob[D0_BASE:D0_BASE + DQN_H] = (d["net.0.bias"].astype(np.float64) + w0[2 * POS:].sum(0)).astype(np.float32)
     delta = np.concatenate([w0[:POS] - w0[2 * POS:], w0[POS:2 * POS] - w0[2 * POS:]])
     blob[D0_DELTA:D0_DELTA + 450 * DQN_H] = delta.astype(np.float32).reshape(-1)
+    blob[GF_P:D0_P] = pack_mfma_b(g["policy_head.2.weight"].T, 29, 15)
+    blob[D0_P:D1_P] = pack_mfma_b(delta.astype(np.float32), 29, 16)
+    blob[D1_P:D2_P] = pack_mfma_b(d["net.2.weight"].T, 16, 16)
+    blob[D2_P:GN_TOTAL] = pack_mfma_b(d["net.4.weight"].T, 16, 15)
     return blob
 
 

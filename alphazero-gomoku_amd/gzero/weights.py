@@ -143,12 +143,27 @@ V2_B = V2_W + 64
 F16_RES0 = (V2_B + 4 + 3) & ~3  # 16-byte aligned (h8 loads)
 F16_STRIDE = K * CH
 F16_C0 = F16_RES0 + 4 * F16_STRIDE
-TOTAL = F16_C0 + 8 * 64 * 8
+PF_P = F16_C0 + 8 * 64 * 8
+PF_KB, PF_NT = 29, 15
+V1_P = PF_P + PF_KB * PF_NT * 256
+V1_KB, V1_NT = 15, 4
+TOTAL = V1_P + V1_KB * V1_NT * 256
 
 PRECISIONS = {"fp32": 0, "f16x3": 1}  # GZ_PV_FP32, GZ_PV_F16X3
 
 PV_MACS = 133_690_114  # conv0 777,600 + 4 x 33,177,600 + heads 202,114
 PV_FLOPS = 2 * PV_MACS
+
+
+def pack_mfma_b(wt, kb, nt):
+    """W^T [K][N] (K-major) -> MFMA B-fragment order [kb][nt][lane 64][4] of the
+    batched heads (csrc/gz_f16conv.h heads_gemm_block): element (kb, t, lane, j) =
+    W^T[16 kb + 4 (lane // 16) + j][16 t + lane % 16], zero past K and N."""
+    wt = np.asarray(wt, np.float32)
+    pad = np.zeros((16 * kb, 16 * nt), np.float32)
+    pad[:wt.shape[0], :wt.shape[1]] = wt
+    # [kb][g 4][j 4][nt][li 16] -> [kb][nt][g][li][j]
+    return pad.reshape(kb, 4, 4, nt, 16).transpose(0, 3, 1, 4, 2).reshape(-1)
 
 
 def pack_pv_weights(sd):
@@ -203,6 +218,8 @@ def pack_pv_weights(sd):
     blob[V1_B:V1_B + 64] = sd["value_fc1.bias"].numpy()
     blob[V2_W:V2_W + 64] = sd["value_fc2.weight"].reshape(64).numpy()
     blob[V2_B] = float(sd["value_fc2.bias"][0])
+    blob[PF_P:V1_P] = pack_mfma_b(sd["policy_fc.weight"].t().numpy(), PF_KB, PF_NT)
+    blob[V1_P:TOTAL] = pack_mfma_b(sd["value_fc1.weight"].t().numpy(), V1_KB, V1_NT)
     return blob
 
 
