@@ -163,6 +163,36 @@ __device__ inline int pow3(int i) {
     return r;
 }
 
+// After `who` plays the empty cell at grid index g0: is there an empty cell f != g0
+// where `who` then completes five with g0 inside the five?  (A five through f that
+// avoids g0 was already a threat before the move.)  Every 5-window along the 4
+// lines through g0 (border cells read 3: blocked) with 3 of who's stones and one
+// empty cell besides g0 gives such an f.
+__device__ inline bool new_five_through(const uint8_t* grid, int g0, int who) {
+    const int STEP[4] = {GRID_W, 1, GRID_W + 1, GRID_W - 1};  // (1,0) (0,1) (1,1) (1,-1)
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        int st[9], em[9];
+#pragma unroll
+        for (int k = -4; k <= 4; k++) {
+            const int v = k == 0 ? who : grid[g0 + k * STEP[d]];
+            st[k + 4] = v == who;
+            em[k + 4] = v == 0;
+        }
+#pragma unroll
+        for (int s0 = 0; s0 <= 4; s0++) {
+            int ns = 0, ne = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                ns += st[s0 + k];
+                ne += em[s0 + k];
+            }
+            if (ns == 4 && ne == 1) return true;  // g0 + 3 stones, one empty cell
+        }
+    }
+    return false;
+}
+
 __device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, int mover, int n_moves, int P,
                             const gz_planner_params& pp, const float* __restrict__ pv, const float* __restrict__ qv,
                             uint64_t key, uint32_t* cnt) {
@@ -228,11 +258,12 @@ __device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, in
                 f.w[bit >> 5] &= ~(1u << (bit & 31));
                 opp_wins = bb_any(f);
             } else {
-                BB o2 = Ost;
-                bb_set(o2, bit);
-                BB f = threats(o2).win & E;
+                // the mover is P's opponent: after m it completes five at a cell f != m
+                // iff f already did (Fo) or a five-window through m holds 3 of its
+                // stones, m and the empty f (new_five_through)
+                BB f = Fo;
                 f.w[bit >> 5] &= ~(1u << (bit & 31));
-                opp_wins = bb_any(f);
+                opp_wins = bb_any(f) || new_five_through(sh->grid, (r + 4) * GRID_W + (c + 4), oppP);
             }
             if (opp_wins) {
                 score = -1e5;
