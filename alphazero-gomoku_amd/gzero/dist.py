@@ -22,16 +22,26 @@ def world():
     return 0, 1
 
 
+def local_device():
+    """GPU of this rank: LOCAL_RANK (one process per GPU).  GZ_DIST_SAME_DEVICE=1 puts
+    every rank on GPU 0 -- a rehearsal of the multi-rank path on a one-GPU box, with
+    GZ_DIST_BACKEND=gloo (RCCL refuses two ranks on one device)."""
+    if os.environ.get("GZ_DIST_SAME_DEVICE") == "1":
+        return 0
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def init_from_env(backend=None):
-    """Initialise torch.distributed from torchrun's env vars (no-op for WORLD_SIZE=1)."""
+    """Initialise torch.distributed from torchrun's env vars (no-op for WORLD_SIZE=1).
+    Backend: `backend`, else GZ_DIST_BACKEND, else nccl (= RCCL) with a GPU, gloo without."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1 or dist.is_initialized():
         return world()
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("GZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device())
     dist.init_process_group(backend=backend)
     return world()
 

@@ -48,12 +48,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_traffic():
+def load_traffic(boards):
+    """HBM bytes per PV launch of `boards` boards: rocprof FETCH_SIZE + WRITE_SIZE per board
+    (profiles/pv_traffic.json, collected by profiles/collect.sh) x boards, or None."""
     p = os.path.join(REPO, "profiles", "pv_traffic.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        return d.get("bytes_per_launch"), d
+        if d.get("bytes_per_board"):
+            return round(d["bytes_per_board"] * boards, 1), d
     return None, None
 
 
@@ -134,8 +137,7 @@ def main():
     args = ap.parse_args()
 
     rank, ws = gdist.init_from_env()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(gdist.local_device())
     if ws != args.gpus and rank == 0:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")
 
@@ -196,7 +198,7 @@ def main():
     mean_leaves = float(np.mean(leaves))
     mean_pv_s = float(np.mean(pv_ms)) / 1e3
     achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
-    traffic, _ = load_traffic()
+    traffic, _ = load_traffic(mean_leaves) if args.pv_precision == "f16x3" else (None, None)
     if args.pv_precision == "fp32":
         peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
     else:
