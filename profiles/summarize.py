@@ -4,11 +4,12 @@ rocprofv3 kernel trace and per-launch HBM-side bytes from the separate
 FETCH_SIZE / WRITE_SIZE passes.
 
 Bytes: rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md
-(HBM section) FETCH_SIZE reads 1/2 of the bytes of a WIDE (16 B/lane) coalesced
-stream on gfx950; the PV forward's HBM reads are a mix of 16-B weight-fragment
-loads (L2 hits after the first board), 4-B board and 16-B head-record loads, and
-the self-play kernel's accesses are mixed too, i.e. uncalibrated widths, so the
-raw counter is reported (corrected = raw, flagged) rather than guessing a factor.
+(HBM section) FETCH_SIZE reads 1/2 of the bytes of a wide (16 B/lane) coalesced
+stream on gfx950 and other widths must be calibrated on a known byte count:
+tools/hbm_calib.hip streams 1 GiB through each width the PV forward uses
+(profiles/r01/hbm_calib.json): FETCH_SIZE = 0.500 x bytes for 4-B AND 16-B
+coalesced loads, WRITE_SIZE = 1.000 x bytes for 4-B and 16-B stores.  So
+corrected bytes = 2 x FETCH_SIZE + WRITE_SIZE (the raw sum is kept beside it).
 
 The PV forward (one gz_pv_forward) is two kernels for f16x3: pv_kernel_f16x3
 (tower) and pv_heads_kernel (batched FC heads); both are summed as "pv_forward".
@@ -67,16 +68,18 @@ for k in PVK + ["selfplay_kernel"]:
         summary["kernels"].setdefault(k, {})["hbm_bytes_per_launch"] = {
             "fetch_raw": sum(f) / len(f) * 1024, "write": sum(w) / len(w) * 1024,
             "total_raw": (sum(f) / len(f) + sum(w) / len(w)) * 1024,
-            "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024; access widths uncalibrated -> raw"}
+            "total": (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024,
+            "note": "total = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), calibrated by tools/hbm_calib.hip"}
 boards = bench["config"]["pv_boards_per_step"]
 pvf = {"kernels": PVK,
        "avg_ms_timed_window": sum(summary["kernels"][k]["avg_ms_timed_window"] for k in PVK)}
 if PVK and all("hbm_bytes_per_launch" in summary["kernels"][k] for k in PVK):
-    tb = sum(summary["kernels"][k]["hbm_bytes_per_launch"]["total_raw"] for k in PVK)
+    tb = sum(summary["kernels"][k]["hbm_bytes_per_launch"]["total"] for k in PVK)
     pvf["hbm_bytes_per_launch"] = tb
     json.dump({"bytes_per_launch": tb, "boards_per_launch": boards, "bytes_per_board": tb / boards,
                "algorithmic_bytes_per_board": 64 + 225 * 4 * 2 + 4,
-               "note": "f16x3: includes the tower -> heads record (2,816 B written and read per board)",
+               "note": ("2 x FETCH_SIZE + WRITE_SIZE (tools/hbm_calib.hip calibration); f16x3: includes the "
+                        "tower -> heads record (2,816 B written and read per board)"),
                "kernels": PVK, "source": src},
               open(os.path.join(os.path.dirname(dst.rstrip("/")), "pv_traffic.json"), "w"), indent=1)
 summary["pv_forward"] = pvf
