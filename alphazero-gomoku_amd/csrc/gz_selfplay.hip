@@ -521,7 +521,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
     }
     int64_t game_id = h->game_id;
     const int64_t gstride = h->game_id_stride;
-    long long games = 0, moves_played = 0;
+    long long games = 0, moves_played = 0, mcts_played = 0;
     Tree t = tree_at(smem, p.num_simulations);
     __syncthreads();
     for (int it = 0; it < n_plies; it++) {
@@ -551,6 +551,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         __syncthreads();
         const int over = win ? player : ((ne == 1 || n_moves + 1 >= 200) ? 3 : 0);
         moves_played++;
+        mcts_played += n_moves >= 6;  // (plies 0-5: _opening_move, never a search)
         if (over) {  // buf.finalize_with_winner (training.py:89-94) and restart
             const int winner = over == 3 ? 0 : over;
             const int n = n_moves + 1;
@@ -589,6 +590,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         h->games_done += games;
         atomicAdd((unsigned long long*)&ctr->moves, (unsigned long long)moves_played);
         atomicAdd((unsigned long long*)&ctr->games, (unsigned long long)games);
+        atomicAdd((unsigned long long*)&ctr->mcts_moves, (unsigned long long)mcts_played);
     }
 }
 
@@ -658,6 +660,7 @@ __global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int 
         h->player = over ? 1 : 3 - player;
         h->games_done += games;
         atomicAdd((unsigned long long*)&ctr->moves, 1ull);
+        if (n_moves >= 6) atomicAdd((unsigned long long*)&ctr->mcts_moves, 1ull);
         if (games) atomicAdd((unsigned long long*)&ctr->games, 1ull);
     }
 }

@@ -69,11 +69,11 @@ class SearchStats(ctypes.Structure):
 class SelfplayCounters(ctypes.Structure):
     _fields_ = [("records", ctypes.c_int32), ("leaves", ctypes.c_int32),
                 ("records_dropped", ctypes.c_int32), ("leaves_dropped", ctypes.c_int32),
-                ("moves", ctypes.c_int64), ("games", ctypes.c_int64)]
+                ("moves", ctypes.c_int64), ("games", ctypes.c_int64), ("mcts_moves", ctypes.c_int64)]
 
 
 assert ctypes.sizeof(BoardState) == 80 and ctypes.sizeof(Record) == 80
-assert ctypes.sizeof(SearchStats) == 24 and ctypes.sizeof(SelfplayCounters) == 32
+assert ctypes.sizeof(SearchStats) == 24 and ctypes.sizeof(SelfplayCounters) == 40
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32

@@ -19,7 +19,8 @@ from .boards import RECORD_DTYPE, STATE_DTYPE, words_to_cells
 from .device import GNWeights, PVWeights, ptr, require_gpu, search_params, stream
 
 COUNTER_DTYPE = np.dtype([("records", "<i4"), ("leaves", "<i4"), ("records_dropped", "<i4"),
-                          ("leaves_dropped", "<i4"), ("moves", "<i8"), ("games", "<i8")])
+                          ("leaves_dropped", "<i4"), ("moves", "<i8"), ("games", "<i8"),
+                          ("mcts_moves", "<i8")])
 
 
 class SelfPlayEngine:
@@ -80,6 +81,22 @@ class SelfPlayEngine:
         _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
                                             self.leaf_cap, ptr(self.d_counters), stream()), "gz_selfplay_run")
+
+    def advance(self, n_plies):
+        """Play n_plies plies on every slot without gathering leaves for the PV forward
+        (the moves are the same either way: the search never reads the priors,
+        ai_agent.py:523).  Used to bring the slots to a steady-state mix of game plies
+        (continuous refill) before a measurement; records of games finished here are
+        not kept."""
+        if self.planner_steps:
+            raise ValueError("advance() is for planner_steps == 0 (planner plies need the GN forward)")
+        p = _lib.SearchParams.from_buffer_copy(self.params)
+        p.flags = 0
+        for _ in range(int(n_plies)):
+            self.d_counters.zero_()
+            _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(p), 1,
+                                                ptr(self.d_records), self.record_cap, None, 0,
+                                                ptr(self.d_counters), stream()), "gz_selfplay_run")
 
     def launch_pv(self):
         if not self.gather:

@@ -6,6 +6,11 @@ empty board, 200 simulations per move, medium difficulty (c_puct 1.6,
 exploration 0.05), beta = 0, planner_steps = 0, random-init network weights
 (numpy default_rng(0)), continuous refill of finished games.
 
+Measured in steady state: every slot first plays --burn-in plies (default 96)
+without the PV forward -- the moves are the same, the search never reads the
+priors -- so the timed window sees continuous refill's mix of game plies (opening
+plies included) rather than the synchronised start of 4096 fresh games.
+
 One "step" = every game slot plays `--plies-per-step` plies (one kernel launch,
 one wavefront per game) followed by the policy-value forward of EVERY node
 those searches created -- the GomokuModel.predict calls the reference makes
@@ -118,8 +123,8 @@ def cpu_baseline(positions, sims, seed, budget_s, torch_threads):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--slots", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=200)
     ap.add_argument("--beta", type=float, default=0.0)
@@ -132,6 +137,9 @@ def main():
     ap.add_argument("--no-elided", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--burn-in", type=int, default=None,
+                    help="plies played before the warm-up without the PV forward, so the timed window sees the "
+                         "steady-state mix of game plies of continuous refill (default 96; 0 in planner mode)")
     ap.add_argument("--planner-steps", type=int, default=0,
                     help="BG-planner plies per rollout (BASELINE config 4: 5 with --beta 0.2)")
     args = ap.parse_args()
@@ -172,6 +180,9 @@ def main():
             gathered[0] += out.numel()
         return ev, ctr
 
+    burn_in = args.burn_in if args.burn_in is not None else (0 if args.planner_steps else 96)
+    if burn_in:
+        eng.advance(burn_in)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -185,12 +196,14 @@ def main():
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
     ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c in recs]
-    moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs))], dtype=torch.float64, device="cuda")
+    moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs)), float(sum(int(c["mcts_moves"]) for c in ctrs))],
+                         dtype=torch.float64, device="cuda")
     if ws > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(moves, op=dist.ReduceOp.SUM)
     T = float(elapsed.item())
-    total_moves = float(moves.item())
+    total_moves = float(moves[0].item())
+    total_mcts = float(moves[1].item())
     value = total_moves / T
     pv_ms = [a.elapsed_time(b) for (a, b), _ in recs]
     leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
@@ -239,18 +252,24 @@ def main():
             "config": {
                 "workload": (f"BASELINE config {4 if args.planner_steps else 2}: {args.slots} concurrent self-play "
                              f"games per GPU, 15x15, {args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), "
-                             f"beta={args.beta}, planner_steps={args.planner_steps}, continuous refill; policy-value "
+                             f"beta={args.beta}, planner_steps={args.planner_steps}, continuous refill (timed after "
+                             f"{burn_in} burn-in plies: the steady-state mix of game plies); policy-value "
                              "forward on every non-terminal node the searches create (reference-work mode, "
                              f"{args.pv_precision})"),
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,
                 "plies_per_step": P,
+                "burn_in_plies": burn_in,
                 "parallelism": f"dp{ws} (games sharded by id, all-gather of records)",
                 "pv_boards_per_step": round(mean_leaves, 1),
                 "pv_boards_dropped": dropped,
             },
             "roofline": roofline,
+            "mcts_moves": {"value": round(total_mcts / T, 3), "unit": "moves/s",
+                           "share": round(total_mcts / total_moves, 4) if total_moves else None,
+                           "note": "plies decided by a search (SURVEY 8d): value counts every ply, incl. the opening "
+                                   "plies 0-5 that _opening_move plays without one (ai_agent.py:138-166)"},
         }
 
     # ---- prior-elided run (same kernel, no PV gather / forward)

@@ -95,6 +95,8 @@ typedef struct gz_selfplay_counters {
     int32_t leaves_dropped;
     int64_t moves;           /* plies played */
     int64_t games;           /* games finished */
+    int64_t mcts_moves;      /* plies decided by MCTS (n_moves >= 6; the opening plies
+                                0-5 of _opening_move do no search, ai_agent.py:138-166) */
 } gz_selfplay_counters;
 
 const char* gz_last_error(void);
