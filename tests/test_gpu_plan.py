@@ -168,3 +168,24 @@ def test_selfplay_planner_games_vs_oracle(oracle, gnw):
         ref = oracle.play_game(prm, prm, gid)
         assert g["moves"] == ref["moves"], gid
         assert g["z"] == ref["z"], gid
+
+
+def test_config1_game_vs_oracle(oracle, gnw):
+    """BASELINE config 1 (1 game, 50 sims, beta 0.2, planner_steps 5, medium), played to
+    the end by the self-play engine: moves, players and z equal the oracle's
+    play_one_game driven by the GPU's net outputs (injected p / q)."""
+    from gzero.selfplay import SelfPlayEngine, records_to_games
+    eng = SelfPlayEngine(n_slots=1, num_simulations=50, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED,
+                         plies_per_step=16, planner_steps=5, planner_difficulty="medium", gn_weights=gnw)
+    game = None
+    for _ in range(13):  # <= 200 plies
+        eng.step()
+        got = records_to_games(eng.records())
+        if 0 in got:
+            game = got[0]
+            break
+    assert game is not None
+    prm = oracle.make_params("medium", sims=50, beta=0.2, seed=SEED, planner_steps=5, pq=_pq_from_gpu(gnw))
+    ref = oracle.play_game(prm, prm, 0)
+    assert game["moves"] == ref["moves"]
+    assert game["players"] == ref["players"] and game["z"] == ref["z"]
