@@ -74,3 +74,27 @@ def test_selfplay_leaf_count_equals_reference_predicts(oracle):
         assert c["moves"] == ref["n"] and c["games"] == 1
         assert c["leaves"] == ref["predicts"]
         assert c["leaves_dropped"] == 0
+
+
+def test_sharded_ranks_play_the_single_gpu_games():
+    """Config 3's sharding (gzero.dist.shard_ids): rank r of W plays game ids
+    r*S + s + g*W*S.  Two 'ranks' of 8 slots each produce exactly the games that one
+    16-slot engine plays for the same ids (a game's RNG streams depend only on its id),
+    so an N-GPU run is the 1-GPU run's games, partitioned."""
+    from gzero import dist as gdist
+    S, W = 8, 2
+    one = SelfPlayEngine(n_slots=S * W, num_simulations=6, beta=0.2, seed=SEED, plies_per_step=40)
+    ref = records_to_games(_play(one, 120, chunk=40))
+    shard = {}
+    for r in range(W):
+        base, stride = gdist.shard_ids(r, W, S)
+        eng = SelfPlayEngine(n_slots=S, num_simulations=6, beta=0.2, seed=SEED, plies_per_step=40,
+                             game_id_base=base, game_id_stride=stride)
+        for gid, g in records_to_games(_play(eng, 120, chunk=40)).items():
+            assert gid % (W * S) // S == r  # disjoint by construction
+            shard[gid] = g
+    common = sorted(set(ref) & set(shard))
+    assert len(common) >= S
+    for gid in common:
+        assert shard[gid]["moves"] == ref[gid]["moves"], gid
+        assert shard[gid]["z"] == ref[gid]["z"], gid
