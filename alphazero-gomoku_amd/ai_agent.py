@@ -142,3 +142,23 @@ class AIFactory:
     @staticmethod
     def get_available_difficulties() -> List[str]:
         return ["easy", "medium", "hard"]
+
+
+def test_ai():
+    """Module smoke check, as the reference's (ai_agent.py:626-660): one medium move on
+    the empty board, its position evaluation and the auto-save; failures are printed,
+    not raised (like the reference's)."""
+    board = GomokuBoard()
+    try:
+        ai = AIFactory.create_ai("alphazero", board.BLACK, "medium")
+        t0 = time.time()
+        move = ai.get_move(board)
+        print(f"move {move} in {time.time() - t0:.3f}s | evaluation {ai.evaluate_position(board):.3f}")
+        ai._auto_save_model()
+        print("AlphaZero AI smoke check passed")
+    except Exception as e:  # noqa: BLE001 (reported, as the reference does)
+        print(f"AlphaZero AI smoke check failed: {e}")
+
+
+if __name__ == "__main__":
+    test_ai()

@@ -128,3 +128,25 @@ class GomokuBoard:
         from gzero.boards import make_states
         return make_states(self.board.reshape(1, -1), n_moves=self.get_move_count(),
                            player=self.current_player, over=int(self.game_over), winner=self.winner or 0)
+
+
+def test_gomoku_board():
+    """Module smoke check, as the reference's (gomoku_board.py:330-373): prints a
+    board, plays the centre, five alternating stones along a row, and an undo."""
+    b = GomokuBoard()
+    print(b)
+    print("current player", b.current_player, "| valid moves", len(b.get_valid_moves()))
+    print("make_move(7, 7):", b.make_move(7, 7))
+    five = GomokuBoard()
+    for c in range(5):
+        five.make_move(7, 7 + c)  # the colours alternate along row 7, so no five forms (as in the reference)
+    print(five)
+    print("game over", five.game_over, "| winner", five.winner)
+    b.make_move(6, 6)
+    b.undo_move()
+    print(b)
+    print("GomokuBoard smoke check done")
+
+
+if __name__ == "__main__":
+    test_gomoku_board()

@@ -136,3 +136,25 @@ class GomokuModel:
 def create_pretrained_model(board_size: int = 15) -> GomokuModel:
     path = f"models/pretrained_gomoku_{board_size}x{board_size}.pth"
     return GomokuModel(path if os.path.exists(path) else None, board_size)
+
+
+def test_model():
+    """Module smoke check, as the reference's (neural_network.py:385-424): predict on a
+    board with one centre stone, the masked move probabilities, and a save/load round
+    trip through models/test_model.pth (removed afterwards).  Needs the GPU engine."""
+    model = GomokuModel()
+    board_state = np.zeros((15, 15), dtype=int)
+    board_state[7, 7] = 1
+    policy, value = model.predict(board_state)
+    print("policy", policy.shape, "sum", float(np.sum(policy)), "| value", value)
+    print("move probabilities", model.get_move_probabilities(board_state, [(7, 6), (7, 8), (6, 7), (8, 7)]))
+    path = "models/test_model.pth"
+    model.save_model(path)
+    print("reloaded:", GomokuModel().load_model(path))
+    if os.path.exists(path):
+        os.remove(path)
+    print("GomokuModel smoke check done")
+
+
+if __name__ == "__main__":
+    test_model()

@@ -127,3 +127,18 @@ def test_ai_with_planner_golden():
         same += (mv[0] * 15 + mv[1]) == c["move"]
         assert ai.last_search_stats["predicts"] == c["predicts"]
     assert same >= 18
+
+
+def test_module_smoke_checks(tmp_path, monkeypatch, capsys):
+    """The reference's per-module smoke functions (test_gomoku_board, test_model,
+    test_ai) exist on the drop-in modules and run on the GPU engine."""
+    import ai_agent
+    import gomoku_board
+    import neural_network
+    monkeypatch.chdir(tmp_path)  # test_model / _auto_save_model write under ./models
+    gomoku_board.test_gomoku_board()
+    neural_network.test_model()
+    ai_agent.test_ai()
+    out = capsys.readouterr().out
+    assert "reloaded: True" in out
+    assert "AlphaZero AI smoke check passed" in out
