@@ -65,6 +65,15 @@ def load_traffic(boards):
     return None, None
 
 
+def load_clock(kernel):
+    """Measured shader clock and MFMA-busy share of `kernel` under load, or None."""
+    p = os.path.join(REPO, "profiles", "r01", "clock.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("kernels", {}).get(kernel)
+    return None
+
+
 def cpu_baseline(positions, sims, seed, budget_s, torch_threads):
     """C oracle (single thread) searching the same positions the GPU starts its
     timed window from, plus torch-CPU fp32 forwards for the nodes it created."""
@@ -233,6 +242,12 @@ def main():
                        "avg_ms": round(float(np.mean(pv_ms)), 3)},
         "note": note,
     }
+    clk = load_clock("pv_kernel_f16x3" if args.pv_precision == "f16x3" else "pv_kernel_f32")
+    if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
+        roofline["clock"] = {"ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
+                             "peak_at_clock": round(peak * clk["median_ghz"] / 2.4, 1),
+                             "frac_at_clock": round(achieved / (peak * clk["median_ghz"] / 2.4), 4),
+                             "source": "profiles/r01/clock.json (rocprofv3 GRBM_GUI_ACTIVE / duration)"}
 
     out = None
     if rank == 0:
