@@ -742,6 +742,90 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
     }
 }
 
+// ============================================================ masked prior (ai_agent.py:564-582)
+// MCTSNode._get_prior_probability: the float32 softmax at the node's unexplored
+// moves (the empty cells in row-major order, gomoku_board.py:201-213) as float64,
+// divided by their float64 np.sum when it is > 0.  np.sum of a contiguous float64
+// vector is numpy's pairwise summation (blocks of <= 128 terms: < 8 terms left to
+// right from 0.0, else 8 interleaved accumulators combined ((0+1)+(2+3))+((4+5)+(6+7))
+// plus the remainder left to right; longer vectors split at n/2 rounded down to a
+// multiple of 8), restated here term for term so the sum rounds exactly like the
+// reference's (oracle.np_pairwise_sum).  Output: dense [n][225] float64, the prior at
+// empty cells and 0 at stones (the reference's compact vector = dense[empty cells]).
+// One workgroup per 64 boards; lane b of wave 0 sums board b.
+constexpr int PR_B = 64;
+
+__device__ double np_pairwise_block(const float* a, int m) {
+    if (m < 8) {
+        double res = 0.0;
+        for (int i = 0; i < m; i++) res += (double)a[i];
+        return res;
+    }
+    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int i = 8;
+    for (; i < m - (m % 8); i += 8) {
+        r0 += (double)a[i];
+        r1 += (double)a[i + 1];
+        r2 += (double)a[i + 2];
+        r3 += (double)a[i + 3];
+        r4 += (double)a[i + 4];
+        r5 += (double)a[i + 5];
+        r6 += (double)a[i + 6];
+        r7 += (double)a[i + 7];
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < m; i++) res += (double)a[i];
+    return res;
+}
+
+__global__ __launch_bounds__(256) void pv_prior_kernel(const uint32_t* __restrict__ boards, int n, const int32_t* d_count,
+                                                       const float* __restrict__ probs, double* __restrict__ prior) {
+    __shared__ float p[PR_B * POS];          // probs, then each board's empty-cell terms compacted in place
+    __shared__ uint32_t occ[PR_B * 8];       // stones (black | white) per board
+    __shared__ double psum[PR_B];
+    const int count = board_count(n, d_count);
+    const int b0 = blockIdx.x * PR_B;
+    if (b0 >= count) return;
+    const int nb = count - b0 < PR_B ? count - b0 : PR_B;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < nb * POS; i += 256) p[i] = probs[(size_t)b0 * POS + i];
+    for (int i = tid; i < nb * 8; i += 256) {
+        const uint32_t* bd = boards + (size_t)(b0 + (i >> 3)) * 16;
+        occ[i] = bd[i & 7] | bd[8 + (i & 7)];
+    }
+    __syncthreads();
+    if (tid < nb) {
+        float* a = p + tid * POS;
+        const uint32_t* o = occ + tid * 8;
+        int k = 0;
+        for (int cell = 0; cell < POS; cell++) {  // row-major empty cells (k <= cell: in place is safe)
+            const int bit = (cell / 15) * 16 + cell % 15;
+            if (!((o[bit >> 5] >> (bit & 31)) & 1u)) a[k++] = a[cell];
+        }
+        double s;
+        if (k <= 128) {
+            s = np_pairwise_block(a, k);
+        } else {
+            int k2 = k / 2;
+            k2 -= k2 % 8;
+            s = np_pairwise_block(a, k2) + np_pairwise_block(a + k2, k - k2);
+        }
+        psum[tid] = s;
+    }
+    __syncthreads();
+    for (int i = tid; i < nb * POS; i += 256) {
+        const int bb = i / POS, cell = i % POS;
+        const int bit = (cell / 15) * 16 + cell % 15;
+        double v = 0.0;
+        if (!((occ[bb * 8 + (bit >> 5)] >> (bit & 31)) & 1u)) {
+            const double x = (double)probs[(size_t)(b0 + bb) * POS + cell];
+            const double s = psum[bb];
+            v = s > 0.0 ? x / s : x;
+        }
+        prior[(size_t)(b0 + bb) * POS + cell] = v;
+    }
+}
+
 }  // namespace
 
 #ifdef GZ_PV_STAMPS
@@ -774,8 +858,8 @@ extern "C" size_t gz_pv_workspace_bytes(int32_t n) {
 }
 
 extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                             float* d_logits, float* d_value, float* d_probs, void* d_workspace, int32_t precision,
-                             void* stream) {
+                             float* d_logits, float* d_value, float* d_probs, double* d_prior, void* d_workspace,
+                             int32_t precision, void* stream) {
     if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_logits || !d_value))) {
         gz_internal_set_error("gz_pv_forward: bad arguments");
         return GZ_ERR_ARG;
@@ -786,6 +870,10 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
     }
     if (!d_workspace) {
         gz_internal_set_error("gz_pv_forward: d_workspace is required");
+        return GZ_ERR_ARG;
+    }
+    if (d_prior && !d_probs) {
+        gz_internal_set_error("gz_pv_forward: d_prior needs d_probs (the prior is renormalised from the softmax)");
         return GZ_ERR_ARG;
     }
     if (n == 0) return GZ_OK;
@@ -800,6 +888,7 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
         pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count,
                                                            d_logits, d_value, d_probs);
     }
+    if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_kernel: ") + hipGetErrorString(e)).c_str());

@@ -96,7 +96,7 @@ SIGNATURES = {
     "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "gz_pv_weight_floats": (_SZ, []),
     "gz_pv_workspace_bytes": (_SZ, [_I32]),
-    "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _P]),
+    "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "gz_gn_weight_floats": (_SZ, []),
     "gz_gn_workspace_bytes": (_SZ, [_I32]),
     "gz_gn_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),

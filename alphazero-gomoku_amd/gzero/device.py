@@ -180,28 +180,35 @@ class PVWeights:
         return self.workspace
 
 
-def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=None, d_probs=None):
-    """Device-resident forward: d_boards int32/uint32 tensor [n,16]; returns output tensors."""
+def pv_forward_dev(weights, d_boards, n, d_count=None, d_logits=None, d_value=None, d_probs=None, d_prior=None):
+    """Device-resident forward: d_boards int32/uint32 tensor [n,16]; returns output tensors.
+    d_prior (float64 [n*225], needs d_probs): MCTSNode._get_prior_probability, dense."""
     lib = require_gpu()
     if d_logits is None:
         d_logits = torch.empty(n * 225, dtype=torch.float32, device="cuda")
     if d_value is None:
         d_value = torch.empty(n, dtype=torch.float32, device="cuda")
     _lib.check(lib.gz_pv_forward(ptr(weights.tensor), ptr(d_boards), int(n), ptr(d_count), ptr(d_logits),
-                                 ptr(d_value), ptr(d_probs), ptr(weights.workspace_for(n)), weights.mode, stream()),
+                                 ptr(d_value), ptr(d_probs), ptr(d_prior), ptr(weights.workspace_for(n)),
+                                 weights.mode, stream()),
                "gz_pv_forward")
     return d_logits, d_value, d_probs
 
 
-def pv_forward(weights, leaf_rows):
-    """Host convenience: [n,16] uint32 leaf rows -> (logits [n,225], value [n], probs [n,225])."""
+def pv_forward(weights, leaf_rows, want_prior=False):
+    """Host convenience: [n,16] uint32 leaf rows -> (logits [n,225], value [n], probs [n,225])
+    (+ prior [n,225] float64, dense over cells, 0 at stones, if want_prior)."""
     rows = np.ascontiguousarray(leaf_rows, np.uint32).reshape(-1, 16)
     n = rows.shape[0]
     d_b = torch.from_numpy(rows.view(np.int32).copy()).cuda()
     d_probs = torch.empty(n * 225, dtype=torch.float32, device="cuda")
-    lg, v, pr = pv_forward_dev(weights, d_b, n, d_probs=d_probs)
+    d_prior = torch.empty(n * 225, dtype=torch.float64, device="cuda") if want_prior else None
+    lg, v, pr = pv_forward_dev(weights, d_b, n, d_probs=d_probs, d_prior=d_prior)
     torch.cuda.synchronize()
-    return lg.cpu().numpy().reshape(n, 225), v.cpu().numpy(), pr.cpu().numpy().reshape(n, 225)
+    out = (lg.cpu().numpy().reshape(n, 225), v.cpu().numpy(), pr.cpu().numpy().reshape(n, 225))
+    if want_prior:
+        out += (d_prior.cpu().numpy().reshape(n, 225),)
+    return out
 
 
 class GNWeights:

@@ -58,8 +58,10 @@ class SelfPlayEngine:
             self.d_logits = torch.empty(self.leaf_cap * 225, dtype=torch.float32, device="cuda")
             self.d_value = torch.empty(self.leaf_cap, dtype=torch.float32, device="cuda")
             self.d_probs = torch.empty(self.leaf_cap * 225, dtype=torch.float32, device="cuda")
+            # MCTSNode.prior_prob of every node (ai_agent.py:522-523,564-582), dense float64
+            self.d_prior = torch.empty(self.leaf_cap * 225, dtype=torch.float64, device="cuda")
         else:
-            self.d_leaves = self.d_logits = self.d_value = self.d_probs = None
+            self.d_leaves = self.d_logits = self.d_value = self.d_probs = self.d_prior = None
         base = int(game_id_base)
         stride = self.n_slots if game_id_stride is None else int(game_id_stride)
         _lib.check(self.lib.gz_selfplay_init(ptr(self.d_slots), self.n_slots, S, base, stride, stream()),
@@ -104,7 +106,8 @@ class SelfPlayEngine:
         d_count = self.d_counters[4:8]  # counters.leaves
         _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
                                           ptr(d_count), ptr(self.d_logits), ptr(self.d_value),
-                                          ptr(self.d_probs), ptr(self.pv_weights.workspace_for(self.leaf_cap)),
+                                          ptr(self.d_probs), ptr(self.d_prior),
+                                          ptr(self.pv_weights.workspace_for(self.leaf_cap)),
                                           self.pv_weights.mode, stream()), "gz_pv_forward")
 
     def step(self, n_plies=None):

@@ -160,7 +160,11 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
  * csrc/gz_pvnet.h / gzero/weights.py).  Boards [n][16] uint32 bit planes.  If
  * d_count is not NULL it holds the number of valid boards on the device
  * (n = capacity).  Outputs: logits [n][225], value [n] (tanh), probs
- * [n][225] (softmax) or NULL.  precision: GZ_PV_FP32 (exact f32 MFMA) or
+ * [n][225] (softmax) or NULL; prior (optional, needs probs) = [n][225] float64
+ * MCTSNode._get_prior_probability (ai_agent.py:564-582): the softmax at the empty
+ * cells renormalised by their float64 sum (numpy's pairwise order), 0 at stones --
+ * the reference's compact vector is prior[i][empty cells, row-major].
+ * precision: GZ_PV_FP32 (exact f32 MFMA) or
  * GZ_PV_F16X3 (3-term fp16 split on the fp16 MFMA, ~22-bit operands, f32
  * accumulation).  d_workspace: gz_pv_workspace_bytes(n) bytes, required (fp32:
  * per-wave slabs; f16x3: the 1x1 head convs' outputs of every board, 2,816 B
@@ -170,8 +174,8 @@ int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulat
 size_t gz_pv_weight_floats(void);
 size_t gz_pv_workspace_bytes(int32_t n);
 int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
-                  float* d_logits, float* d_value, float* d_probs, void* d_workspace, int32_t precision,
-                  void* stream);
+                  float* d_logits, float* d_value, float* d_probs, double* d_prior, void* d_workspace,
+                  int32_t precision, void* stream);
 
 /* ---- K7: BG planner nets (bg_planner.py:22-78, BGPlannerAI.get_move :243-250) ----
  * d_weights: packed blob of gz_gn_weight_floats() floats (csrc/gz_gnet.h,

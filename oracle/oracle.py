@@ -245,3 +245,50 @@ def play_game(black, white, game_id, cap=256, want_cells=False, max_plies=0):
     if want_cells:
         out["cells"] = np.frombuffer(bytes(cells), dtype=np.int8)[: n * CELLS].reshape(n, CELLS).copy()
     return out
+
+
+# ---------------------------------------------------------------- prior (a20)
+def _np_pairwise_block(a):
+    """numpy's pairwise_sum for one block of <= 128 float64 terms (the order
+    np.sum(valid_probs) adds in): < 8 terms left to right from 0.0, else 8
+    interleaved accumulators, combined ((0+1)+(2+3))+((4+5)+(6+7)), then the
+    remainder left to right."""
+    n = len(a)
+    if n < 8:
+        res = 0.0
+        for x in a:
+            res += x
+        return res
+    r = list(a[:8])
+    i = 8
+    while i < n - (n % 8):
+        for j in range(8):
+            r[j] += a[i + j]
+        i += 8
+    res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    while i < n:
+        res += a[i]
+        i += 1
+    return res
+
+
+def np_pairwise_sum(a):
+    """np.sum of a contiguous float64 vector (numpy pairwise summation, block 128)."""
+    a = [float(x) for x in a]
+    if len(a) <= 128:
+        return _np_pairwise_block(a)
+    n2 = len(a) // 2
+    n2 -= n2 % 8
+    return np_pairwise_sum(a[:n2]) + np_pairwise_sum(a[n2:])
+
+
+def prior(probs, cells):
+    """MCTSNode._get_prior_probability (ai_agent.py:564-582): the float32 softmax
+    at the node's unexplored moves (= empty cells, row-major, gomoku_board.py:201-213)
+    as float64, divided by their float64 sum when it is > 0.  Returns the compact
+    vector (one entry per empty cell)."""
+    probs = np.asarray(probs, np.float32).reshape(-1)
+    cells = np.asarray(cells).reshape(-1)
+    v = [float(probs[i]) for i in range(CELLS) if cells[i] == 0]
+    s = np_pairwise_sum(v)
+    return np.array([x / s for x in v] if s > 0 else v, np.float64)

@@ -602,6 +602,33 @@ def part_pvnet():
                    "value_f32_b64": enc(np.asarray(value_all)), "probs_f32_b64": enc(np.stack(probs_all))})
 
 
+def part_prior():
+    """G4b: MCTSNode._get_prior_probability (ai_agent.py:564-582) -- the softmax
+    gathered at the node's unexplored (= legal, row-major) moves and renormalised
+    in float64 -- on the boards of the pvnet fixture, same weights."""
+    import base64
+    import numpy as np
+    import torch
+    from gzero import weights
+    h = ref()
+    with gzip.open(os.path.join(HERE, "pvnet.json.gz"), "rt") as f:
+        pv = json.load(f)
+    sd = weights.init_state_dict(seed=pv["weights_seed"])
+    path = os.path.join(os.getcwd(), "pv_prior.pth")
+    torch.save({"model_state_dict": sd, "model_type": "alphazero_gomoku", "board_size": 15, "device": "cpu"}, path)
+    model = h.nn.GomokuModel(model_path=path, board_size=15, device="cpu")
+    counts, priors = [], []
+    for case in pv["cases"]:
+        b = replay(h, case["moves"])
+        node = h.ai.MCTSNode(b, None, None, model, {})
+        pr = np.asarray(node.prior_prob, np.float64)
+        assert len(pr) == len(node.unexplored_moves)
+        counts.append(len(pr))
+        priors.append(pr)
+    dump("prior", {"weights_seed": pv["weights_seed"], "counts": counts,
+                   "prior_f64_b64": base64.b64encode(np.concatenate(priors).tobytes()).decode()})
+
+
 def part_augment():
     """G8: training.augment_sample -- label index and where the plane's stone lands."""
     import numpy as np
@@ -953,7 +980,7 @@ def part_sgd():
 
 
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
-         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "augment": part_augment,
+         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "augment": part_augment,
          "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
          "sgd": part_sgd}
 

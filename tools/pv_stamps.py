@@ -23,7 +23,7 @@ ap.add_argument("--lib", default="libgzpv_stamps.so")
 a = ap.parse_args()
 lib = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", a.lib))
 P = ctypes.c_void_p
-lib.gz_pv_forward.argtypes = [P, P, ctypes.c_int32, P, P, P, P, P, ctypes.c_int32, P]
+lib.gz_pv_forward.argtypes = [P, P, ctypes.c_int32, P, P, P, P, P, P, ctypes.c_int32, P]
 lib.gz_pv_stamps_read.argtypes = [P, ctypes.c_int]
 lib.gz_pv_workspace_bytes.restype = ctypes.c_size_t
 blob = torch.from_numpy(weights.pack_pv_weights(weights.init_state_dict(0))).cuda()
@@ -39,7 +39,7 @@ mode = weights.PRECISIONS[a.precision]
 out = np.zeros(32, np.uint64)
 for it in range(2):
     lib.gz_pv_stamps_read(out.ctypes.data, 1)
-    rc = lib.gz_pv_forward(blob.data_ptr(), d_b.data_ptr(), a.n, None, lg.data_ptr(), v.data_ptr(), pr.data_ptr(),
+    rc = lib.gz_pv_forward(blob.data_ptr(), d_b.data_ptr(), a.n, None, lg.data_ptr(), v.data_ptr(), pr.data_ptr(), None,
                            ws.data_ptr(), mode, None)
     assert rc == 0
     torch.cuda.synchronize()
