@@ -65,6 +65,22 @@ class AlphaZeroGomokuAI:
         self.games_played = 0
         self._last_decision_time = None
         self.last_search_stats = None
+        self._used = False       # has searched in the current game
+        self._last_count = -1    # move count of the last get_move board
+
+    # a new game moves the AI's streams this far in game-id space, so the ids a
+    # caller assigns to parallel games (0, 1, 2, ...) never meet a later game's
+    GAME_ID_STRIDE = 1 << 32
+
+    def new_game(self):
+        """Start a new game: the next get_move draws from fresh streams.  The
+        reference draws every game from the running global ``random``; here the
+        streams are keyed by game id, so a reused AI moves to the next id (the
+        first game keeps the constructor's ``game_id``)."""
+        if self._used:
+            self.game_id += self.GAME_ID_STRIDE
+        self._used = False
+        self._last_count = -1
 
     def _search_params(self, gather):
         return device.search_params(self.params.get("num_simulations", 200), self.params["c_puct"],
@@ -72,7 +88,14 @@ class AlphaZeroGomokuAI:
                                     gather)
 
     def get_move(self, board: GomokuBoard) -> Optional[Tuple[int, int]]:
-        """ai_agent.py:109-136 (opening book, MCTS, exploration) on the GPU."""
+        """ai_agent.py:109-136 (opening book, MCTS, exploration) on the GPU.
+        A board with fewer stones than the last one this AI saw (a reset or a
+        new board in a UI loop) starts a new game (``new_game``)."""
+        n = board.get_move_count()
+        if n < self._last_count:
+            self.new_game()
+        self._last_count = n
+        self._used = True
         return self.get_moves([board], [self.game_id])[0]
 
     def get_moves(self, boards: List[GomokuBoard], game_ids: List[int]) -> List[Optional[Tuple[int, int]]]:

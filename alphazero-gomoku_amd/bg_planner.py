@@ -21,8 +21,61 @@ from gzero.planner_nets import GraphNet, OpponentDQN, pack_planner_weights  # no
 
 
 class KnowledgeSearch:
+    """bg_planner.py:81-196.  ``score_move`` / ``top_k_moves`` score every cell of
+    the board in one wavefront on the GPU (``gz_knowledge_scores``); the stable
+    descending sort of ``top_k_moves`` is the reference's own (Python's sort)."""
+
     def __init__(self, board_size: int = 15):
         self.n = board_size
+
+    def scores(self, board, player: int) -> np.ndarray:
+        """score_move(board, (r, c), player) of all 225 cells, float64 (-1e9 at stones)."""
+        from gzero import device
+        if not board.game_over:
+            return device.knowledge_scores(board.to_state(), [player])[0]
+        # finished board: make_move fails on the copy, which keeps its winner
+        # (bg_planner.py:94-106) -- the same score for every empty cell but the bias
+        empty = board.board.reshape(-1) == 0
+        opp = 2 if player == 1 else 1
+        out = np.full(225, -1e9)
+        if board.winner == player:
+            out[empty] = 1e6
+        elif board.winner == opp and empty.any():
+            out[empty] = -1e5
+        else:
+            base = self._pattern_score(board, player)
+            for cell in np.flatnonzero(empty):
+                out[cell] = base + self._center_bias(divmod(int(cell), self.n))
+        return out
+
+    def score_move(self, board, move: Tuple[int, int], player: int) -> float:
+        r, c = int(move[0]), int(move[1])
+        if not board.is_valid_move(r, c):  # off-board or occupied (bg_planner.py:92-93)
+            return -1e9
+        return float(self.scores(board, player)[r * self.n + c])
+
+    def top_k_moves(self, board, player: int, k: int = 10) -> List[Tuple[int, int]]:
+        moves = board.get_valid_moves()
+        if not moves:
+            return []
+        sc = self.scores(board, player)
+        scored = [(float(sc[r * self.n + c]), (r, c)) for r, c in moves]
+        scored.sort(reverse=True, key=lambda x: x[0])
+        return [m for _, m in scored[:k]]
+
+    def _opponent_can_win_next(self, board, opponent: int) -> bool:
+        """bg_planner.py:116-125: some valid cell where ``opponent``, moving next,
+        ends the game as the winner (make_move fails on a finished board, whose
+        winner then stands)."""
+        if not board.get_valid_moves():
+            return False
+        if board.game_over:
+            return board.winner == opponent
+        from gzero import device
+        st = board.to_state()
+        st["player"] = opponent
+        new, ok, _ = device.board_step(np.repeat(st, 225), np.arange(225))
+        return bool(((new["over"] == 1) & (new["winner"] == opponent) & (ok == 1)).any())
 
     def _pattern_score(self, board, player: int) -> float:
         from gzero import device

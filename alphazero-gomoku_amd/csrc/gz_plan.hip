@@ -193,9 +193,11 @@ __device__ inline bool new_five_through(const uint8_t* grid, int g0, int who) {
     return false;
 }
 
-__device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, int mover, int n_moves, int P,
-                            const gz_planner_params& pp, const float* __restrict__ pv, const float* __restrict__ qv,
-                            uint64_t key, uint32_t* cnt) {
+// KnowledgeSearch.score_move(board, m, P) (bg_planner.py:90-106) of every cell,
+// lane-strided: sc[s] is cell lane + 64 s (-inf for occupied / off-board cells);
+// returns the number of empty cells.
+__device__ __forceinline__ int knowledge_scores(PlanShared* sh, const BB& black, const BB& white, int mover,
+                                                int n_moves, int P, double (&sc)[4]) {
     const int lane = lane_id();
     const int DR[4] = {1, 0, 1, 1}, DC[4] = {0, 1, 1, -1};  // bg_planner.py:147
     const BB E = empties(black, white);
@@ -233,13 +235,10 @@ __device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, in
     __syncthreads();
 
     // score of every legal cell (lane-strided, row-major)
-    double sc[4];
-    int cl[4];
 #pragma unroll
     for (int s = 0; s < 4; s++) {
         const int cell = lane + 64 * s;
         sc[s] = -__builtin_inf();
-        cl[s] = cell;
         if (cell >= GZ_CELLS) continue;
         const int r = cell / GZ_N, c = cell % GZ_N, bit = r * 16 + c;
         if (!bb_test(E, bit)) continue;
@@ -292,6 +291,18 @@ __device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, in
         }
         sc[s] = score;
     }
+    return ne;
+}
+
+__device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, int mover, int n_moves, int P,
+                            const gz_planner_params& pp, const float* __restrict__ pv, const float* __restrict__ qv,
+                            uint64_t key, uint32_t* cnt) {
+    const int lane = lane_id();
+    double sc[4];
+    int cl[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) cl[s] = lane + 64 * s;
+    const int ne = knowledge_scores(sh, black, white, mover, n_moves, P, sc);
     // top-k: Python's stable sort, descending (score desc, row-major asc)
     const int m = ne < pp.k ? ne : pp.k;
     for (int rnk = 0; rnk < m; rnk++) {
@@ -763,6 +774,26 @@ __global__ __launch_bounds__(WAVE) void planner_move_kernel(const gz_board_state
     }
 }
 
+// KnowledgeSearch.score_move for every cell of every board (bg_planner.py:90-106):
+// -1e9 where the move is invalid (occupied), as the reference returns
+__global__ __launch_bounds__(WAVE) void knowledge_scores_kernel(const gz_board_state* boards, const int32_t* player,
+                                                                int n, double* scores) {
+    __shared__ PlanShared sh;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const gz_board_state b = boards[i];
+    BB black, white;
+    load_bb(black, b.black);
+    load_bb(white, b.white);
+    double sc[4];
+    knowledge_scores(&sh, black, white, b.player, b.n_moves, player[i], sc);
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const int cell = lane_id() + 64 * s;
+        if (cell < GZ_CELLS) scores[(size_t)i * GZ_CELLS + cell] = sc[s] == -__builtin_inf() ? -1e9 : sc[s];
+    }
+}
+
 __global__ void boards_to_rows_kernel(const gz_board_state* boards, int n, uint32_t* rows) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -880,4 +911,13 @@ extern "C" int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_
 extern "C" size_t gz_planner_move_workspace_bytes(int32_t n) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
     return align256(m * 64) + align256(m * 225 * 4 * 2) + gz_gn_workspace_bytes((int32_t)m);
+}
+
+extern "C" int gz_knowledge_scores(const gz_board_state* d_boards, const int32_t* d_player, int32_t n,
+                                   double* d_scores, void* stream) {
+    if (n < 0 || (n > 0 && (!d_boards || !d_player || !d_scores)))
+        return plan_fail(GZ_ERR_ARG, "gz_knowledge_scores: bad arguments");
+    if (n == 0) return GZ_OK;
+    knowledge_scores_kernel<<<n, WAVE, 0, (hipStream_t)stream>>>(d_boards, d_player, n, d_scores);
+    return plan_check("knowledge_scores_kernel");
 }

@@ -302,3 +302,17 @@ def planner_move(states, ais, keys, pparams, gn_weights):
                "gz_planner_move")
     torch.cuda.synchronize()
     return d_moves.cpu().numpy(), d_draws.cpu().numpy().view(np.uint32)
+
+
+def knowledge_scores(states, players):
+    """KnowledgeSearch.score_move(board, (r, c), player) for every cell of every
+    state (gz_knowledge_scores): float64 [n, 225], -1e9 at occupied cells."""
+    lib = require_gpu()
+    states = np.ascontiguousarray(states, dtype=STATE_DTYPE)
+    n = len(states)
+    d_states = to_dev(states)
+    d_pl = torch.as_tensor(np.asarray(players, np.int32)).cuda()
+    d_sc = torch.empty(max(1, n) * 225, dtype=torch.float64, device="cuda")
+    _lib.check(lib.gz_knowledge_scores(ptr(d_states), ptr(d_pl), n, ptr(d_sc), stream()), "gz_knowledge_scores")
+    torch.cuda.synchronize()
+    return d_sc[: n * 225].cpu().numpy().reshape(n, 225)

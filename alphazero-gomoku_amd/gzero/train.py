@@ -77,8 +77,15 @@ class DeviceDataset(Dataset):
     def __len__(self):
         return self.n + 8 * self.m
 
-    def gather(self, d_ids, out=None):
-        """Samples d_ids (device int64) -> (x [B,3,15,15] f32, y [B] int64, v [B,1] f32) on the device."""
+    def check_ids(self, d_ids):
+        check_ids(self, d_ids)
+
+    def gather(self, d_ids, out=None, check=True):
+        """Samples d_ids (device int64) -> (x [B,3,15,15] f32, y [B] int64, v [B,1] f32) on the device.
+        ``check`` validates the ids first (one host sync; the trainer checks a whole
+        epoch's ids once and passes False)."""
+        if check:
+            self.check_ids(d_ids)
         b = int(d_ids.numel())
         if out is None:
             out = (torch.empty((b,) + SAMPLE_SHAPE, dtype=torch.float32, device="cuda"),
@@ -105,6 +112,21 @@ class DeviceDataset(Dataset):
     def __getitem__(self, i):
         x, y, v = self.gather(torch.tensor([int(i)], dtype=torch.int64, device="cuda"))
         return x[0], y[0], v[0]
+
+
+def check_ids(ds, d_ids):
+    """Raise (GzeroError) if any sample id is outside [0, len(ds)): gz_dataset_gather
+    would write label -1 and zero planes, and CrossEntropyLoss would turn that label
+    into a device-side assert.  One host sync."""
+    if d_ids.numel():
+        lo, hi = int(d_ids.min().item()), int(d_ids.max().item())
+        if lo < 0 or hi >= len(ds):
+            raise _lib.GzeroError(f"gz_dataset_gather: sample id out of range [{lo}, {hi}] for {len(ds)} samples")
+
+
+def _gather(ds, ids):
+    """A batch of an epoch whose ids were checked once (check_ids)."""
+    return ds.gather(ids, check=False) if isinstance(ds, DeviceDataset) else ds.gather(ids)
 
 
 class _IndexSet(Dataset):
@@ -195,12 +217,13 @@ class DeviceTrainer:
             if n else torch.zeros(0, dtype=torch.int64)
         order = order.to(self.device)
         ids_all = self._ids(indices, order)
+        check_ids(ds, ids_all)
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         batches = 0
         for mine, local, gcount in self._slices(ids_all, batch_size):
             self.optimizer.zero_grad(set_to_none=False)
             if local > 0:
-                x, y, v = ds.gather(mine)
+                x, y, v = _gather(ds, mine)
                 logits, val = self.net(x)
                 loss = self.ce(logits, y) + self.mse(val, v)
                 (loss * (local / gcount) if self.world > 1 else loss).backward()
@@ -224,19 +247,28 @@ class DeviceTrainer:
 
     @torch.no_grad()
     def validate_epoch(self, ds, batch_size=128, indices=None):
+        """Mean per-batch validation loss (training.py:313-337).  Data parallel:
+        batch k is evaluated by rank k mod N and the per-batch losses are
+        SUM-all-reduced, so every rank returns the same global value (and each
+        batch is evaluated once, not N times)."""
         self.net.eval()
         n = len(ds) if indices is None else int(indices.numel())
         # iterate an (unshuffled) DataLoader as the reference does: it draws one torch seed
         order = loader_order(n, batch_size, shuffle=False)
         order = (torch.cat(order) if order else torch.zeros(0, dtype=torch.int64)).to(self.device)
         ids_all = self._ids(indices, order)
+        check_ids(ds, ids_all)
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         batches = 0
-        for k in range(0, n, batch_size):
-            x, y, v = ds.gather(ids_all[k:k + batch_size])
+        for bi, k in enumerate(range(0, n, batch_size)):
+            batches += 1
+            if bi % self.world != self.rank:
+                continue
+            x, y, v = _gather(ds, ids_all[k:k + batch_size])
             logits, val = self.net(x)
             total += (self.ce(logits, y) + self.mse(val, v)).double()
-            batches += 1
+        if self.world > 1:
+            dist.all_reduce(total, group=self.group)
         return float(total.item()) / max(1, batches)
 
     def step_scheduler(self):

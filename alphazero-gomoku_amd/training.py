@@ -109,9 +109,26 @@ class GomokuSelfPlayDataset(Dataset):
 # ---------------------------------------------------------------- self-play
 
 
+def _is_device_failure(e: BaseException) -> bool:
+    """Errors that must not be papered over with a random move: the engine is
+    missing or a HIP call failed (a dead GPU would otherwise silently turn
+    self-play into random-move training data)."""
+    from gzero._lib import GzeroError, GzeroUnavailable
+    if isinstance(e, (GzeroUnavailable, GzeroError)):
+        return True
+    return isinstance(e, RuntimeError) and any(s in str(e) for s in ("HIP", "hip", "CUDA", "cuda", "device-side"))
+
+
 def play_one_game(ai_black, ai_white, step_timeout: float = 10.0,
                   game_timeout: float = 300.0) -> Tuple[SimpleReplay, int]:
-    """One game between two AIs (training.py:141-218); timeouts fall back to a random move."""
+    """One game between two AIs (training.py:141-218); timeouts and AI-logic
+    exceptions fall back to a random move as in the reference, device failures
+    (GzeroUnavailable, GzeroError, HIP runtime errors) propagate.  Each call is
+    a new game for both AIs: their random streams move to a fresh game id
+    (AlphaZeroGomokuAI.new_game), as the reference's global ``random`` would."""
+    for ai in (ai_black, ai_white):
+        if hasattr(ai, "new_game"):
+            ai.new_game()
     board = GomokuBoard()
     buf = SimpleReplay()
     t_game = time.time()
@@ -128,7 +145,9 @@ def play_one_game(ai_black, ai_white, step_timeout: float = 10.0,
                 if not valid:
                     break
                 move = random.choice(valid)
-        except Exception:  # training.py:191-198
+        except Exception as e:  # training.py:191-198
+            if _is_device_failure(e):
+                raise
             valid = board.get_valid_moves()
             if not valid:
                 break
@@ -205,7 +224,8 @@ class RandomAgent:
 
 def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficulty: str = "easy",
                    eval_num_sim: int = 60, eval_plans: int = 2, seed: Optional[int] = None,
-                   return_games: bool = False, alternate: bool = True):
+                   return_games: bool = False, alternate: bool = True, seeds: Optional[Tuple[int, int]] = None,
+                   game_id_base: int = 0):
     """training.py:221-270 with all ``games`` played at once: every ply, the games
     whose side to move belongs to the same agent are searched in ONE batched GPU
     call (AlphaZeroGomokuAI.get_moves).  As in the reference the evaluated model
@@ -216,10 +236,16 @@ def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficul
     the streams of (seed_a / seed_b, g): the result equals playing the games one
     by one with per-game AIs of those seeds and ``game_id = g``.  ``alternate=False``
     keeps the evaluated model on black in every game -- what training.main's six
-    ``evaluate_model(..., games=1)`` calls amount to (training.py:484-492)."""
+    ``evaluate_model(..., games=1)`` calls amount to (training.py:484-492).
+    ``seeds`` = (seed_a, seed_b) overrides the pair derived from ``seed``; game g
+    uses game id ``game_id_base + g`` (tests/golden arena fixture: one seed for
+    both sides, as the reference's single global stream)."""
     from ai_agent import AlphaZeroGomokuAI
     seed = random.getrandbits(64) if seed is None else int(seed)
     seed_a, seed_b = seed, (seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
+    if seeds is not None:
+        seed_a, seed_b = int(seeds[0]), int(seeds[1])
+    gid = [int(game_id_base) + g for g in range(games)]
     # one AI object per (agent, colour): the colour is the AI's player in the search
     ai_a, ai_b = {}, {}
     for color in (GomokuBoard.BLACK, GomokuBoard.WHITE):
@@ -247,9 +273,9 @@ def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficul
         for (who, cp), gs in groups.items():
             agent = (ai_a if who == "a" else ai_b)[cp]
             if isinstance(agent, RandomAgent):
-                mv = [RandomAgent(agent.seed, g).get_move(boards[g]) for g in gs]
+                mv = [RandomAgent(agent.seed, gid[g]).get_move(boards[g]) for g in gs]
             else:
-                mv = agent.get_moves([boards[g] for g in gs], gs)
+                mv = agent.get_moves([boards[g] for g in gs], [gid[g] for g in gs])
             for g, m in zip(gs, mv):
                 if m is None:
                     stopped.add(g)
@@ -380,6 +406,31 @@ def _replay_records(rep: "SimpleReplay"):
     return rec
 
 
+def _rng_isolated(fn, *a, **k):
+    """Run fn (rank 0's arena) without moving the global random / numpy / torch
+    RNGs: the arena builds AIs, planners and models that draw from them, and every
+    rank must keep drawing the same dataset subset, split and loader order."""
+    py, npst = random.getstate(), np.random.get_state()
+    devices = [torch.cuda.current_device()] if torch.cuda.is_available() else []
+    with torch.random.fork_rng(devices=devices):
+        try:
+            return fn(*a, **k)
+        finally:
+            random.setstate(py)
+            np.random.set_state(npst)
+
+
+def _broadcast_int(x: int) -> int:
+    """Rank 0's value of x on every rank (identity for one process)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return int(x)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    dist.broadcast(t, 0)
+    return int(t.item())
+
+
 def main(iterations: int = 6, games_per_iteration: int = 10, seed: Optional[int] = None, models_dir: str = "models",
          num_simulations: int = 200, planner_steps: int = 5, eval_games: int = 6):
     """training.main (training.py:361-537) on the MI355X engine: same loop, the
@@ -395,6 +446,7 @@ def main(iterations: int = 6, games_per_iteration: int = 10, seed: Optional[int]
     rank, ws = gdist.init_from_env()
     seed = int(seed if seed is not None else 20240101)
     random.seed(seed)  # every rank draws the same dataset / split / shuffles
+    np.random.seed(seed % (1 << 32))
     torch.manual_seed(seed)
     if rank == 0:
         os.makedirs(models_dir, exist_ok=True)
@@ -413,7 +465,10 @@ def main(iterations: int = 6, games_per_iteration: int = 10, seed: Optional[int]
             continue
         if rank == 0:
             model.save_model(os.path.join(models_dir, f"alphazero_gomoku_iter_{it}.pth"))
-        improved = res["val_loss"] < best_val
+        # rank 0's decision on every rank (val_loss is already the same global value
+        # everywhere -- DeviceTrainer.validate_epoch all-reduces it -- so this only
+        # guards the early stop and the torch-RNG use of the snapshot against drift)
+        improved = bool(_broadcast_int(int(res["val_loss"] < best_val)))
         if improved:
             best_val, patience_count = res["val_loss"], 0
             best_path = os.path.join(models_dir, "alphazero_gomoku_best.pth")
@@ -424,8 +479,8 @@ def main(iterations: int = 6, games_per_iteration: int = 10, seed: Optional[int]
             best_snapshot.eval_mode()
         else:
             patience_count += 1
-        stats = evaluate_model(model, best_snapshot, games=eval_games, seed=seed + it, alternate=False) \
-            if rank == 0 else {}
+        stats = _rng_isolated(evaluate_model, model, best_snapshot, games=eval_games, seed=seed + it,
+                              alternate=False) if rank == 0 else {}
         res.update(eval=stats, elapsed=time.time() - t0)
         history.append(res)
         if rank == 0:

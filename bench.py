@@ -174,7 +174,9 @@ def main():
         if ws > 1:
             dist.barrier()
 
-    gathered = [0]
+    # N > 1: the per-step RCCL all-gather of finished games' (s, pi, z) records,
+    # fixed-size and sync-free (gzero.dist.RecordExchange: counts stay on the device)
+    ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda") if ws > 1 else None
 
     def step():
         eng.launch_search()
@@ -183,10 +185,9 @@ def main():
         eng.launch_pv()
         ev[1].record()
         ctr = eng.d_counters.clone()  # per-step counters, stays on the device
-        if ws > 1:  # RCCL all-gather of the (s, pi, z) records finished in this step
-            rec, n = eng.records_device()
-            out = gdist.all_gather_records(rec, n)
-            gathered[0] += out.numel()
+        if ex is not None:
+            ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
+            ex.exchange()
         return ev, ctr
 
     burn_in = args.burn_in if args.burn_in is not None else (0 if args.planner_steps else 96)
@@ -286,6 +287,11 @@ def main():
                            "note": "plies decided by a search (SURVEY 8d): value counts every ply, incl. the opening "
                                    "plies 0-5 that _opening_move plays without one (ai_agent.py:138-166)"},
         }
+
+    if ex is not None and rank == 0:
+        out["record_exchange"] = {"chunk_records": ex.chunk, "bytes_per_rank_per_step": ex.chunk * ex.item,
+                                  "pending_after": int(ex.pending().item()), "overflow": int(ex.overflow.item()),
+                                  "note": "fixed-size RCCL all_gather_into_tensor per step, counts on the device"}
 
     # ---- prior-elided run (same kernel, no PV gather / forward)
     if not args.no_elided and not args.planner_steps:

@@ -206,6 +206,15 @@ int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, in
  * planner's colour P, d_keys = RNG stream; d_moves (-1 = None), d_draws.
  * d_workspace: gz_planner_move_workspace_bytes(n) bytes. */
 size_t gz_planner_move_workspace_bytes(int32_t n);
+
+/* KnowledgeSearch.score_move(board, (r, c), player) (bg_planner.py:90-106) for
+ * every cell of every board, the side to move playing the stone: d_scores
+ * [n][225] float64 -- 1e6 (the move wins for player), -1e5 (player's opponent can
+ * then complete five, _opponent_can_win_next :116-125), else _pattern_score +
+ * _center_bias (:127-196); -1e9 at occupied cells (is_valid_move fails).
+ * top_k_moves (:108-114) = the first k cells of a stable descending sort. */
+int gz_knowledge_scores(const gz_board_state* d_boards, const int32_t* d_player, int32_t n, double* d_scores,
+                        void* stream);
 int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_ai, const uint64_t* d_keys, int32_t n,
                     const gz_planner_params* pp, const float* d_gn_weights, void* d_workspace,
                     int32_t* d_moves, uint32_t* d_draws, void* stream);

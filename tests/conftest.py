@@ -41,3 +41,36 @@ def oracle():
     import oracle as O
     O.build()
     return O
+
+
+def hexf32(hs):
+    import numpy as np
+    return np.array([int(h, 16) for h in hs], dtype=np.uint32).view(np.float32)
+
+
+def planner_net_flips(calls, gnw, alpha):
+    """Planner decisions the nets' rounding can flip.  For every recorded reference
+    BGPlannerAI call (board, top-k, the reference's p / q at the top-k cells) the
+    compose argmax alpha*p - (1-alpha)*q (first maximum in top-k order,
+    bg_planner.py:250-265) is taken with the reference's values and with the GPU
+    nets' values on the same board; returns the reference's composed-score gap
+    between the two choices for every call where they differ.  A GPU search or
+    move that differs from the reference's is explained only if this list is
+    non-empty and every gap is a near-tie (<= 1e-6)."""
+    import numpy as np
+    from gzero import boards, device
+    if not calls:
+        return []
+    cells = np.array([[int(ch) for ch in c["board"]] for c in calls], np.int8)
+    bl, wh = boards.cells_to_words(cells)
+    p, q, _ = device.gn_forward(gnw, boards.leaf_words(bl, wh))
+    gaps = []
+    for i, c in enumerate(calls):
+        top = c["top"]
+        pr, qr = hexf32(c["p"]), hexf32(c["q"])
+        ref = [alpha * float(pr[j]) - (1 - alpha) * float(qr[j]) for j in range(len(top))]
+        gpu = [alpha * float(p[i][t]) - (1 - alpha) * float(q[i][t]) for t in top]
+        ra, ga = int(np.argmax(ref)), int(np.argmax(gpu))
+        if ra != ga:
+            gaps.append(abs(ref[ra] - ref[ga]))
+    return gaps

@@ -979,10 +979,80 @@ def part_sgd():
                  "param_stats": stats, "param_sample_f32_b64": sample, "lr_after": sched.get_last_lr()})
 
 
+# ---------------------------------------------------------------------------
+# G10 arena: training.evaluate_model (training.py:221-270) -- who moves with which
+# simulation count, RandomAgent, colour alternation, the None-move stop and the
+# win / loss / draw count.  eval_plans = 0 so no net output can steer a move (the
+# priors are never read, ai_agent.py:523); the easy table's 100 simulations are
+# lowered to ARENA_EASY_SIMS on every AI the arena builds (a wrapper on __init__,
+# mirrored by the test), so the reference finishes in minutes; the same wrapper
+# lifts the 5 s time limit (ai_agent.py:183-189), which would otherwise cut
+# searches short depending on the host's speed.
+# Stream selection: game g of a task = the g-th GomokuBoard evaluate_model builds
+# (game_id = base + g); RandomAgent's random.choice(valid) is keyed by
+# (game_id, ply = 225 - len(valid), sim 0), the stream training.RandomAgent uses.
+# ---------------------------------------------------------------------------
+
+ARENA_EASY_SIMS = 4
+
+
+def _arena_task(args):
+    base, games, with_baseline, eval_num_sim = args
+    import contextlib
+    import io
+    h = ref()
+    A = h.ai.AlphaZeroGomokuAI
+    if not getattr(h, "arena_installed", False):
+        orig_init = A.__init__
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            self.time_limit = float("inf")  # evaluate_model builds its AIs with the 5 s default
+            if self.difficulty == "easy":
+                self.params["num_simulations"] = ARENA_EASY_SIMS
+
+        A.__init__ = init
+
+        class ArenaBoard(h.gb.GomokuBoard):
+            def __init__(self, *a, **k):
+                super().__init__(*a, **k)
+                h.rs.set(game_id=h.arena_gid, ply=0, sim=0)
+                h.arena_gid += 1
+                h.arena_boards.append(self)
+
+        class TrainingRandom:  # training.random: only RandomAgent draws from it here
+            def choice(self, seq):
+                h.rs.set(ply=225 - len(seq), sim=0)
+                return h.rs.choice(seq)
+
+        h.tr.GomokuBoard = ArenaBoard
+        h.tr.random = TrainingRandom()
+        h.arena_installed = True
+    h.arena_gid, h.arena_boards = base, []
+    cur = h.nn.GomokuModel(model_path=None, board_size=15, device="cpu")
+    bl = h.nn.GomokuModel(model_path=None, board_size=15, device="cpu") if with_baseline else None
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = h.tr.evaluate_model(cur, bl, "cpu", games=games, eval_difficulty="easy", eval_num_sim=eval_num_sim,
+                                  eval_plans=0)
+    return {"game_id_base": base, "games": games, "baseline": with_baseline, "eval_num_sim": eval_num_sim,
+            "easy_sims": ARENA_EASY_SIMS, "result": res, "seconds": time.time() - t0,
+            "boards": [{"moves": [r * N + c for r, c, _ in b.move_history], "winner": b.winner}
+                       for b in h.arena_boards]}
+
+
+def part_arena():
+    tasks = [(9000 + 10 * i, 2, False, [3, 6][i % 2]) for i in range(4)]
+    tasks += [(9100 + 10 * i, 2, True, 3) for i in range(4)]
+    with Pool(8) as pool:
+        out = pool.map(_arena_task, tasks, chunksize=1)
+    dump("arena", {"seed": SEED, "cases": out})
+
+
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
          "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "augment": part_augment,
          "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
-         "sgd": part_sgd}
+         "sgd": part_sgd, "arena": part_arena}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(PARTS)

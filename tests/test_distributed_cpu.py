@@ -9,7 +9,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from gzero import boards
-from gzero.dist import all_gather_records, shard_ids, to_records
+from gzero.dist import RecordExchange, all_gather_records, chunks_to_records, shard_ids, to_records
 
 
 def _free_port():
@@ -66,3 +66,110 @@ def test_shards_disjoint():
                 gid = base + s + g * stride
                 assert gid not in ids
                 ids.add(gid)
+
+
+CAP, CHUNK = 12, 5
+# records finished per step by each rank: bursts above the chunk, empty steps
+BURSTS = {0: [3, 12, 0, 7, 0, 0, 0, 0], 1: [0, 5, 11, 1, 0, 0, 0, 0]}
+
+
+def _exchange_worker(rank, ws, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    ex = RecordExchange(CAP, CHUNK, "cpu")
+    serial = 0
+    got = []
+    for n in BURSTS[rank]:
+        rec = np.zeros(CAP, boards.RECORD_DTYPE)
+        rec["game_id"] = rank * 1000 + serial + np.arange(CAP)  # rows past n are junk the exchange must skip
+        rec["move"] = -7
+        rec["move"][:n] = rank
+        serial += n
+        ex.push(torch.from_numpy(rec.view(np.uint8).copy()), torch.tensor([n], dtype=torch.int32))
+        recv, counts = ex.exchange()
+        assert recv.shape == (ws, CHUNK, 80) and counts.shape == (ws,)
+        got.append(chunks_to_records(recv, counts))
+    q.put((rank, np.concatenate(got).tobytes(), int(ex.pending().item()), int(ex.overflow.item())))
+    dist.destroy_process_group()
+
+
+def test_record_exchange_world2():
+    """Fixed-size per-step exchange: every record arrives exactly once, in order,
+    bursts above the chunk carry over to later steps, padding rows never leak."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    outs = {r: np.frombuffer(b, boards.RECORD_DTYPE) for r, b, _, _ in res}
+    assert outs[0].tobytes() == outs[1].tobytes()
+    g = outs[0]
+    assert (g["move"] >= 0).all()
+    for r in range(2):
+        ids = g["game_id"][g["move"] == r]
+        assert list(ids) == [r * 1000 + i for i in range(sum(BURSTS[r]))]
+    assert all(pend == 0 and ovf == 0 for _, _, pend, ovf in res)
+
+
+def test_record_exchange_overflow_counts():
+    ex = RecordExchange(4, 2, "cpu", capacity=6)
+    rec = torch.zeros(4 * 80, dtype=torch.uint8)
+    for _ in range(3):
+        ex.push(rec, torch.tensor([4]))
+    assert int(ex.pending().item()) == 6 and int(ex.overflow.item()) == 6
+    ex.exchange()
+    assert int(ex.pending().item()) == 4
+
+
+# training.main under world size 2: rank 0 alone runs the arena (which draws from
+# the global RNGs) and the ranks' own val_loss values could drift; every rank must
+# still draw the same random / torch / numpy numbers and stop at the same iteration.
+VAL = {0: [1.0, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0], 1: [1.0, 0.5, 0.4, 0.3, 0.2, 0.1, 0.05]}
+
+
+def _main_worker(rank, ws, port, q, tmp):
+    import random
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    os.chdir(tmp)
+    import neural_network
+    import training
+    from gzero import train as gtrain
+    draws = []
+
+    def fake_iteration(model, trainer, it, *a, **k):
+        draws.append((random.random(), float(torch.rand(1)), float(np.random.rand())))
+        return {"iteration": it, "records": 10, "val_loss": VAL[rank][it - 1]}
+
+    def fake_arena(*a, **k):  # the real arena builds AIs / planners / models: all draw
+        random.random(), random.getrandbits(64), torch.rand(7), np.random.rand(3)
+        return {"win_rate": 0.5}
+
+    real_model = neural_network.GomokuModel
+    neural_network.GomokuModel = lambda *a, **k: real_model(*a, **dict(k, device="cpu"))
+    gtrain.DeviceTrainer = lambda model: None
+    training.run_iteration = fake_iteration
+    training.evaluate_model = fake_arena
+    hist = training.main(iterations=7, games_per_iteration=1, seed=5, models_dir=os.path.join(tmp, f"m{rank}"))
+    q.put((rank, len(hist), draws))
+    dist.destroy_process_group()
+
+
+def test_training_main_ranks_stay_in_step(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_main_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (n, d) for r, n, d in (q.get(timeout=180) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    # rank 0's losses: improve at iterations 1-2, then 3 without improvement -> stop after 5
+    assert res[0][0] == res[1][0] == 5
+    assert res[0][1] == res[1][1], (res[0][1], res[1][1])

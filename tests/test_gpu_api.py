@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import SEED, golden
+from conftest import SEED, golden, hexf32, planner_net_flips
 
 pytestmark = pytest.mark.gpu
 
@@ -101,22 +101,26 @@ def _load_planner(ai_or_planner, g):
 def test_bg_planner_ai_golden():
     """BGPlannerAI.get_move on the GPU against the reference (near-ties of the nets allowed)."""
     from bg_planner import BGPlannerAI
+    from gzero import _lib
     g = golden("planner")
-    same = 0
     for c in g["cases"][:90]:
         b = _board(c["moves"])
         pl = BGPlannerAI(c["P"], c["difficulty"], seed=SEED, game_id=c["game_id"])
         _load_planner(pl, g)
         mv = pl.get_move(b)
-        same += (mv[0] * 15 + mv[1]) == c["move"]
-    assert same >= 88
+        m = mv[0] * 15 + mv[1]
+        if m != c["move"]:  # only a near-tie of the reference's composed scores may flip
+            a = _lib.PLANNER[c["difficulty"]][1]
+            comp = {cell: a * float(pp) - (1 - a) * float(qq)
+                    for cell, pp, qq in zip(c["top"], hexf32(c["p"]), hexf32(c["q"]))}
+            assert m in comp and abs(comp[m] - comp[c["move"]]) <= 1e-6, c["game_id"]
 
 
 def test_ai_with_planner_golden():
     """AlphaZeroGomokuAI(planner_steps > 0) = the reference's default AI."""
     from ai_agent import AlphaZeroGomokuAI
+    from gzero import _lib
     g = golden("planner_mcts")
-    same = 0
     for c in g["cases"]:
         b = _board(c["moves"])
         ai = AlphaZeroGomokuAI(b.current_player, c["difficulty"], beta=c["beta"], planner_steps=c["planner_steps"],
@@ -124,9 +128,11 @@ def test_ai_with_planner_golden():
         _load_planner(ai, g)
         ai.params["num_simulations"] = c["sims"]
         mv = ai.get_move(b)
-        same += (mv[0] * 15 + mv[1]) == c["move"]
-        assert ai.last_search_stats["predicts"] == c["predicts"]
-    assert same >= 18
+        if (mv[0] * 15 + mv[1]) != c["move"]:  # explained by a near-tie planner decision inside the search
+            gaps = planner_net_flips(c["calls"], ai.bg_planner.device_weights(), _lib.PLANNER[c["difficulty"]][1])
+            assert gaps and max(gaps) <= 1e-6, (c["game_id"], gaps)
+        else:
+            assert ai.last_search_stats["predicts"] == c["predicts"]
 
 
 def test_module_smoke_checks(tmp_path, monkeypatch, capsys):
@@ -142,3 +148,72 @@ def test_module_smoke_checks(tmp_path, monkeypatch, capsys):
     out = capsys.readouterr().out
     assert "reloaded: True" in out
     assert "AlphaZero AI smoke check passed" in out
+
+
+def test_knowledge_search_golden():
+    """KnowledgeSearch.score_move / top_k_moves of the drop-in (one GPU wavefront
+    per board) against the reference's scores of every legal move and its top-k
+    (bg_planner.py:90-114): exact."""
+    from bg_planner import KnowledgeSearch
+    g = golden("planner")
+    ks = KnowledgeSearch()
+    k_of = {"easy": 8, "medium": 12, "hard": 16}
+    n_full = 0
+    for c in g["cases"]:
+        b = _board(c["moves"])
+        top = ks.top_k_moves(b, c["P"], k=k_of[c["difficulty"]])
+        assert [r * 15 + cc for r, cc in top] == c["top"], c["game_id"]
+        if "scores" in c:
+            sc = ks.scores(b, c["P"])
+            legal = [r * 15 + cc for r, cc in b.get_valid_moves()]
+            assert [float(sc[m]) for m in legal] == c["scores"], c["game_id"]
+            n_full += 1
+            if legal:  # the per-move API and an invalid move
+                assert ks.score_move(b, divmod(legal[-1], 15), c["P"]) == c["scores"][-1]
+            if c["moves"]:
+                assert ks.score_move(b, divmod(c["moves"][0], 15), c["P"]) == -1e9
+    assert n_full >= 150
+
+
+def test_reused_ai_plays_new_games():
+    """A reused AI pair (the reference's training loop calls play_one_game with the
+    same two AIs) draws fresh streams for each game; the first game keeps the
+    constructor's game id."""
+    from ai_agent import AlphaZeroGomokuAI
+    from training import play_one_game
+    ab = AlphaZeroGomokuAI(1, "easy", beta=0.0, planner_steps=0, seed=SEED, game_id=3)
+    aw = AlphaZeroGomokuAI(2, "easy", beta=0.0, planner_steps=0, seed=SEED, game_id=3)
+    ab.params["num_simulations"] = aw.params["num_simulations"] = 2
+    aw.model = ab.model
+    g1 = play_one_game(ab, aw, step_timeout=1e9, game_timeout=1e9)[0].move_indices
+    g2 = play_one_game(ab, aw, step_timeout=1e9, game_timeout=1e9)[0].move_indices
+    assert g1 != g2
+    assert ab.game_id == 3 + AlphaZeroGomokuAI.GAME_ID_STRIDE
+    ab2 = AlphaZeroGomokuAI(1, "easy", beta=0.0, planner_steps=0, seed=SEED, game_id=3)
+    aw2 = AlphaZeroGomokuAI(2, "easy", beta=0.0, planner_steps=0, seed=SEED, game_id=3)
+    ab2.params["num_simulations"] = aw2.params["num_simulations"] = 2
+    assert play_one_game(ab2, aw2, step_timeout=1e9, game_timeout=1e9)[0].move_indices == g1
+
+
+def test_play_one_game_propagates_device_errors(monkeypatch):
+    """AI-logic exceptions fall back to a random move (training.py:191-198); a
+    failing engine call must not (it would turn self-play into random data)."""
+    from ai_agent import AlphaZeroGomokuAI
+    from gzero import _lib
+    from training import play_one_game
+    ab = AlphaZeroGomokuAI(1, "easy", planner_steps=0, seed=SEED)
+    aw = AlphaZeroGomokuAI(2, "easy", planner_steps=0, seed=SEED)
+
+    def dead(*a, **k):
+        raise _lib.GzeroError("gz_search failed (2): hipErrorLaunchFailure")
+
+    monkeypatch.setattr(ab, "get_moves", dead)
+    with pytest.raises(_lib.GzeroError):
+        play_one_game(ab, aw, step_timeout=1e9, game_timeout=1e9)
+
+    def buggy(*a, **k):
+        raise ValueError("AI logic error")
+
+    monkeypatch.setattr(ab, "get_moves", buggy)
+    buf, n = play_one_game(ab, aw, step_timeout=1e9, game_timeout=1e9)
+    assert n > 0 and len(buf) == n

@@ -64,3 +64,35 @@ def test_arena_vs_baseline_equals_games_alone():
         mv, w = _play_alone(cur, base, g, res["seeds"], 100, 10)
         assert rec["moves"] == mv and rec["winner"] == w, g
         assert len(mv) >= 9, g
+
+
+def test_arena_vs_reference_fixture(monkeypatch):
+    """evaluate_model against the reference's own evaluate_model (tests/golden
+    arena.json.gz, make_golden.py part_arena): eval_plans 0 (no net output steers a
+    move), the easy table's simulations lowered to the fixture's count on every AI
+    the arena builds (as the generator does), one seed for both sides (the
+    reference's single global stream) and game ids base + g.  Every game's moves and
+    winner and the win / loss / draw counts equal the reference's."""
+    import ai_agent
+    from conftest import golden
+    from neural_network import GomokuModel
+    from training import evaluate_model
+    g = golden("arena")
+    orig = ai_agent.AlphaZeroGomokuAI.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        if self.difficulty == "easy":
+            self.params["num_simulations"] = g["cases"][0]["easy_sims"]
+
+    monkeypatch.setattr(ai_agent.AlphaZeroGomokuAI, "__init__", init)
+    cur, base = GomokuModel(device="cpu"), GomokuModel(device="cpu")
+    for c in g["cases"]:
+        res = evaluate_model(cur, base if c["baseline"] else None, games=c["games"], eval_difficulty="easy",
+                             eval_num_sim=c["eval_num_sim"], eval_plans=0, seeds=(g["seed"], g["seed"]),
+                             game_id_base=c["game_id_base"], return_games=True)
+        for k in ("wins", "losses", "draws", "win_rate"):
+            assert res[k] == c["result"][k], (c["game_id_base"], k)
+        for got, ref in zip(res["games"], c["boards"]):
+            assert got["moves"] == ref["moves"], c["game_id_base"]
+            assert got["winner"] == ref["winner"]

@@ -11,7 +11,7 @@ are a near-tie (|gap| <= 1e-6) that the nets' rounding can flip.
 import numpy as np
 import pytest
 
-from conftest import SEED, golden
+from conftest import SEED, golden, planner_net_flips
 from gzero import _lib, boards, planner_nets
 
 pytestmark = pytest.mark.gpu
@@ -125,8 +125,9 @@ def test_plan_search_exact_vs_oracle(oracle, gnw, idx):
 
 
 def test_plan_search_vs_reference(oracle, gnw):
-    """All 20 reference searches in one batched call: same move / root statistics
-    unless a planner decision inside was a near-tie of the reference's nets."""
+    """All 20 reference searches: same move / root statistics, or -- for each
+    search that differs -- a recorded planner decision inside it that the nets'
+    rounding flips, at a near-tie (<= 1e-6) of the reference's composed scores."""
     from gzero import device
     g = golden("planner_mcts")
     same = 0
@@ -144,7 +145,10 @@ def test_plan_search_vs_reference(oracle, gnw):
             got = [[int(t["move"][i]), int(t["visits"][i]), float(t["value"][i])] for i in kids]
             ok = got == c["children"]
         same += ok
-    assert same >= 18, same
+        if not ok:
+            gaps = planner_net_flips(c["calls"], gnw, _lib.PLANNER[c["difficulty"]][1])
+            assert gaps and max(gaps) <= 1e-6, (c["game_id"], gaps)
+    assert same >= 15, same
 
 
 def test_selfplay_planner_games_vs_oracle(oracle, gnw):

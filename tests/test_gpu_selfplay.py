@@ -3,6 +3,7 @@ finished games' (s, pi, z) records against the reference's golden games and
 the oracle, plus the PV leaf count against the reference's predict() calls."""
 import numpy as np
 import pytest
+import torch
 
 from conftest import SEED, golden
 from gzero import boards
@@ -98,3 +99,131 @@ def test_sharded_ranks_play_the_single_gpu_games():
     for gid in common:
         assert shard[gid]["moves"] == ref[gid]["moves"], gid
         assert shard[gid]["z"] == ref[gid]["z"], gid
+
+
+def _pv_weights():
+    from gzero import weights
+    from gzero.device import PVWeights
+    sd = weights.init_state_dict(0)
+    return sd, PVWeights(weights.pack_pv_weights(sd), precision="f16x3")
+
+
+def _leaf_rows(eng, n):
+    return eng.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
+
+
+def test_config2_200_sims_vs_oracle(oracle):
+    """BASELINE config 2 per slot (200 sims, medium, beta 0, planner_steps 0, the
+    PV forward on every node the searches create): 16 slots x 12 plies equal the
+    oracle's games, the forwards per step equal its predict() count, and the PV
+    outputs of the last step's nodes match torch fp32 (1e-4) and the oracle's
+    masked prior (exact)."""
+    from gzero import weights
+    sd, w = _pv_weights()
+    n_slots, K, base = 16, 12, 700
+    eng = SelfPlayEngine(n_slots=n_slots, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.0, seed=SEED,
+                         pv_weights=w, plies_per_step=1, game_id_base=base)
+    leaves = 0
+    for _ in range(K):
+        eng.step()
+        c = eng.counters()
+        assert c["leaves_dropped"] == 0 and c["records_dropped"] == 0 and c["moves"] == n_slots
+        assert c["games"] == 0  # no game ends in 12 plies: the slots keep their ids
+        leaves += int(c["leaves"])
+    st, gids = eng.boards()
+    p = oracle.make_params("medium", sims=200, beta=0.0, seed=SEED)
+    pred = 0
+    for s in range(n_slots):
+        assert int(gids[s]) == base + s
+        ref = oracle.play_game(p, p, base + s, max_plies=K)
+        assert ref["n"] == K
+        cells = boards.words_to_cells(st["black"][s], st["white"][s])
+        assert (cells == oracle.new_board(ref["moves"]).cells()).all(), s
+        pred += ref["predicts"]
+    assert leaves == pred
+    # the last step's forwards: logits / value vs torch fp32, prior vs the oracle
+    n = int(eng.counters()["leaves"])
+    rows = _leaf_rows(eng, n)
+    sel = np.random.default_rng(1).choice(n, size=min(n, 384), replace=False)
+    cells = boards.words_to_cells(rows[sel, :8], rows[sel, 8:])
+    ref_lg, ref_v = weights.reference_forward(sd, boards.planes_from_cells(cells))
+    lg = eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225)[sel]
+    v = eng.d_value[:n].cpu().numpy()[sel]
+    assert np.abs(lg - ref_lg).max() < 1e-4 and np.abs(v - ref_v).max() < 1e-4
+    probs = eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225)[sel]
+    prior = eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225)[sel]
+    for k in range(32):  # the reference's vector is the dense prior at the empty cells (row-major)
+        assert np.array_equal(prior[k][cells[k] == 0], oracle.prior(probs[k], cells[k])), k
+        assert (prior[k][cells[k] != 0] == 0).all()
+
+
+def test_config2_4096_slot_step_properties(oracle):
+    """One timed-size step of the bench workload (4096 slots, 200 sims, PV forward on
+    every node) after a burn-in: no drops; for sampled slots the number of
+    forwards over boards containing the slot's root equals the oracle's predict()
+    count and the move played equals the oracle's; every finished game's records
+    are plies 0..n-1 with z = +1 for the winner's plies, -1 for the loser's, 0 on a
+    draw; probabilities sum to 1 and priors renormalise over the empty cells."""
+    sd, w = _pv_weights()
+    eng = SelfPlayEngine(n_slots=4096, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.0, seed=SEED,
+                         pv_weights=w, plies_per_step=1)
+    eng.advance(70)
+    st0, gid0 = eng.boards()
+    eng.step()
+    c = eng.counters()
+    assert c["leaves_dropped"] == 0 and c["records_dropped"] == 0 and c["moves"] == 4096
+    n = int(c["leaves"])
+    assert 0 < n <= eng.leaf_cap
+    rows = _leaf_rows(eng, n)
+    st1, gid1 = eng.boards()
+    p = oracle.make_params("medium", sims=200, beta=0.0, seed=SEED)
+    nm = st0["n_moves"]
+    blk = np.unpackbits(np.ascontiguousarray(st0["black"]).view(np.uint8), axis=1).astype(bool)
+    wht = np.unpackbits(np.ascontiguousarray(st0["white"]).view(np.uint8), axis=1).astype(bool)
+    cand = [s for s in range(4096) if nm[s] >= 12]
+    checked = 0
+    for s in np.random.default_rng(3).permutation(cand):
+        if checked == 12:
+            break
+        # a leaf of slot s' holds s's root only if s's stones missing from s' root fit on
+        # a search path: skip roots within 8 stones of another slot's (same opening line)
+        miss = (blk[s] & ~blk).sum(axis=1) + (wht[s] & ~wht).sum(axis=1)
+        miss[s] = 1 << 20
+        if miss.min() <= 8:
+            continue
+        cells0 = boards.words_to_cells(st0["black"][s], st0["white"][s])
+        b = oracle.new_board([])
+        for i in range(225):
+            b.cell[i] = int(cells0[i])
+        b.n_moves, b.player = int(st0["n_moves"][s]), int(st0["player"][s])
+        mv, tree = oracle.get_move(b, b.player, p, int(gid0[s]))
+        par = tree["parent"]
+        depth = [0] * len(par)
+        for i in range(1, len(par)):
+            depth[i] = depth[par[i]] + 1
+        assert max(depth) <= 8
+        rb, rw = st0["black"][s], st0["white"][s]
+        inside = np.all((rows[:, :8] & rb) == rb, axis=1) & np.all((rows[:, 8:] & rw) == rw, axis=1)
+        assert int(inside.sum()) == tree["predicts"], (s, int(inside.sum()), tree["predicts"])
+        if gid1[s] == gid0[s]:  # the game goes on: the board is the root plus the oracle's move
+            cells1 = boards.words_to_cells(st1["black"][s], st1["white"][s])
+            exp = cells0.copy()
+            exp[mv] = st0["player"][s]
+            assert (cells1 == exp).all(), s
+        checked += 1
+    assert checked == 12
+    recs = eng.records()
+    for gid in np.unique(recs["game_id"]):
+        r = recs[recs["game_id"] == gid]
+        r = r[np.argsort(r["ply"])]
+        assert list(r["ply"]) == list(range(len(r)))
+        assert list(r["player"]) == [1 + (i % 2) for i in range(len(r))]
+        z = r["z"]
+        if (z == 0).all():
+            continue
+        winner = int(r["player"][np.argmax(z)])
+        assert all(zz == (1 if pl == winner else -1) for zz, pl in zip(z, r["player"]))
+    probs = eng.d_probs[: n * 225].view(n, 225)
+    assert torch.allclose(probs.sum(dim=1), torch.ones(n, device="cuda"), atol=1e-5)
+    ps = eng.d_prior[: n * 225].view(n, 225).sum(dim=1)
+    assert torch.allclose(ps, torch.ones_like(ps), rtol=0, atol=1e-12)

@@ -56,6 +56,7 @@ def test_dataset_build_exact(fix):
 
 
 def test_dataset_gather_ids():
+    from gzero import _lib
     from gzero.train import DeviceDataset
     g = golden("sgd")
     _, rec = _records(g)
@@ -63,7 +64,9 @@ def test_dataset_gather_ids():
     X, Y, V = ds.materialize()
     n = len(ds)
     ids = torch.tensor([0, n - 1, 5, 5, n, -1, 200, 201, 207, 3 * n], dtype=torch.int64, device="cuda")
-    x, y, v = ds.gather(ids)
+    with pytest.raises(_lib.GzeroError):  # the wrappers refuse out-of-range ids ...
+        ds.gather(ids)
+    x, y, v = ds.gather(ids, check=False)  # ... the kernel writes label -1 and zero planes
     for k, i in enumerate(ids.tolist()):
         if 0 <= i < n:
             assert torch.equal(x[k], X[i]) and int(y[k]) == int(Y[i]) and float(v[k]) == float(V[i])
@@ -143,3 +146,73 @@ def test_device_trainer_follows_reference():
             assert float(a.sum()) == s, k
         elif a.size >= 64:
             assert abs(float(np.sqrt((a * a).sum())) - ss ** 0.5) <= 1e-2 * ss ** 0.5, k
+
+
+def test_run_iteration_config5_one_gpu(oracle):
+    """One training.main iteration (training.run_iteration, training.py:399-480) on
+    one GPU: 4 self-play games (8 sims, beta 0.2, 2 planner plies per rollout, the
+    PV forward on every node), the 35 % augmented dataset, the 90/10 split and one
+    epoch of SGD.  Games = the oracle's play_one_game driven by the GPU planner
+    nets' outputs; dataset = the numpy restatement on the same random draws;
+    train / val loss = the reference's CPU loop (training.train_epoch /
+    validate_epoch with a DataLoader) on that dataset within 3e-3."""
+    from torch.utils.data import DataLoader, Subset, TensorDataset
+    import training
+    from bg_planner import BGPlannerAI
+    from gzero import boards, planner_nets, weights
+    from gzero.train import DeviceTrainer
+    from neural_network import GomokuModel
+    n_games, sims, steps, seed = 4, 8, 2, 11
+    planner = BGPlannerAI(1, "medium", seed=0)
+    planner.graph_net.load_state_dict(planner_nets.init_graphnet_state(21))
+    planner.opp_dqn.load_state_dict(planner_nets.init_dqn_state(22))
+    gnw = planner.device_weights()
+    sd0 = weights.init_state_dict(seed=7)
+    model = GomokuModel(device="cpu")
+    model.model.load_state_dict(sd0)
+    trainer = DeviceTrainer(model)
+    random.seed(123)
+    torch.manual_seed(456)
+    res = training.run_iteration(model, trainer, 0, n_games, num_simulations=sims, beta=0.2, planner_steps=steps,
+                                 seed=seed, epochs=1, planner=planner, verbose=False)
+    # the games (ids 0..3 at iteration 0), against the oracle with the GPU's p / q
+    from gzero import device
+
+    def pq(board, game_id, sim, step):
+        cells = np.frombuffer(bytes(board.cell), dtype=np.int8)
+        bl, wh = boards.cells_to_words(cells.reshape(1, 225))
+        p, q, _ = device.gn_forward(gnw, boards.leaf_words(bl, wh))
+        return p[0], q[0]
+
+    prm = oracle.make_params("medium", sims=sims, beta=0.2, seed=seed, planner_steps=steps, pq=pq)
+    cells, moves, zs = [], [], []
+    for gid in range(n_games):
+        ref = oracle.play_game(prm, prm, gid, want_cells=True)
+        cells.append(ref["cells"])
+        moves += ref["moves"]
+        zs += ref["z"]
+    cells = np.concatenate(cells)
+    assert res["records"] == len(moves)
+    # the dataset and split on the same random draws (random.seed(123) above)
+    rnd = random.Random(123)
+    n = len(moves)
+    sel = rnd.sample(range(n), k=max(1, int(n * 0.35)))
+    ox, oy, ov = TO.dataset_samples(cells, np.array(moves), np.array(zs), sel)
+    assert res["samples"] == len(oy)
+    idx = list(range(len(oy)))
+    rnd.shuffle(idx)
+    split = int(len(idx) * 0.9)
+    # the reference's loop on CPU from the same initial weights and torch seed
+    cpu = GomokuModel(device="cpu")
+    cpu.model.load_state_dict(sd0)
+    ds = TensorDataset(torch.from_numpy(ox), torch.from_numpy(oy.astype(np.int64)),
+                       torch.from_numpy(ov.astype(np.float32)).view(-1, 1))
+    torch.manual_seed(456)
+    opt = torch.optim.Adam(cpu.model.parameters(), lr=8e-4, weight_decay=1e-5)
+    tl = training.train_epoch(cpu, DataLoader(Subset(ds, idx[:split]), batch_size=128, shuffle=True), opt,
+                              torch.device("cpu"), grad_clip=0.8)
+    vl = training.validate_epoch(cpu, DataLoader(Subset(ds, idx[split:]), batch_size=128, shuffle=False),
+                                 torch.device("cpu"))
+    np.testing.assert_allclose(res["train_loss"], tl, rtol=3e-3)
+    np.testing.assert_allclose(res["val_loss"], vl, rtol=3e-3)
+    assert trainer.scheduler.get_last_lr() == [8e-4]  # StepLR(2, 0.85) after one step
