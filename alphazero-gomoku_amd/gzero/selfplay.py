@@ -89,11 +89,12 @@ class SelfPlayEngine:
         (the moves are the same either way: the search never reads the priors,
         ai_agent.py:523).  Used to bring the slots to a steady-state mix of game plies
         (continuous refill) before a measurement; records of games finished here are
-        not kept."""
-        if self.planner_steps:
-            raise ValueError("advance() is for planner_steps == 0 (planner plies need the GN forward)")
+        not kept.  On a planner engine (config 4) the burn-in plies are searched without
+        planner plies (the planner pipeline needs the GN forward per ply): the slots
+        reach a steady-state mix of positions, and the measured plies are planner plies."""
         p = _lib.SearchParams.from_buffer_copy(self.params)
         p.flags = 0
+        p.planner_steps = 0
         for _ in range(int(n_plies)):
             self.d_counters.zero_()
             _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(p), 1,

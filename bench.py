@@ -74,59 +74,174 @@ def load_clock(kernel):
     return None
 
 
-def cpu_baseline(positions, sims, seed, budget_s, torch_threads):
-    """C oracle (single thread) searching the same positions the GPU starts its
-    timed window from, plus torch-CPU fp32 forwards for the nodes it created."""
+def _cpu_worker(task):
+    """One host process of the CPU baseline: the C oracle's search (1 thread) of
+    `plies` MCTS plies from a timed-window start position, then the torch-fp32 CPU
+    forwards (1 thread) of every node those searches created -- the reference's
+    per-ply work (ai_agent.py:168-204 + GomokuModel.predict per node)."""
+    black, white, n_moves, player, gid, sims, seed, budget = task
+    import torch as T
+    T.set_num_threads(1)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
-    O.build()
-    from gzero.boards import words_to_cells
-    t_search = 0.0
-    plies = 0
-    predicts = 0
-    t_start = time.perf_counter()
-    for (black, white, n_moves, player, gid) in positions:
-        cells = words_to_cells(black, white)
-        b = O.Board()
-        O.lib().or_board_init(b)
-        for i in range(225):
-            b.cell[i] = int(cells[i])
-        b.n_moves, b.player = int(n_moves), int(player)
-        p = O.make_params("medium", sims=sims, beta=0.0, seed=seed)
-        while not b.over and time.perf_counter() - t_start < budget_s:
-            t0 = time.perf_counter()
-            mv, tree = O.get_move(b, b.player, p, gid, cap=8)
-            t_search += time.perf_counter() - t0
-            predicts += tree["predicts"]
-            plies += 1
-            O.lib().or_make_move(b, mv // 15, mv % 15)
-            if plies >= 8:
-                break
-        if time.perf_counter() - t_start >= budget_s:
-            break
-    # PV forwards on the host cores, timed on a bounded number of boards and scaled
-    torch.set_num_threads(torch_threads)
+    from gzero.boards import words_to_cells, planes_from_cells
+    cells = words_to_cells(black, white)
+    b = O.Board()
+    O.lib().or_board_init(b)
+    for i in range(225):
+        b.cell[i] = int(cells[i])
+    b.n_moves, b.player = int(n_moves), int(player)
     net = weights.PolicyValueNet()
     net.load_state_dict(weights.init_state_dict(0))
     net.eval()
-    n_eval = max(1, min(predicts, 1024))
-    x = torch.from_numpy(np.random.default_rng(0).integers(0, 2, (n_eval, 3, 15, 15)).astype(np.float32))
-    with torch.no_grad():
-        net(x[:8])
-        t0 = time.perf_counter()
-        for i in range(0, n_eval, 256):
-            net(x[i:i + 256])
-        t_pv = (time.perf_counter() - t0) * predicts / n_eval
-    total = t_search + t_pv
+    p = O.make_params("medium", sims=sims, beta=0.0, seed=seed)
+    t0 = time.perf_counter()
+    plies = predicts = 0
+    while not b.over and time.perf_counter() - t0 < budget:
+        root = np.frombuffer(bytes(b.cell), dtype=np.int8).copy()
+        mv, tree = O.get_move(b, b.player, p, gid, cap=4096)
+        # the forwards of this ply's nodes: every node's board (root + path stones);
+        # terminal nodes are not forwarded (predicts counts the non-terminal ones)
+        par, mvs = tree["parent"], tree["move"]
+        nb = np.zeros((len(par), 225), np.int8)
+        col = np.zeros(len(par), np.int8)
+        nb[0], col[0] = root, 3 - b.player
+        for i in range(1, len(par)):
+            nb[i] = nb[par[i]]
+            col[i] = 3 - col[par[i]]
+            nb[i, mvs[i]] = col[i]
+        n = min(tree["predicts"], len(par))
+        x = T.from_numpy(planes_from_cells(nb[:n]))
+        with T.no_grad():
+            for i in range(0, n, 64):
+                net(x[i:i + 64])
+        predicts += n
+        plies += 1
+        O.lib().or_make_move(b, mv // 15, mv % 15)
+    return plies, predicts, time.perf_counter() - t0
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(pool, procs, positions, sims, seed, budget_s):
+    """The reference's CPU self-play work on the GPU box's host cores: `procs`
+    single-thread processes (P processes x 1 thread), each
+    searching from one of the GPU run's timed-window start positions with the C
+    oracle and running the torch-fp32 CPU forwards of the nodes it created, for
+    budget_s seconds; value = all processes' plies / wall time."""
+    tasks = [positions[i % len(positions)] + (sims, seed, budget_s) for i in range(procs)]
+    t0 = time.perf_counter()
+    res = pool.map(_cpu_worker, tasks)
+    wall = time.perf_counter() - t0
+    plies = sum(r[0] for r in res)
+    predicts = sum(r[1] for r in res)
     return {
-        "value": plies / total if total > 0 else None,
+        "value": plies / wall if wall > 0 else None,
         "unit": "moves/s",
-        "cores": int(torch_threads),
+        "cores": int(procs),
         "kind": "port",
-        "sample": (f"{plies} MCTS plies at {sims} sims from the GPU run's timed-window start positions: "
-                   f"C oracle search {t_search:.2f}s on 1 thread + {predicts} policy-value forwards "
-                   f"(torch fp32 CPU, batch 256, {torch_threads} threads; {n_eval} timed, scaled) {t_pv:.2f}s"),
+        "cpu": cpu_model(),
+        "sample": (f"{procs} processes x 1 thread for {budget_s:.0f} s each ({wall:.1f} s wall): {plies} MCTS plies "
+                   f"at {sims} sims from the GPU run's timed-window start positions (C oracle search) + the "
+                   f"{predicts} policy-value forwards of the nodes they created (torch fp32 CPU, 1 thread)"),
     }
+
+
+def measure(eng, steps, warmup, burn_in, ws, ex=None):
+    """Burn-in plies (no PV forward), `warmup` untimed steps, then EXACTLY `steps`
+    timed steps bracketed by barrier + synchronize, MAX over ranks.  A step = every
+    slot plays plies_per_step plies, then the PV forward of every node created,
+    then (N > 1) the record exchange."""
+    def barrier():
+        if ws > 1:
+            dist.barrier()
+
+    def step():
+        eng.launch_search()
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        eng.launch_pv()
+        ev[1].record()
+        ctr = eng.d_counters.clone()  # per-step counters, stays on the device
+        if ex is not None:
+            ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
+            ex.exchange()
+        return ev, ctr
+
+    if burn_in:
+        eng.advance(burn_in)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    boards0, gids0 = eng.boards()  # timed-window start positions (for the CPU baseline)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    recs = [step() for _ in range(steps)]
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c in recs]
+    moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs)), float(sum(int(c["mcts_moves"]) for c in ctrs))],
+                         dtype=torch.float64, device="cuda")
+    if ws > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(moves, op=dist.ReduceOp.SUM)
+    T = float(elapsed.item())
+    leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
+    pv_ms = [a.elapsed_time(b) for (a, b), _ in recs]
+    return {
+        "T": T, "moves": float(moves[0].item()), "mcts": float(moves[1].item()),
+        "pv_ms": pv_ms, "leaves": leaves,
+        "dropped": sum(int(c["leaves_dropped"]) + max(0, int(c["leaves"]) - eng.leaf_cap) for c in ctrs),
+        "boards0": boards0, "gids0": gids0,
+    }
+
+
+def roofline_of(m, precision):
+    mean_leaves = float(np.mean(m["leaves"]))
+    mean_pv_s = float(np.mean(m["pv_ms"])) / 1e3
+    achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
+    traffic, _ = load_traffic(mean_leaves) if precision == "f16x3" else (None, None)
+    if precision == "fp32":
+        peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
+    else:
+        # each algorithmic multiply of the 3x3 convs costs 3 fp16 MFMA products
+        peak = F16_MFMA_PEAK_TFLOPS / 3.0
+        note = ("3-term fp16 split on v_mfma_f32_16x16x32_f16 (f32 accumulate): peak = dense fp16 MFMA "
+                "peak / 3 products per fp32-equivalent multiply")
+    r = {
+        "kernel": (f"gz_pv_forward<{precision}> (AlphaZeroGomokuNet forward"
+                   + (": pv_kernel_f16x3 tower + pv_heads_kernel FC heads + pv_prior_kernel)" if precision == "f16x3"
+                      else ": pv_kernel_f32 + pv_prior_kernel)")),
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": round(peak, 1),
+        "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": traffic,
+        "per_launch": {"boards": round(mean_leaves, 1), "flop_per_board": PV_FLOP,
+                       "avg_ms": round(float(np.mean(m["pv_ms"])), 3),
+                       "us_per_board": round(float(np.mean(m["pv_ms"])) * 1e3 / max(1.0, mean_leaves), 4)},
+        "note": note,
+    }
+    clk = load_clock("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32")
+    if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
+        r["clock"] = {"ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
+                      "peak_at_clock": round(peak * clk["median_ghz"] / 2.4, 1),
+                      "frac_at_clock": round(achieved / (peak * clk["median_ghz"] / 2.4), 4),
+                      "source": "profiles/r01/clock.json (rocprofv3 GRBM_GUI_ACTIVE / duration)"}
+    return r
 
 
 def main():
@@ -146,110 +261,57 @@ def main():
     ap.add_argument("--no-elided", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--burn-in", type=int, default=None,
-                    help="plies played before the warm-up without the PV forward, so the timed window sees the "
-                         "steady-state mix of game plies of continuous refill (default 96; 0 in planner mode)")
+    ap.add_argument("--burn-in", type=int, default=600,
+                    help="plies played before the warm-up without the PV forward (the search never reads the "
+                         "priors, so the moves are the same), so the timed window sees continuous refill's "
+                         "steady-state mix of game plies rather than 4096 games started together")
     ap.add_argument("--planner-steps", type=int, default=0,
                     help="BG-planner plies per rollout (BASELINE config 4: 5 with --beta 0.2)")
+    ap.add_argument("--config4-steps", type=int, default=20,
+                    help="N = 1 secondary: BASELINE config 4 (beta 0.2, planner_steps 5) timed over this many "
+                         "steps after the same burn-in (0 = skip)")
+    ap.add_argument("--fp32-steps", type=int, default=4,
+                    help="N = 1 secondary: the exact-fp32 PV forward timed over this many steps (0 = skip)")
     args = ap.parse_args()
 
     rank, ws = gdist.init_from_env()
+    pool = None
+    procs = 0
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        # host worker processes come from a forkserver started before this process
+        # touches the GPU (no process that initialised HIP forks or execs)
+        import multiprocessing as mp
+        procs = min(16, os.cpu_count() or 1)
+        pool = mp.get_context("forkserver").Pool(procs)
+        pool.map(abs, range(procs))  # start the workers now
     torch.cuda.set_device(gdist.local_device())
     if ws != args.gpus and rank == 0:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")
 
-    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision=args.pv_precision)
+    sd = weights.init_state_dict(0)
+    w = PVWeights(weights.pack_pv_weights(sd), precision=args.pv_precision)
     base, stride = gdist.shard_ids(rank, ws, args.slots)
     P = args.plies_per_step
     gnw = None
-    if args.planner_steps:
+    if args.planner_steps or (ws == 1 and args.config4_steps):
         from gzero import planner_nets
         gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
-    eng = SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
-                         beta=args.beta, seed=args.seed, pv_weights=w, plies_per_step=P,
-                         game_id_base=base, game_id_stride=stride, planner_steps=args.planner_steps,
-                         planner_difficulty="medium", gn_weights=gnw)
 
-    def barrier():
-        if ws > 1:
-            dist.barrier()
+    def engine(beta, planner_steps, pv):
+        return SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
+                              beta=beta, seed=args.seed, pv_weights=pv, plies_per_step=P,
+                              game_id_base=base, game_id_stride=stride, planner_steps=planner_steps,
+                              planner_difficulty="medium", gn_weights=gnw if planner_steps else None)
 
+    eng = engine(args.beta, args.planner_steps, w)
     # N > 1: the per-step RCCL all-gather of finished games' (s, pi, z) records,
     # fixed-size and sync-free (gzero.dist.RecordExchange: counts stay on the device)
     ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda") if ws > 1 else None
-
-    def step():
-        eng.launch_search()
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev[0].record()
-        eng.launch_pv()
-        ev[1].record()
-        ctr = eng.d_counters.clone()  # per-step counters, stays on the device
-        if ex is not None:
-            ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
-            ex.exchange()
-        return ev, ctr
-
-    burn_in = args.burn_in if args.burn_in is not None else (0 if args.planner_steps else 96)
-    if burn_in:
-        eng.advance(burn_in)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    boards0, gids0 = eng.boards()  # timed-window start positions (for the CPU baseline)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    recs = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c in recs]
-    moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs)), float(sum(int(c["mcts_moves"]) for c in ctrs))],
-                         dtype=torch.float64, device="cuda")
-    if ws > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(moves, op=dist.ReduceOp.SUM)
-    T = float(elapsed.item())
-    total_moves = float(moves[0].item())
-    total_mcts = float(moves[1].item())
-    value = total_moves / T
-    pv_ms = [a.elapsed_time(b) for (a, b), _ in recs]
-    leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
-    dropped = sum(int(c["leaves_dropped"]) + max(0, int(c["leaves"]) - eng.leaf_cap) for c in ctrs)
-    mean_leaves = float(np.mean(leaves))
-    mean_pv_s = float(np.mean(pv_ms)) / 1e3
-    achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
-    traffic, _ = load_traffic(mean_leaves) if args.pv_precision == "f16x3" else (None, None)
-    if args.pv_precision == "fp32":
-        peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
-    else:
-        # each algorithmic multiply of the 3x3 convs costs 3 fp16 MFMA products
-        peak = F16_MFMA_PEAK_TFLOPS / 3.0
-        note = ("3-term fp16 split on v_mfma_f32_16x16x32_f16 (f32 accumulate): peak = dense fp16 MFMA "
-                "peak / 3 products per fp32-equivalent multiply")
-    roofline = {
-        "kernel": (f"gz_pv_forward<{args.pv_precision}> (AlphaZeroGomokuNet forward"
-                   + (": pv_kernel_f16x3 tower + pv_heads_kernel FC heads)" if args.pv_precision == "f16x3"
-                      else ": pv_kernel_f32)")),
-        "bound": "mfma",
-        "achieved": round(achieved, 3),
-        "peak": round(peak, 1),
-        "unit": "TFLOP/s",
-        "frac": round(achieved / peak, 4),
-        "traffic": traffic,
-        "per_launch": {"boards": round(mean_leaves, 1), "flop_per_board": PV_FLOP,
-                       "avg_ms": round(float(np.mean(pv_ms)), 3)},
-        "note": note,
-    }
-    clk = load_clock("pv_kernel_f16x3" if args.pv_precision == "f16x3" else "pv_kernel_f32")
-    if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
-        roofline["clock"] = {"ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
-                             "peak_at_clock": round(peak * clk["median_ghz"] / 2.4, 1),
-                             "frac_at_clock": round(achieved / (peak * clk["median_ghz"] / 2.4), 4),
-                             "source": "profiles/r01/clock.json (rocprofv3 GRBM_GUI_ACTIVE / duration)"}
-
+    burn_in = args.burn_in
+    m = measure(eng, args.steps, args.warmup, burn_in, ws, ex)
+    T = m["T"]
+    value = m["moves"] / T
+    half = args.steps // 2
     out = None
     if rank == 0:
         out = {
@@ -270,28 +332,55 @@ def main():
                              f"games per GPU, 15x15, {args.sims} sims/move, medium (c_puct 1.6, exploration 0.05), "
                              f"beta={args.beta}, planner_steps={args.planner_steps}, continuous refill (timed after "
                              f"{burn_in} burn-in plies: the steady-state mix of game plies); policy-value "
-                             "forward on every non-terminal node the searches create (reference-work mode, "
-                             f"{args.pv_precision})"),
+                             "forward + masked prior on every non-terminal node the searches create "
+                             f"(reference-work mode, {args.pv_precision})"),
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,
                 "plies_per_step": P,
                 "burn_in_plies": burn_in,
                 "parallelism": f"dp{ws} (games sharded by id, all-gather of records)",
-                "pv_boards_per_step": round(mean_leaves, 1),
-                "pv_boards_dropped": dropped,
+                "pv_boards_per_step": round(float(np.mean(m["leaves"])), 1),
+                "pv_boards_per_step_halves": [round(float(np.mean(m["leaves"][:half])), 1),
+                                              round(float(np.mean(m["leaves"][half:])), 1)] if half else None,
+                "pv_boards_dropped": m["dropped"],
             },
-            "roofline": roofline,
-            "mcts_moves": {"value": round(total_mcts / T, 3), "unit": "moves/s",
-                           "share": round(total_mcts / total_moves, 4) if total_moves else None,
+            "roofline": roofline_of(m, args.pv_precision),
+            "mcts_moves": {"value": round(m["mcts"] / T, 3), "unit": "moves/s",
+                           "share": round(m["mcts"] / m["moves"], 4) if m["moves"] else None,
                            "note": "plies decided by a search (SURVEY 8d): value counts every ply, incl. the opening "
                                    "plies 0-5 that _opening_move plays without one (ai_agent.py:138-166)"},
         }
-
     if ex is not None and rank == 0:
         out["record_exchange"] = {"chunk_records": ex.chunk, "bytes_per_rank_per_step": ex.chunk * ex.item,
                                   "pending_after": int(ex.pending().item()), "overflow": int(ex.overflow.item()),
                                   "note": "fixed-size RCCL all_gather_into_tensor per step, counts on the device"}
+    boards0, gids0 = m["boards0"], m["gids0"]
+    del eng
+
+    # ---- N = 1 secondaries: config 4 and the exact-fp32 forward (same burn-in)
+    if ws == 1 and args.config4_steps and not args.planner_steps:
+        e4 = engine(0.2, 5, w)
+        m4 = measure(e4, args.config4_steps, 2, burn_in, 1)
+        out["config4"] = {
+            "value": round(m4["moves"] / m4["T"], 3), "unit": "moves/s", "steps": args.config4_steps, "warmup": 2,
+            "ms_per_step": round(m4["T"] / args.config4_steps * 1e3, 3),
+            "pv_boards_per_step": round(float(np.mean(m4["leaves"])), 1),
+            "workload": (f"BASELINE config 4: {args.slots} games, {args.sims} sims/move, beta 0.2, planner_steps 5 "
+                         "(every rollout starts with 5 BGPlannerAI plies: GraphNet + OpponentDQN forward, knowledge "
+                         f"search, top-k compose), PV forward + prior on every node; burn-in {burn_in} plies "
+                         "searched without planner plies (the planner pipeline needs the GN forward per ply)"),
+        }
+        del e4
+    if ws == 1 and args.fp32_steps and args.pv_precision == "f16x3" and not args.planner_steps:
+        w32 = PVWeights(weights.pack_pv_weights(sd), precision="fp32")
+        e32 = engine(args.beta, 0, w32)
+        m32 = measure(e32, args.fp32_steps, 1, burn_in, 1)
+        out["fp32"] = {"value": round(m32["moves"] / m32["T"], 3), "unit": "moves/s", "steps": args.fp32_steps,
+                       "warmup": 1, "ms_per_step": round(m32["T"] / args.fp32_steps * 1e3, 3),
+                       "roofline": roofline_of(m32, "fp32"),
+                       "note": "config 2 with the exact-f32 MFMA forward (v_mfma_f32_16x16x4_f32)"}
+        del e32, w32
 
     # ---- prior-elided run (same kernel, no PV gather / forward)
     if not args.no_elided and not args.planner_steps:
@@ -304,7 +393,8 @@ def main():
             el.launch_search(n)
             done += n
         torch.cuda.synchronize()
-        barrier()
+        if ws > 1:
+            dist.barrier()
         e0 = time.perf_counter()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -318,7 +408,8 @@ def main():
             done += n
         ev1.record()
         torch.cuda.synchronize()
-        barrier()
+        if ws > 1:
+            dist.barrier()
         e1 = torch.tensor([time.perf_counter() - e0], dtype=torch.float64, device="cuda")
         mv_t = torch.tensor([float(mv_el)], dtype=torch.float64, device="cuda")
         if ws > 1:
@@ -333,11 +424,12 @@ def main():
                 "note": "identical moves and tuples; the reference never reads the priors (ai_agent.py:523)",
             }
 
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        pos = [(boards0["black"][i], boards0["white"][i], boards0["n_moves"][i], boards0["player"][i], int(gids0[i]))
-               for i in range(min(8, len(boards0)))]
-        threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(pos, args.sims, args.seed, args.cpu_seconds, threads)
+    if pool is not None:
+        pos = [(boards0["black"][i], boards0["white"][i], int(boards0["n_moves"][i]), int(boards0["player"][i]),
+                int(gids0[i])) for i in range(min(64, len(boards0))) if boards0["n_moves"][i] >= 6]
+        out["cpu_baseline"] = cpu_baseline(pool, procs, pos, args.sims, args.seed, args.cpu_seconds)
+        pool.close()
+        pool.join()
 
     if rank == 0:
         print(json.dumps(out), flush=True)
