@@ -845,7 +845,7 @@ extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_g
     hipStream_t s = (hipStream_t)stream;
     const int S = p->num_simulations;
     Workspace w = carve(d_workspace, n, S);
-    LeafSink sink{d_leaves, leaf_cap, d_leaf_count};
+    LeafSink sink{d_leaves, leaf_cap, d_leaf_count, nullptr};
     const int n_jobs = n * S;
     const int jb = (n_jobs + 255) / 256;
     int rc;

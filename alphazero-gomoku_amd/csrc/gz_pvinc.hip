@@ -1,0 +1,479 @@
+// gz_pvinc.hip -- incremental policy-value forward of a search's sibling nodes
+// (AlphaZeroGomokuNet, neural_network.py:74-159, f16x3 precision).
+//
+// MCTSNode.__init__ runs GomokuModel.predict for every new node (ai_agent.py:
+// 522-523).  A root child differs from the root by one stone at cell m, so in
+// layer L of the tower (x0 = conv0, y1, x1, y2, x2) only the positions within
+// Chebyshev radius L+1 of m can differ from the root's maps: 3x3, 5x5, 7x7, 9x9,
+// 11x11 windows (clipped to the board) -- about 31 % of the 4 x 225 positions of
+// the residual convs.  The root is evaluated by the full kernel, which also
+// stores its x0, y1, x1, y2 maps (gz_pvnet.hip, pv_kernel_f16x3<.., true>); each
+// child then recomputes only its windows, reading the root's values around them.
+//
+// Exactness: every recomputed position takes the same products in the same order
+// as the full kernel (k = tap*128 + cin in 32-deep MFMA k-steps, hi*hi, w_lo*a_hi,
+// w_hi*a_lo; the same epilogue, the same hi/lo split, the same head-conv partial
+// sums per wave), and an MFMA output element depends only on its own row and
+// column operands, so the child's logits, value, softmax and prior are bit for
+// bit those of a full forward of the child's board (tests/test_gpu_pvinc.py).
+//
+// One 512-thread workgroup per child at a time (8 waves, wave = n-tile pair x M
+// half, as the full kernel).  LDS holds the layer inputs as windows around m in
+// the full kernel's hi/lo plane layout ([16 channel groups][P positions][8]):
+//   X0 r3 (7x7)  Y1 r4 (9x9)  X1 r5 (11x11)  Y2 r6 (13x13)
+// -- the input of layer L needs the previous map at radius L+2; positions outside
+// the recomputed radius are the root's, off-board positions are zero (the
+// convolution's padding).  X0 and Y1 are dead once x1 is computed, so Y2 reuses
+// their space: 62 KB (X1) + 86.5 KB (Y2) + 7 KB.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "gz_f16conv.h"
+#include "gz_pvnet.h"
+#include "../../include/gzero.h"
+
+using namespace gzpv;
+
+namespace {
+
+using namespace gzc;
+
+constexpr int NTC = 512;
+constexpr int P_X0 = 49, P_Y1 = 81, P_X1 = 121, P_Y2 = 169;
+constexpr int wbytes(int P) { return 2 * 16 * P * 16; }  // hi + lo planes
+constexpr int OFF_X1 = 0;
+constexpr int OFF_Y2 = OFF_X1 + wbytes(P_X1);
+constexpr int OFF_X0 = OFF_Y2;                   // aliases Y2 (dead by then)
+constexpr int OFF_Y1 = OFF_X0 + wbytes(P_X0);    // aliases Y2
+constexpr int OFF_HP = OFF_Y2 + wbytes(P_Y2);
+constexpr int HP_ROWS = 128;                     // >= 121 rows of the x2 window
+constexpr int OFF_COL = OFF_HP + 4 * 3 * HP_ROWS * 4;
+constexpr int LDS_C = OFF_COL + 16 * 32 * 2;
+static_assert(OFF_Y1 + wbytes(P_Y1) <= OFF_HP, "X0 + Y1 fit in the Y2 region");
+static_assert(LDS_C <= 160 * 1024, "LDS budget");
+
+// A window of a map: radius r around the child's stone (cr, cc), width w = 2r+1,
+// P = w*w positions, hi plane then lo plane, each [16 cg][P][8].
+struct Win {
+    _Float16* hi;
+    int P, w, r;
+    __device__ int plane() const { return 16 * P * 8; }
+    __device__ int off(int ch0, int loc) const { return ((ch0 >> 3) * P + loc) * 8 + (ch0 & 7); }
+};
+
+__device__ inline Win make_win(char* lds, int off, int r) {
+    Win x;
+    x.hi = (_Float16*)(lds + off);
+    x.r = r;
+    x.w = 2 * r + 1;
+    x.P = x.w * x.w;
+    return x;
+}
+
+// root's values (global map, full kernel layout [plane][16 cg][256][8]) into the
+// window, except the recomputed square of radius rc; zeros off the board
+__device__ inline void fill_window(const Win& x, int rc, const _Float16* __restrict__ gm, int cr, int cc, int tid) {
+    const int n = 2 * 16 * x.P;
+    for (int i = tid; i < n; i += NTC) {
+        const int plane = i / (16 * x.P);
+        const int rem = i - plane * 16 * x.P;
+        const int cg = rem / x.P, loc = rem - cg * x.P;
+        const int pr = cr - x.r + loc / x.w, pc = cc - x.r + loc % x.w;
+        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
+        if (on && dr <= rc && dc <= rc) continue;  // written by the layer that recomputes it
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (on) v = *(const uint4*)(gm + plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8);
+        *(uint4*)(x.hi + plane * x.plane() + (cg * x.P + loc) * 8) = v;
+    }
+}
+
+// the recomputed rows of one layer: the square of radius rl around (cr, cc),
+// clipped, row-major
+struct Rows {
+    int r0, c0, wr, n;
+};
+__device__ inline Rows make_rows(int cr, int cc, int rl) {
+    Rows q;
+    q.r0 = cr - rl < 0 ? 0 : cr - rl;
+    const int r1 = cr + rl > BN - 1 ? BN - 1 : cr + rl;
+    q.c0 = cc - rl < 0 ? 0 : cc - rl;
+    const int c1 = cc + rl > BN - 1 ? BN - 1 : cc + rl;
+    q.wr = c1 - q.c0 + 1;
+    q.n = (r1 - q.r0 + 1) * q.wr;
+    return q;
+}
+
+// implicit-GEMM 3x3 conv of the window `in` at the positions ctr[m] (window-local
+// index of the output position, per lane), the wave's n-tiles {2np, 2np+1}: the
+// k-steps, products and their order are those of f16_conv (gz_f16conv.h).
+template <int NM>
+__device__ __forceinline__ void win_conv(const Win& in, const int (&ctr)[NM], const _Float16* __restrict__ Wf, int np,
+                                         int lane, f32x4 (&acc)[2][NM]) {
+    constexpr int CQ = 4, KS = 9 * CQ;
+    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
+    const int q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = ((2 * np) * 64 + lane) * 16;
+    auto wload = [&](int ks, int n, int lo) -> h8 {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+    };
+    const _Float16* lo_plane = in.hi + in.plane();
+    h8 b[2][2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        b[n][0] = wload(0, n, 0);
+        b[n][1] = wload(0, n, 1);
+    }
+    for (int tap = 0; tap < 9; tap++) {
+        const int toff = (tap / 3 - 1) * in.w + (tap % 3 - 1);
+        int nb[NM];
+#pragma unroll
+        for (int m = 0; m < NM; m++) nb[m] = (ctr[m] + toff + q * in.P) * 8;
+#pragma unroll
+        for (int cq = 0; cq < CQ; cq++) {
+            const int ks = tap * CQ + cq;
+            const int ao = cq * 4 * in.P * 8;
+            h8 ah[NM], al[NM];
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                ah[m] = *(const h8*)(in.hi + ao + nb[m]);
+                al[m] = *(const h8*)(lo_plane + ao + nb[m]);
+            }
+            h8 bn[2][2];
+            const int ks1 = ks + 1 < KS ? ks + 1 : 0;
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                bn[n][0] = wload(ks1, n, 0);
+                bn[n][1] = wload(ks1, n, 1);
+            }
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
+            }
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                b[n][0] = bn[n][0];
+                b[n][1] = bn[n][1];
+            }
+        }
+    }
+}
+
+// one residual conv of the child: rows of radius rl, input window `in`, output
+// window `out` (or the head partials when HEADS), skip window (SKIP)
+template <int NM, bool SKIP, bool HEADS>
+__device__ __forceinline__ void child_layer(const Win& in, const Win& out, const Win& skw, int cr, int cc, int rl,
+                                            const float* __restrict__ W, int layer, int wave, int lane,
+                                            float* __restrict__ hpart) {
+    const int np = wave & 3, mg = wave >> 2;
+    const int li = lane & 15;
+    const Rows rows = make_rows(cr, cc, rl);
+    int ctr[NM];
+    int rowid[NM];
+#pragma unroll
+    for (int m = 0; m < NM; m++) {
+        int i = (mg * NM + m) * 16 + li;
+        rowid[m] = i;
+        if (i >= rows.n) i = 0;  // padding rows recompute row 0 (discarded)
+        const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+        ctr[m] = (pr - cr + in.r) * in.w + (pc - cc + in.r);
+    }
+    f32x4 acc[2][NM];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NM; m++) acc[n][m] = zero4();
+    win_conv<NM>(in, ctr, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, lane, acc);
+    const float* R = W + RES0 + layer * RES_STRIDE;
+    if (!HEADS) {
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+            const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                const int i = rowid[m];
+                if (i >= rows.n) continue;
+                const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+                f32x4 sk = zero4();
+                if (SKIP) {
+                    const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
+                    const h4 xh = *(const h4*)(skw.hi + sl);
+                    const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
+                }
+                h4 hi, lo;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
+                    if (SKIP) y += sk[r];
+                    y = y > 0.f ? y : 0.f;
+                    const _Float16 h = (_Float16)y;
+                    hi[r] = h;
+                    lo[r] = (_Float16)(y - (float)h);
+                }
+                const int o = out.off(ch0, (pr - cr + out.r) * out.w + (pc - cc + out.r));
+                *(h4*)(out.hi + o) = hi;
+                *(h4*)(out.hi + out.plane() + o) = lo;
+            }
+        }
+    } else {
+        // last residual layer: relu(acc*S + T + skip) reduced into the 1x1 head convs'
+        // per-wave partial sums, exactly as f16_store_heads (gz_pvnet.hip)
+        float s0[NM], s1[NM], sv[NM];
+#pragma unroll
+        for (int m = 0; m < NM; m++) s0[m] = s1[m] = sv[m] = 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+            const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
+            const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
+            const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+#pragma unroll
+            for (int m = 0; m < NM; m++) {
+                int i = rowid[m];
+                if (i >= rows.n) i = 0;
+                const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+                const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
+                const h4 xh = *(const h4*)(skw.hi + sl);
+                const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
+                    y = y > 0.f ? y : 0.f;
+                    s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
+                    s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
+                    sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            float a = s0[m], c = s1[m], v = sv[m];
+            a += __shfl_xor(a, 16);
+            c += __shfl_xor(c, 16);
+            v += __shfl_xor(v, 16);
+            a += __shfl_xor(a, 32);
+            c += __shfl_xor(c, 32);
+            v += __shfl_xor(v, 32);
+            const int i = rowid[m];
+            if (lane < 16 && i < rows.n) {
+                hpart[(np * 3 + 0) * HP_ROWS + i] = a;
+                hpart[(np * 3 + 1) * HP_ROWS + i] = c;
+                hpart[(np * 3 + 2) * HP_ROWS + i] = v;
+            }
+        }
+    }
+}
+
+__device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
+
+// list[0 .. *list_count): child leaves; meta[child] = its root's leaf index,
+// ord[root] = the root's map slot (maps written by pv_kernel_f16x3<true, true>);
+// hbuf: the per-board head-conv records (the root's is read, the child's written)
+__global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restrict__ W,
+                                                          const uint32_t* __restrict__ boards,
+                                                          const int32_t* __restrict__ meta,
+                                                          const int32_t* __restrict__ ord,
+                                                          const int32_t* __restrict__ list,
+                                                          const int32_t* __restrict__ list_count,
+                                                          const _Float16* __restrict__ maps, float* __restrict__ hbuf) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
+    const Win X0 = make_win(lds, OFF_X0, 3), Y1 = make_win(lds, OFF_Y1, 4);
+    const Win X1 = make_win(lds, OFF_X1, 5), Y2 = make_win(lds, OFF_Y2, 6);
+    float* hpart = (float*)(lds + OFF_HP);
+    _Float16* col = (_Float16*)(lds + OFF_COL);
+    const int count = *list_count;
+    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+        const int tid = threadIdx.x, lane = tid & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int b = __builtin_amdgcn_readfirstlane(list[it]);
+        const int rb = __builtin_amdgcn_readfirstlane(meta[b]);
+        const int o = __builtin_amdgcn_readfirstlane(ord[rb]);
+        // the child's stone: the one bit where its board and the root's differ
+        int cell = 0;
+        const uint32_t* cb = boards + (size_t)b * 16;
+        const uint32_t* rbd = boards + (size_t)rb * 16;
+        for (int k = 0; k < 16; k++) {
+            const uint32_t d = __builtin_amdgcn_readfirstlane(cb[k] ^ rbd[k]);
+            if (d) {
+                const int bit = (k & 7) * 32 + __builtin_ctz(d);
+                cell = (bit >> 4) * BN + (bit & 15);
+            }
+        }
+        const int cr = cell / BN, cc = cell % BN;
+        const _Float16* gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
+
+        // phase 0: the root's values around the recomputed windows; conv0's im2col
+        fill_window(X0, 1, gm, cr, cc, tid);
+        fill_window(Y1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
+        fill_window(X1, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
+        {
+            const Rows r0w = make_rows(cr, cc, 1);
+            const int row = tid >> 5, k = tid & 31;  // 16 rows x 32 k
+            _Float16 v = (_Float16)0.f;
+            if (row < r0w.n && k < 27) {
+                const int pr = r0w.r0 + row / r0w.wr, pc = r0w.c0 + row % r0w.wr;
+                const int tap = k / 3, cin = k % 3;
+                const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
+                if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
+                    const int bit = bit_of_board(rr, c2);
+                    const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+                    v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
+                }
+            }
+            col[row * 32 + k] = v;
+        }
+        __syncthreads();
+        // conv0 + BN + ReLU at the <= 9 positions around the stone (conv0_f16: wave = n-tile)
+        {
+            const Rows r0w = make_rows(cr, cc, 1);
+            const int li = lane & 15, q = lane >> 4, nt = wave;
+            const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
+            const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
+            const int ch0 = nt * 16 + 4 * q;
+            const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
+            const h8 a = *(const h8*)(col + li * 32 + 8 * q);
+            f32x4 acc = zero4();
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
+            if (li < r0w.n) {
+                const int pr = r0w.r0 + li / r0w.wr, pc = r0w.c0 + li % r0w.wr;
+                h4 hi, lo;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float y = __builtin_fmaf(acc[r], s[r], t[r]);
+                    y = y > 0.f ? y : 0.f;
+                    const _Float16 h = (_Float16)y;
+                    hi[r] = h;
+                    lo[r] = (_Float16)(y - (float)h);
+                }
+                const int off = X0.off(ch0, (pr - cr + 3) * 7 + (pc - cc + 3));
+                *(h4*)(X0.hi + off) = hi;
+                *(h4*)(X0.hi + X0.plane() + off) = lo;
+            }
+        }
+        __syncthreads();
+        child_layer<1, false, false>(X0, Y1, X0, cr, cc, 2, W, 0, wave, lane, hpart);  // y1
+        __syncthreads();
+        child_layer<2, true, false>(Y1, X1, X0, cr, cc, 3, W, 1, wave, lane, hpart);   // x1 = relu(.. + x0)
+        __syncthreads();
+        fill_window(Y2, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);  // X0 / Y1 are dead
+        child_layer<3, false, false>(X1, Y2, X1, cr, cc, 4, W, 2, wave, lane, hpart);  // y2
+        __syncthreads();
+        child_layer<4, true, true>(Y2, Y2, X1, cr, cc, 5, W, 3, wave, lane, hpart);    // x2 -> head convs
+        __syncthreads();
+        // the child's head-conv record: recomputed positions from hpart (bias first, then
+        // the 4 waves' partials in order, as the full kernel), the rest is the root's
+        {
+            const Rows r4 = make_rows(cr, cc, 5);
+            const float* hr = hbuf + (size_t)rb * HSTRIDE;
+            float* h = hbuf + (size_t)b * HSTRIDE;
+            for (int j = tid; j < HSTRIDE; j += NTC) {
+                float v = hr[j];
+                int pos = -1, which = 0;
+                if (j < POS) {
+                    pos = j;
+                } else if (j < 2 * POS) {
+                    pos = j - POS;
+                    which = 1;
+                } else if (j >= HV_OFF && j < HV_OFF + POS) {
+                    pos = j - HV_OFF;
+                    which = 2;
+                }
+                if (pos >= 0) {
+                    const int pr = pos / BN, pc = pos % BN;
+                    if (pr >= r4.r0 && pr < r4.r0 + r4.n / r4.wr && pc >= r4.c0 && pc < r4.c0 + r4.wr) {
+                        const int i = (pr - r4.r0) * r4.wr + (pc - r4.c0);
+                        float acc = which == 0 ? W[P_B] : (which == 1 ? W[P_B + 1] : W[V_B]);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) acc += hpart[(q * 3 + which) * HP_ROWS + i];
+                        v = acc;
+                    }
+                }
+                h[j] = v;
+            }
+        }
+        // no barrier: the next child writes X0 / Y1 / X1 (read before the last barrier)
+        // and hpart only after several more barriers
+    }
+}
+
+// one thread per leaf: roots (meta -1) take the next map slot (ord), others -1
+__global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
+                                  int root_cap, int32_t* __restrict__ ord, int32_t* __restrict__ ctr) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    int o = -1;
+    if (meta[i] == -1) {
+        o = atomicAdd(&ctr[0], 1);
+        if (o >= root_cap) o = -1;
+    }
+    ord[i] = o;
+}
+
+// lists: roots with a map slot (full forward + maps), children of such roots
+// (incremental), everything else (full forward)
+__global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
+                                  const int32_t* __restrict__ ord, int32_t* __restrict__ ctr,
+                                  int32_t* __restrict__ roots, int32_t* __restrict__ children,
+                                  int32_t* __restrict__ full) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int m = meta[i];
+    if (m == -1 && ord[i] >= 0) {
+        roots[atomicAdd(&ctr[1], 1)] = i;
+    } else if (m >= 0 && m < count && meta[m] == -1 && ord[m] >= 0) {
+        children[atomicAdd(&ctr[2], 1)] = i;
+    } else {
+        full[atomicAdd(&ctr[3], 1)] = i;
+    }
+}
+
+}  // namespace
+
+extern "C" void gz_internal_set_error(const char* msg);
+
+// Launches of the incremental forward's own kernels (called by gz_pv_forward_tree in
+// gz_pvnet.hip, which runs the full kernel on the root and full lists in between).
+extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
+                                         int32_t* d_ord, int32_t* d_ctr, int32_t* d_roots, int32_t* d_children,
+                                         int32_t* d_full, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess) {
+        gz_internal_set_error("gz_pv_forward_tree: memset");
+        return GZ_ERR_HIP;
+    }
+    const int g = (n + 255) / 256;
+    tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_ctr);
+    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_ctr, d_roots, d_children, d_full);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string("tree classify: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+
+extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
+                                         const int32_t* d_ord, const int32_t* d_children, const int32_t* d_nchildren,
+                                         const _Float16* d_maps, float* d_hbuf, int grid, void* stream) {
+    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(d_weights, d_boards, d_meta, d_ord, d_children, d_nchildren,
+                                                           d_maps, d_hbuf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string("pv_child_kernel: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}

@@ -50,6 +50,16 @@ constexpr int V1_P = PF_P + PF_KB * PF_NT * 256;
 constexpr int V1_KB = 15, V1_NT = 4;
 constexpr int TOTAL = V1_P + V1_KB * V1_NT * 256;
 
+// incremental forward (gz_pvinc.hip): a root board's intermediate maps x0, y1, x1,
+// y2 are stored in the LDS layout of the f16x3 kernel: hi plane [16 ch-groups]
+// [256 rows][8] then the lo plane -- PV_MAP_HALVES halves per map
+constexpr int PV_MAP_PLANE = CH * 256;
+constexpr int PV_MAP_HALVES = 2 * PV_MAP_PLANE;
+// per-board record of the 1x1 head convs' outputs between the tower and the FC heads
+// (gz_pvnet.hip / gz_pvinc.hip -> pv_heads_kernel): hp [0, 450) channel-major, zero to
+// HP_K; hv [HV_OFF, HV_OFF + 225), zero to HSTRIDE
+constexpr int HP_K = 464, HV_OFF = HP_K, HV_K = 240, HSTRIDE = HV_OFF + HV_K;
+
 // algorithmic work of one forward (neural_network.py:132-159), MACs
 constexpr long long MACS = 133690114LL;
 }  // namespace gzpv

@@ -154,10 +154,35 @@ __device__ __forceinline__ void f16_load(const ActF16x3& act, f32x4 (&out)[2][NM
     }
 }
 
+// f16_put4 that also stores the result to the global copy g of the map (the same
+// [hi plane][lo plane] layout as LDS) when g != nullptr: a root board's
+// intermediate maps for the incremental forward of its children (gz_pvinc.hip)
+template <bool SKIP>
+__device__ __forceinline__ void pv_put4(ActF16x3& act, const f32x4& acc, const f32x4& s, const f32x4& t,
+                                        const f32x4& skip, int ch0, int pos, _Float16* __restrict__ g) {
+    h4 hi, lo;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        float y = __builtin_fmaf(acc[r], s[r], t[r]);
+        if (SKIP) y += skip[r];
+        y = y > 0.f ? y : 0.f;
+        const _Float16 h = (_Float16)y;
+        hi[r] = h;
+        lo[r] = (_Float16)(y - (float)h);
+    }
+    const int o = ActF16x3::off(ch0, pos);
+    *(h4*)(act.hi + o) = hi;
+    *(h4*)(act.lo + o) = lo;
+    if (g) {
+        *(h4*)(g + o) = hi;
+        *(h4*)(g + PV_MAP_PLANE + o) = lo;
+    }
+}
+
 template <int NM, bool SKIP>
 __device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][NM], const float* __restrict__ S,
                                           const float* __restrict__ T, const f32x4 (&skip)[2][NM], int np, int m0,
-                                          int lane) {
+                                          int lane, _Float16* __restrict__ g) {
     asm volatile("" : "+v"(lane));  // addresses are recomputed per layer, not hoisted (and spilled)
     lane &= 63;
 #pragma unroll
@@ -167,7 +192,7 @@ __device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][N
 #pragma unroll
         for (int m = 0; m < NM; m++) {
             const int pos = (m0 + m) * 16 + (lane & 15);
-            if (pos < POS) f16_put4<SKIP>(act, acc[n][m], s, t, skip[n][m], ch0, pos);
+            if (pos < POS) pv_put4<SKIP>(act, acc[n][m], s, t, skip[n][m], ch0, pos, g);
         }
     }
 }
@@ -196,11 +221,11 @@ __device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const
         for (int m = 0; m < NM; m++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                float y = acc[n][m][r] * s[r] + t[r] + skip[n][m][r];
+                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + skip[n][m][r];
                 y = y > 0.f ? y : 0.f;
-                s0[m] += w0[r] * y;
-                s1[m] += w1[r] * y;
-                sv[m] += wv[r] * y;
+                s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
+                s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
+                sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
             }
     }
 #pragma unroll
@@ -221,9 +246,10 @@ __device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const
     }
 }
 
+// gmaps: nullptr, or the root's 4 map copies (x0, y1, x1, y2); y1, x1, y2 are stored here
 template <int NM, int m0>
 __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict__ W, int wave, int lane,
-                                          float* __restrict__ hpart) {
+                                          float* __restrict__ hpart, _Float16* __restrict__ gmaps) {
     const int np = wave & 3;
     for (int blk = 0; blk < 2; blk++) {
         f32x4 skip[2][NM];
@@ -244,9 +270,11 @@ __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict
             PV_WAVE_STAMP(16);
             PV_STAMP(3);
             if (half == 0)
-                f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+                f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane,
+                                     gmaps ? gmaps + (size_t)(1 + layer) * PV_MAP_HALVES : nullptr);
             else if (blk == 0)
-                f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane);
+                f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane,
+                                    gmaps ? gmaps + (size_t)2 * PV_MAP_HALVES : nullptr);
             else
                 f16_store_heads<NM>(acc, W, R + RES_S, R + RES_T, skip, np, m0, lane, hpart);
             __syncthreads();
@@ -284,7 +312,7 @@ __device__ __forceinline__ void build_im2col(_Float16* __restrict__ col, const f
 // fp16, so a*w = a*w_hi + a*w_lo (2 MFMAs, no a_lo term); K = 27 (k = tap*3 + cin)
 // padded to one 32-deep k-step.  Wave w: N tile w, all 15 M tiles.
 __device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict__ W, const _Float16* col, int nt,
-                                          int lane) {
+                                          int lane, _Float16* __restrict__ g) {
     const int li = lane & 15, q = lane >> 4;
     const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
     const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
@@ -300,7 +328,7 @@ __device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a[m], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a[m], acc, 0, 0, 0);
         const int pos = m * 16 + li;
-        if (pos < POS) f16_put4<false>(act, acc, s, t, none, ch0, pos);
+        if (pos < POS) pv_put4<false>(act, acc, s, t, none, ch0, pos, g);
     }
 }
 
@@ -317,7 +345,7 @@ __device__ __forceinline__ void store_tiles(Act& act, const f32x4 acc[MT], const
         for (int r = 0; r < 4; r++) {
             int pos = m * 16 + 4 * g + r;
             if (pos < POS) {
-                float y = acc[m][r] * s + t;
+                float y = __builtin_fmaf(acc[m][r], s, t);
                 if (skip) y += skip[m][r];
                 act.put(ch, pos, y > 0.f ? y : 0.f);
             }
@@ -559,30 +587,41 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
 // (one wave per SIMD with 512 registers and all 15 M tiles per wave measured 37%
 // slower: the compiler serialises the A-fragment reads of a single stream)
 constexpr int NT16 = 512;
-// per-board record of the 1x1 head convs' outputs between the tower and the FC heads:
-// hp [0, 450) channel-major, zero to HP_K; hv [HV_OFF, HV_OFF + 225), zero to HSTRIDE
-constexpr int HP_K = 464, HV_OFF = HP_K, HV_K = 240, HSTRIDE = HV_OFF + HV_K;
 #ifndef PV_SPLIT
 #define PV_SPLIT 8  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
 #endif
 #ifndef PV_YOUNG_TILES
 #define PV_YOUNG_TILES (15 - PV_SPLIT)
 #endif
+// list (optional): the boards to run, list[0 .. *list_count); ord / maps: the
+// root ordinal of every board (-1: none) and the root map area -- a board with
+// 0 <= ord < root_cap also stores its x0, y1, x1, y2 maps (gz_pvinc.hip)
+template <bool LIST, bool DUMP>
 __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restrict__ W,
                                                          const uint32_t* __restrict__ boards, int n,
-                                                         const int32_t* d_count, float* __restrict__ hbuf) {
+                                                         const int32_t* d_count, float* __restrict__ hbuf,
+                                                         const int32_t* __restrict__ list,
+                                                         const int32_t* __restrict__ list_count,
+                                                         const int32_t* __restrict__ ord,
+                                                         _Float16* __restrict__ maps, int root_cap) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const Smem sm = smem_layout(lds);
     ActF16x3 act;
     act.hi = (_Float16*)lds;
     act.lo = act.hi + CH * ROWS16;
-    const int count = board_count(n, d_count);
+    const int count = LIST ? *list_count : board_count(n, d_count);
     act.zero_slots(threadIdx.x, NT16, CH);
     for (int i = threadIdx.x; i < 3 * (ROWS - POS); i += NT16)
         sm.planes[(i / (ROWS - POS)) * ROWS + POS + i % (ROWS - POS)] = 0.f;
 
     PV_STAMP(30);  // start of the clock (slot 30 is not a phase)
-    for (int b = blockIdx.x; b < count; b += gridDim.x) {
+    for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
+        const int b = LIST ? list[li_] : li_;
+        _Float16* gm = nullptr;
+        if (DUMP) {
+            const int o = ord[b];
+            if (o >= 0 && o < root_cap) gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
+        }
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -593,13 +632,13 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         _Float16* col = (_Float16*)sm.hp;
         build_im2col<NT16>(col, sm.planes, tid);
         __syncthreads();
-        conv0_f16(act, W, col, wave, lane);
+        conv0_f16(act, W, col, wave, lane, gm);
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
-            f16_tower<PV_YOUNG_TILES, PV_SPLIT>(act, W, wave, lane, sm.hpart);
+            f16_tower<PV_YOUNG_TILES, PV_SPLIT>(act, W, wave, lane, sm.hpart, gm);
         else
-            f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart);
+            f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart, gm);
         int tid_h = threadIdx.x;  // re-read: a pinned tid kept live across the tower is spilled
         asm volatile("" : "+v"(tid_h));
         // the 1x1 head convs' outputs go to HBM; the FC heads run batched over boards
@@ -707,7 +746,7 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
     // value_fc2 + tanh: one thread per board
     if (tid < HB && b0 + tid < count) {
         float tot = 0.f;
-        for (int j = 0; j < 64; j++) tot += W[V2_W + j] * h1[tid * 64 + j];
+        for (int j = 0; j < 64; j++) tot = __builtin_fmaf(W[V2_W + j], h1[tid * 64 + j], tot);
         value[b0 + tid] = tanhf(tot + W[V2_B]);
     }
     // softmax: wave w handles boards w, w+4, ...; lane covers outputs lane + 64u
@@ -884,7 +923,8 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
                                             (float*)d_workspace);
     else
     {
-        pv_kernel_f16x3<<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace);
+        pv_kernel_f16x3<false, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace, nullptr,
+                                                     nullptr, nullptr, nullptr, 0);
         pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count,
                                                            d_logits, d_value, d_probs);
     }
@@ -892,6 +932,94 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_kernel: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+
+// ============================================================ incremental forward (gz_pvinc.hip)
+extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
+                                         int32_t* d_ord, int32_t* d_ctr, int32_t* d_roots, int32_t* d_children,
+                                         int32_t* d_full, void* stream);
+extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
+                                         const int32_t* d_ord, const int32_t* d_children, const int32_t* d_nchildren,
+                                         const _Float16* d_maps, float* d_hbuf, int grid, void* stream);
+
+namespace {
+constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct TreeWs {
+    float* hbuf;
+    int32_t *ord, *roots, *children, *full, *ctr;
+    _Float16* maps;
+};
+TreeWs tree_carve(void* ws, int32_t n) {
+    const size_t m = (size_t)(n < 1 ? 1 : n);
+    char* p = (char*)ws;
+    TreeWs t;
+    t.hbuf = (float*)p;
+    p += al256(m * HSTRIDE * sizeof(float));
+    t.ord = (int32_t*)p;
+    p += al256(m * 4);
+    t.roots = (int32_t*)p;
+    p += al256(m * 4);
+    t.children = (int32_t*)p;
+    p += al256(m * 4);
+    t.full = (int32_t*)p;
+    p += al256(m * 4);
+    t.ctr = (int32_t*)p;
+    p += 256;
+    t.maps = (_Float16*)p;
+    return t;
+}
+}  // namespace
+
+extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
+    const size_t m = (size_t)(n < 1 ? 1 : n);
+    return al256(m * HSTRIDE * sizeof(float)) + 4 * al256(m * 4) + 256 +
+           (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16);
+}
+
+extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
+                                  const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
+                                  float* d_probs, double* d_prior, void* d_workspace, void* stream) {
+    if (n < 0 || root_cap < 0 || (n > 0 && (!d_weights || !d_boards || !d_meta || !d_logits || !d_value || !d_workspace))) {
+        gz_internal_set_error("gz_pv_forward_tree: bad arguments");
+        return GZ_ERR_ARG;
+    }
+    if (d_prior && !d_probs) {
+        gz_internal_set_error("gz_pv_forward_tree: d_prior needs d_probs");
+        return GZ_ERR_ARG;
+    }
+    if (n == 0) return GZ_OK;
+    hipStream_t s = (hipStream_t)stream;
+    TreeWs t = tree_carve(d_workspace, n);
+    int rc = gz_internal_tree_classify(d_meta, n, d_count, root_cap, t.ord, t.ctr, t.roots, t.children, t.full, stream);
+    if (rc) return rc;
+    const int grid = pv_grid(n);
+    // roots (full forward, maps stored), then every board without a stored root (full
+    // forward), then the roots' children (incremental); ctr = [roots seen, #roots, #children, #full]
+    pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
+                                                     t.ord, t.maps, root_cap);
+    pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
+                                                      nullptr, nullptr, 0);
+    rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.children, t.ctr + 2, t.maps, t.hbuf, grid,
+                                   stream);
+    if (rc) return rc;
+    pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
+    if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string("gz_pv_forward_tree: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+
+// counts of the last tree forward's lists: [roots seen, roots with maps, children, full]
+extern "C" int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out4, void* stream) {
+    TreeWs t = tree_carve((void*)d_workspace, n);
+    if (hipMemcpyAsync(d_out4, t.ctr, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) {
+        gz_internal_set_error("gz_pv_tree_stats: copy");
         return GZ_ERR_HIP;
     }
     return GZ_OK;

@@ -123,7 +123,10 @@ __device__ __forceinline__ int mcts(RootShared* rs, int64_t game_id, const gz_se
     so.predicts = 1 + nonterm;  // root + every non-terminal child runs predict
     if (gather) {
         int bidx = leaf_reserve(sink, 1 + nonterm);
-        if (lane == 0) leaf_write(sink, bidx, lds_bb(rs->black), lds_bb(rs->white));
+        if (lane == 0) {
+            leaf_write(sink, bidx, lds_bb(rs->black), lds_bb(rs->white));
+            leaf_meta(sink, bidx, -1);
+        }
         int off = 1;
         for (int base = 1; base < n_par; base += WAVE) {
             int j = base + lane;
@@ -135,6 +138,7 @@ __device__ __forceinline__ int mcts(RootShared* rs, int64_t game_id, const gz_se
                 if (player == 1) bb_set(cbk, bit);
                 else bb_set(cwh, bit);
                 leaf_write(sink, bidx + off + rank_in(m), cbk, cwh);
+                leaf_meta(sink, bidx + off + rank_in(m), bidx);
             }
             off += __popcll(m);
         }
@@ -314,7 +318,10 @@ __device__ __forceinline__ int mcts(RootShared* rs, int64_t game_id, const gz_se
                     so.predicts++;
                     if (gather) {
                         int bidx = leaf_reserve(sink, 1);
-                        if (lane == 0) leaf_write(sink, bidx, cbk, cwh);
+                        if (lane == 0) {
+                            leaf_write(sink, bidx, cbk, cwh);
+                            leaf_meta(sink, bidx, -2);
+                        }
                     }
                 }
                 x = c;
@@ -881,7 +888,7 @@ int gz_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t
     if (gather && (!d_leaves || !d_leaf_count || leaf_cap < 0))
         return fail(GZ_ERR_ARG, "gz_search: leaf gathering needs d_leaves and d_leaf_count");
     if (n == 0) return GZ_OK;
-    LeafSink sink{d_leaves, leaf_cap, d_leaf_count};
+    LeafSink sink{d_leaves, leaf_cap, d_leaf_count, nullptr};
     size_t tb = tree_bytes_for(p->num_simulations);
     search_kernel<<<n, WAVE, smem_bytes(p->num_simulations), as_stream(stream)>>>(
         d_boards, d_game_ids, n, *p, (char*)d_trees, tb, d_moves, d_stats, sink, gather ? 1 : 0);
@@ -899,7 +906,7 @@ int gz_selfplay_init(void* d_slots, int32_t n_slots, int32_t num_simulations, in
 
 int gz_selfplay_run(void* d_slots, int32_t n_slots, const gz_search_params* p, int32_t n_plies,
                     gz_record* d_records, int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap,
-                    gz_selfplay_counters* d_counters, void* stream) {
+                    int32_t* d_leaf_meta, gz_selfplay_counters* d_counters, void* stream) {
     int rc = validate_params(p);
     if (rc) return rc;
     if (!d_slots || n_slots <= 0 || n_plies < 0 || !d_counters || !d_records || record_cap < 0)
@@ -907,7 +914,7 @@ int gz_selfplay_run(void* d_slots, int32_t n_slots, const gz_search_params* p, i
     bool gather = (p->flags & GZ_FLAG_GATHER_LEAVES) != 0;
     if (gather && (!d_leaves || leaf_cap < 0)) return fail(GZ_ERR_ARG, "gz_selfplay_run: leaf buffer missing");
     if (n_plies == 0) return GZ_OK;
-    LeafSink sink{d_leaves, leaf_cap, &d_counters->leaves};
+    LeafSink sink{d_leaves, leaf_cap, &d_counters->leaves, gather ? d_leaf_meta : nullptr};
     selfplay_kernel<<<n_slots, WAVE, smem_bytes(p->num_simulations), as_stream(stream)>>>(
         (char*)d_slots, n_slots, *p, n_plies, d_records, record_cap, sink, gather ? 1 : 0, d_counters);
     return check_launch("selfplay_kernel");

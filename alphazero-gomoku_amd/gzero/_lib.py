@@ -92,11 +92,14 @@ SIGNATURES = {
     "gz_search": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(SearchParams), _P, _P, _P, _P, _I32, _P, _P]),
     "gz_slot_bytes": (_SZ, [_I32]),
     "gz_selfplay_init": (ctypes.c_int, [_P, _I32, _I32, _I64, _I64, _P]),
-    "gz_selfplay_run": (ctypes.c_int, [_P, _I32, ctypes.POINTER(SearchParams), _I32, _P, _I32, _P, _I32, _P, _P]),
+    "gz_selfplay_run": (ctypes.c_int, [_P, _I32, ctypes.POINTER(SearchParams), _I32, _P, _I32, _P, _I32, _P, _P, _P]),
     "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "gz_pv_weight_floats": (_SZ, []),
     "gz_pv_workspace_bytes": (_SZ, [_I32]),
     "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
+    "gz_pv_tree_workspace_bytes": (_SZ, [_I32, _I32]),
+    "gz_pv_forward_tree": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _P]),
+    "gz_pv_tree_stats": (ctypes.c_int, [_P, _I32, _P, _P]),
     "gz_gn_weight_floats": (_SZ, []),
     "gz_gn_workspace_bytes": (_SZ, [_I32]),
     "gz_gn_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),

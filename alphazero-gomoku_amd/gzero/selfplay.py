@@ -26,9 +26,14 @@ COUNTER_DTYPE = np.dtype([("records", "<i4"), ("leaves", "<i4"), ("records_dropp
 class SelfPlayEngine:
     def __init__(self, n_slots=4096, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2,
                  seed=0, max_depth=100, pv_weights=None, plies_per_step=1, game_id_base=0,
-                 game_id_stride=None, planner_steps=0, planner_difficulty="medium", gn_weights=None):
+                 game_id_stride=None, planner_steps=0, planner_difficulty="medium", gn_weights=None,
+                 pv_mode="full"):
         """planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
-        planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights."""
+        planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights.
+        pv_mode: "full" = one full forward per node (gz_pv_forward); "tree" = the
+        incremental forward (gz_pv_forward_tree: a root's children recompute only
+        the windows around their new stone; bit-identical outputs; f16x3 and
+        planner_steps == 0 only)."""
         self.lib = require_gpu()
         self.n_slots = int(n_slots)
         self.plies_per_step = int(plies_per_step)
@@ -45,6 +50,11 @@ class SelfPlayEngine:
                                          dtype=torch.uint8, device="cuda")
         self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
             else PVWeights(pv_weights)
+        if pv_mode not in ("full", "tree"):
+            raise ValueError(f"pv_mode must be 'full' or 'tree', not {pv_mode!r}")
+        self.tree = pv_mode == "tree" and self.gather
+        if self.tree and (self.planner_steps or self.pv_weights.mode != _lib.GZ_PV_F16X3):
+            raise ValueError("pv_mode='tree' needs f16x3 weights and planner_steps == 0")
         S = self.params.num_simulations
         slot_bytes = self.lib.gz_slot_bytes(S)
         self.d_slots = torch.zeros(self.n_slots * slot_bytes, dtype=torch.uint8, device="cuda")
@@ -62,6 +72,12 @@ class SelfPlayEngine:
             self.d_prior = torch.empty(self.leaf_cap * 225, dtype=torch.float64, device="cuda")
         else:
             self.d_leaves = self.d_logits = self.d_value = self.d_probs = self.d_prior = None
+        self.d_meta = self.d_tree_ws = None
+        if self.tree:
+            self.d_meta = torch.empty(self.leaf_cap, dtype=torch.int32, device="cuda")
+            self.root_cap = self.n_slots * self.plies_per_step  # one root per slot per ply
+            self.d_tree_ws = torch.empty(self.lib.gz_pv_tree_workspace_bytes(self.leaf_cap, self.root_cap),
+                                         dtype=torch.uint8, device="cuda")
         base = int(game_id_base)
         stride = self.n_slots if game_id_stride is None else int(game_id_stride)
         _lib.check(self.lib.gz_selfplay_init(ptr(self.d_slots), self.n_slots, S, base, stride, stream()),
@@ -82,7 +98,8 @@ class SelfPlayEngine:
             return
         _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
-                                            self.leaf_cap, ptr(self.d_counters), stream()), "gz_selfplay_run")
+                                            self.leaf_cap, ptr(self.d_meta), ptr(self.d_counters), stream()),
+                   "gz_selfplay_run")
 
     def advance(self, n_plies):
         """Play n_plies plies on every slot without gathering leaves for the PV forward
@@ -98,13 +115,19 @@ class SelfPlayEngine:
         for _ in range(int(n_plies)):
             self.d_counters.zero_()
             _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(p), 1,
-                                                ptr(self.d_records), self.record_cap, None, 0,
+                                                ptr(self.d_records), self.record_cap, None, 0, None,
                                                 ptr(self.d_counters), stream()), "gz_selfplay_run")
 
     def launch_pv(self):
         if not self.gather:
             return
         d_count = self.d_counters[4:8]  # counters.leaves
+        if self.tree:
+            _lib.check(self.lib.gz_pv_forward_tree(ptr(self.pv_weights.tensor), ptr(self.d_leaves), ptr(self.d_meta),
+                                                   self.leaf_cap, ptr(d_count), self.root_cap, ptr(self.d_logits),
+                                                   ptr(self.d_value), ptr(self.d_probs), ptr(self.d_prior),
+                                                   ptr(self.d_tree_ws), stream()), "gz_pv_forward_tree")
+            return
         _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
                                           ptr(d_count), ptr(self.d_logits), ptr(self.d_value),
                                           ptr(self.d_probs), ptr(self.d_prior),
@@ -114,6 +137,14 @@ class SelfPlayEngine:
     def step(self, n_plies=None):
         self.launch_search(n_plies)
         self.launch_pv()
+
+    def tree_stats(self):
+        """List sizes of the last tree forward: roots seen, roots with maps,
+        incremental children, full-forward boards (synchronising)."""
+        out = torch.zeros(4, dtype=torch.int32, device="cuda")
+        _lib.check(self.lib.gz_pv_tree_stats(ptr(self.d_tree_ws), self.leaf_cap, ptr(out), stream()),
+                   "gz_pv_tree_stats")
+        return [int(x) for x in out.cpu()]
 
     # ---- host views (synchronising)
     def counters(self):

@@ -256,6 +256,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--pv-precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="policy-value forward: 3-term fp16 split (f32 accumulate) or exact fp32 MFMA")
+    ap.add_argument("--pv-mode", default="full", choices=["full", "tree"],
+                    help="full: one full forward per node; tree: the incremental forward of a root's children "
+                         "(gz_pv_forward_tree, bit-identical outputs)")
     ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
     ap.add_argument("--elided-plies", type=int, default=20)
     ap.add_argument("--no-elided", action="store_true")
@@ -297,13 +300,15 @@ def main():
         from gzero import planner_nets
         gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
 
-    def engine(beta, planner_steps, pv):
+    def engine(beta, planner_steps, pv, mode="full"):
         return SelfPlayEngine(n_slots=args.slots, num_simulations=args.sims, c_puct=1.6, exploration=0.05,
                               beta=beta, seed=args.seed, pv_weights=pv, plies_per_step=P,
                               game_id_base=base, game_id_stride=stride, planner_steps=planner_steps,
-                              planner_difficulty="medium", gn_weights=gnw if planner_steps else None)
+                              planner_difficulty="medium", gn_weights=gnw if planner_steps else None,
+                              pv_mode=mode)
 
-    eng = engine(args.beta, args.planner_steps, w)
+    eng = engine(args.beta, args.planner_steps, w,
+                 args.pv_mode if (args.pv_precision == "f16x3" and not args.planner_steps) else "full")
     # N > 1: the per-step RCCL all-gather of finished games' (s, pi, z) records,
     # fixed-size and sync-free (gzero.dist.RecordExchange: counts stay on the device)
     ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda") if ws > 1 else None
