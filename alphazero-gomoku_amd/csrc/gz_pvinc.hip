@@ -40,6 +40,29 @@ namespace {
 using namespace gzc;
 
 constexpr int NTC = 512;
+
+// Phase stamps (tools/pvinc_stamps.py only): -DGZ_PVINC_STAMPS accumulates s_memtime
+// deltas of workgroup 0 / wave 0 per phase (vector atomics); compiled out otherwise.
+#ifdef GZ_PVINC_STAMPS
+__device__ unsigned long long gz_pvinc_stamps[16];
+__device__ unsigned long long gz_pvinc_stamps_n;
+#define PI_T0() unsigned long long pit_ = __builtin_amdgcn_s_memtime()
+#define PI_STAMP(i)                                                                   \
+    do {                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            atomicAdd(&gz_pvinc_stamps[i], t_ - pit_);                                \
+            pit_ = t_;                                                                \
+        }                                                                             \
+    } while (0)
+#else
+#define PI_T0() \
+    do {        \
+    } while (0)
+#define PI_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
 constexpr int P_X0 = 49, P_Y1 = 81, P_X1 = 121, P_Y2 = 169;
 constexpr int wbytes(int P) { return 2 * 16 * P * 16; }  // hi + lo planes
 constexpr int OFF_X1 = 0;
@@ -72,22 +95,61 @@ __device__ inline Win make_win(char* lds, int off, int r) {
 }
 
 // root's values (global map, full kernel layout [plane][16 cg][256][8]) into the
-// window, except the recomputed square of radius rc; zeros off the board
-__device__ inline void fill_window(const Win& x, int rc, const _Float16* __restrict__ gm, int cr, int cc, int tid) {
+// window, except the recomputed square of radius rc; zeros off the board.  Split in
+// a load half (every item of the thread issued at once, into registers) and a
+// store half, so a fill costs one memory latency, not one per item.
+template <int IT>
+struct FillBuf {
+    uint4 v[IT];
+    uint32_t skip;  // bit k: item k is not stored (recomputed there, or past the window)
+};
+
+// window item i -> (plane, cg, loc); board position; whether the fill writes it
+__device__ __forceinline__ bool fill_item(const Win& x, int rc, int cr, int cc, int i, int& plane, int& cg, int& loc,
+                                          int& pr, int& pc, bool& on) {
+    plane = i / (16 * x.P);
+    const int rem = i - plane * 16 * x.P;
+    cg = rem / x.P;
+    loc = rem - cg * x.P;
+    pr = cr - x.r + loc / x.w;
+    pc = cc - x.r + loc % x.w;
+    on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+    const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
+    return !(on && dr <= rc && dc <= rc);  // else written by the layer that recomputes it
+}
+
+template <int IT>
+__device__ __forceinline__ void fill_load(FillBuf<IT>& f, const Win& x, int rc, const _Float16* __restrict__ gm,
+                                          int cr, int cc, int tid) {
     const int n = 2 * 16 * x.P;
-    for (int i = tid; i < n; i += NTC) {
-        const int plane = i / (16 * x.P);
-        const int rem = i - plane * 16 * x.P;
-        const int cg = rem / x.P, loc = rem - cg * x.P;
-        const int pr = cr - x.r + loc / x.w, pc = cc - x.r + loc % x.w;
-        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
-        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-        if (on && dr <= rc && dc <= rc) continue;  // written by the layer that recomputes it
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (on) v = *(const uint4*)(gm + plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8);
-        *(uint4*)(x.hi + plane * x.plane() + (cg * x.P + loc) * 8) = v;
+    f.skip = 0;
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const int i = tid + k * NTC;
+        f.v[k] = make_uint4(0u, 0u, 0u, 0u);
+        int plane, cg, loc, pr, pc;
+        bool on;
+        if (i < n && fill_item(x, rc, cr, cc, i, plane, cg, loc, pr, pc, on)) {
+            if (on) f.v[k] = *(const uint4*)(gm + plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8);
+        } else {
+            f.skip |= 1u << k;
+        }
     }
 }
+
+template <int IT>
+__device__ __forceinline__ void fill_store(const FillBuf<IT>& f, const Win& x, int tid) {
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        if (f.skip & (1u << k)) continue;
+        const int i = tid + k * NTC;
+        const int plane = i / (16 * x.P);
+        const int rem = i - plane * 16 * x.P;
+        *(uint4*)(x.hi + plane * x.plane() + rem * 8) = f.v[k];  // rem = cg * P + loc
+    }
+}
+
+constexpr int fill_items(int P) { return (2 * 16 * P + NTC - 1) / NTC; }
 
 // the recomputed rows of one layer: the square of radius rl around (cr, cc),
 // clipped, row-major
@@ -106,198 +168,259 @@ __device__ inline Rows make_rows(int cr, int cc, int rl) {
 }
 
 // implicit-GEMM 3x3 conv of the window `in` at the positions ctr[m] (window-local
-// index of the output position, per lane), the wave's n-tiles {2np, 2np+1}: the
-// k-steps, products and their order are those of f16_conv (gz_f16conv.h).
-template <int NM>
-__device__ __forceinline__ void win_conv(const Win& in, const int (&ctr)[NM], const _Float16* __restrict__ Wf, int np,
-                                         int lane, f32x4 (&acc)[2][NM]) {
+// index of the output position, per lane) for the wave's NTW n-tiles nt0.. and its
+// first nt (runtime, <= NMAX) M tiles: the k-steps, products and their order per
+// accumulator are those of f16_conv (gz_f16conv.h).  The weight fragments of the
+// next 4 k-steps are in flight (ring slot = cq, so the indexing stays static).
+template <int NTW, int NT, int NMAX>
+__device__ __forceinline__ void win_conv_nt(const Win& in, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
+                                            int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
     constexpr int CQ = 4, KS = 9 * CQ;
     constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
-    const int wo = ((2 * np) * 64 + lane) * 16;
+    const int wo = (nt0 * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     const _Float16* lo_plane = in.hi + in.plane();
-    h8 b[2][2];
+    // weight ring: 4 k-steps in flight for one n-tile, 2 for two (their k-steps are
+    // twice as long); slot = cq % RING keeps the indexing static
+    constexpr int RING = NTW == 1 ? 4 : 2;
+    h8 b[RING][NTW][2];
 #pragma unroll
-    for (int n = 0; n < 2; n++) {
-        b[n][0] = wload(0, n, 0);
-        b[n][1] = wload(0, n, 1);
-    }
+    for (int c = 0; c < RING; c++)
+#pragma unroll
+        for (int n = 0; n < NTW; n++) {
+            b[c][n][0] = wload(c, n, 0);
+            b[c][n][1] = wload(c, n, 1);
+        }
+#pragma unroll 1
     for (int tap = 0; tap < 9; tap++) {
         const int toff = (tap / 3 - 1) * in.w + (tap % 3 - 1);
-        int nb[NM];
+        int nb[NT];
 #pragma unroll
-        for (int m = 0; m < NM; m++) nb[m] = (ctr[m] + toff + q * in.P) * 8;
+        for (int m = 0; m < NT; m++) nb[m] = (ctr[m] + toff + q * in.P) * 8;
 #pragma unroll
         for (int cq = 0; cq < CQ; cq++) {
-            const int ks = tap * CQ + cq;
             const int ao = cq * 4 * in.P * 8;
-            h8 ah[NM], al[NM];
+            h8 ah[NT], al[NT];
 #pragma unroll
-            for (int m = 0; m < NM; m++) {
+            for (int m = 0; m < NT; m++) {
                 ah[m] = *(const h8*)(in.hi + ao + nb[m]);
                 al[m] = *(const h8*)(lo_plane + ao + nb[m]);
             }
-            h8 bn[2][2];
-            const int ks1 = ks + 1 < KS ? ks + 1 : 0;
+            const int sl = cq % RING;  // static once the cq loop is unrolled
 #pragma unroll
-            for (int n = 0; n < 2; n++) {
-                bn[n][0] = wload(ks1, n, 0);
-                bn[n][1] = wload(ks1, n, 1);
+            for (int m = 0; m < NT; m++) {
+#pragma unroll
+                for (int n = 0; n < NTW; n++)
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NTW; n++)
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[m], acc[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NTW; n++)
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[m], acc[n][m], 0, 0, 0);
             }
+            // refill this slot with k-step ks + RING (past the end: the first k-steps again, unused)
+            const int ksr = tap * CQ + cq + RING;
+            const int kn = ksr < KS ? ksr : ksr - KS;
 #pragma unroll
-            for (int m = 0; m < NM; m++) {
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][1], ah[m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[n][0], al[m], acc[n][m], 0, 0, 0);
-            }
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                b[n][0] = bn[n][0];
-                b[n][1] = bn[n][1];
+            for (int n = 0; n < NTW; n++) {
+                b[sl][n][0] = wload(kn, n, 0);
+                b[sl][n][1] = wload(kn, n, 1);
             }
         }
     }
 }
 
-// one residual conv of the child: rows of radius rl, input window `in`, output
-// window `out` (or the head partials when HEADS), skip window (SKIP)
-template <int NM, bool SKIP, bool HEADS>
-__device__ __forceinline__ void child_layer(const Win& in, const Win& out, const Win& skw, int cr, int cc, int rl,
-                                            const float* __restrict__ W, int layer, int wave, int lane,
-                                            float* __restrict__ hpart) {
-    const int np = wave & 3, mg = wave >> 2;
-    const int li = lane & 15;
-    const Rows rows = make_rows(cr, cc, rl);
-    int ctr[NM];
-    int rowid[NM];
-#pragma unroll
-    for (int m = 0; m < NM; m++) {
-        int i = (mg * NM + m) * 16 + li;
-        rowid[m] = i;
-        if (i >= rows.n) i = 0;  // padding rows recompute row 0 (discarded)
-        const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
-        ctr[m] = (pr - cr + in.r) * in.w + (pc - cc + in.r);
+// win_conv_nt for the runtime tile count nt (1 <= nt <= NMAX): one branch per
+// layer, none inside the k-loop (a guard per tile there splits the loop into
+// basic blocks and the compiler then waits for every load at each boundary)
+template <int NTW, int NMAX>
+__device__ __forceinline__ void win_conv(const Win& in, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
+                                         int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
+    static_assert(NMAX >= 1 && NMAX <= 6, "tile counts");
+    switch (nt) {
+        case 1: win_conv_nt<NTW, 1, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 2: if constexpr (NMAX >= 2) win_conv_nt<NTW, 2, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 3: if constexpr (NMAX >= 3) win_conv_nt<NTW, 3, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 4: if constexpr (NMAX >= 4) win_conv_nt<NTW, 4, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 5: if constexpr (NMAX >= 5) win_conv_nt<NTW, 5, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 6: if constexpr (NMAX >= 6) win_conv_nt<NTW, 6, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        default: break;
     }
-    f32x4 acc[2][NM];
+}
+
+// epilogue of a map layer: y = relu(acc*S + T (+ skip)) at the wave's rows into the
+// output window, hi/lo split (f16_put4)
+template <int NTW, int NMAX, bool SKIP>
+__device__ __forceinline__ void child_store(const f32x4 (&acc)[NTW][NMAX], const Rows& rows, int t0, int nt,
+                                            const Win& out, const Win& skw, int cr, int cc, const float* __restrict__ R,
+                                            int nt0, int lane) {
+    const int li = lane & 15;
 #pragma unroll
-    for (int n = 0; n < 2; n++)
+    for (int n = 0; n < NTW; n++) {
+        const int ch0 = (nt0 + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
 #pragma unroll
-        for (int m = 0; m < NM; m++) acc[n][m] = zero4();
-    win_conv<NM>(in, ctr, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), np, lane, acc);
-    const float* R = W + RES0 + layer * RES_STRIDE;
-    if (!HEADS) {
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-            const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-                const int i = rowid[m];
-                if (i >= rows.n) continue;
-                const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
-                f32x4 sk = zero4();
-                if (SKIP) {
-                    const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
-                    const h4 xh = *(const h4*)(skw.hi + sl);
-                    const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
-                }
-                h4 hi, lo;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
-                    if (SKIP) y += sk[r];
-                    y = y > 0.f ? y : 0.f;
-                    const _Float16 h = (_Float16)y;
-                    hi[r] = h;
-                    lo[r] = (_Float16)(y - (float)h);
-                }
-                const int o = out.off(ch0, (pr - cr + out.r) * out.w + (pc - cc + out.r));
-                *(h4*)(out.hi + o) = hi;
-                *(h4*)(out.hi + out.plane() + o) = lo;
-            }
-        }
-    } else {
-        // last residual layer: relu(acc*S + T + skip) reduced into the 1x1 head convs'
-        // per-wave partial sums, exactly as f16_store_heads (gz_pvnet.hip)
-        float s0[NM], s1[NM], sv[NM];
-#pragma unroll
-        for (int m = 0; m < NM; m++) s0[m] = s1[m] = sv[m] = 0.f;
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-            const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
-            const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
-            const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
-#pragma unroll
-            for (int m = 0; m < NM; m++) {
-                int i = rowid[m];
-                if (i >= rows.n) i = 0;
-                const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+        for (int m = 0; m < NMAX; m++) {
+            const int i = (t0 + m) * 16 + li;
+            if (m >= nt || i >= rows.n) continue;
+            const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+            f32x4 sk = zero4();
+            if (SKIP) {
                 const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
                 const h4 xh = *(const h4*)(skw.hi + sl);
                 const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
-                    y = y > 0.f ? y : 0.f;
-                    s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
-                    s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
-                    sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
-                }
+                for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
+            }
+            h4 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
+                if (SKIP) y += sk[r];
+                y = y > 0.f ? y : 0.f;
+                const _Float16 h = (_Float16)y;
+                hi[r] = h;
+                lo[r] = (_Float16)(y - (float)h);
+            }
+            const int o = out.off(ch0, (pr - cr + out.r) * out.w + (pc - cc + out.r));
+            *(h4*)(out.hi + o) = hi;
+            *(h4*)(out.hi + out.plane() + o) = lo;
+        }
+    }
+}
+
+template <int NMAX>
+__device__ __forceinline__ void tile_centres(const Win& in, const Rows& rows, int t0, int cr, int cc, int lane,
+                                             int (&ctr)[NMAX]) {
+    const int li = lane & 15;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        int i = (t0 + m) * 16 + li;
+        if (i >= rows.n) i = 0;  // padding rows recompute row 0 (discarded)
+        const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+        ctr[m] = (pr - cr + in.r) * in.w + (pc - cc + in.r);
+    }
+}
+
+// a map layer (y1, x1, y2): wave w = n-tile w over all the layer's M tiles, so every
+// weight fragment is read once per child and feeds 3 x (tiles) MFMAs
+template <int NMAX, bool SKIP>
+__device__ __forceinline__ void child_map_layer(const Win& in, const Win& out, const Win& skw, int cr, int cc, int rl,
+                                                const float* __restrict__ W, int layer, int wave, int lane) {
+    const Rows rows = make_rows(cr, cc, rl);
+    const int nt = (rows.n + 15) >> 4;
+    int ctr[NMAX];
+    tile_centres<NMAX>(in, rows, 0, cr, cc, lane, ctr);
+    f32x4 acc[1][NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) acc[0][m] = zero4();
+    win_conv<1, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), wave, lane, acc);
+    child_store<1, NMAX, SKIP>(acc, rows, 0, nt, out, skw, cr, cc, W + RES0 + layer * RES_STRIDE, wave, lane);
+}
+
+// the last residual layer (x2): the 1x1 head convs' partial sums need a wave's
+// 32 channels (n-tiles 2np, 2np+1) in one fma chain per lane (f16_store_heads), so
+// here wave = (n-tile pair np, M half); the M tiles are split evenly
+template <int NMAX>
+__device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, int cr, int cc,
+                                                 const float* __restrict__ W, int wave, int lane,
+                                                 float* __restrict__ hpart) {
+    constexpr int layer = 3;
+    const int np = wave & 3, mg = wave >> 2;
+    const Rows rows = make_rows(cr, cc, 5);
+    const int T = (rows.n + 15) >> 4;
+    const int T0 = (T + 1) >> 1;
+    const int t0 = mg ? T0 : 0, nt = mg ? T - T0 : T0;
+    int ctr[NMAX];
+    tile_centres<NMAX>(in, rows, t0, cr, cc, lane, ctr);
+    f32x4 acc[2][NMAX];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    win_conv<2, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
+    const float* R = W + RES0 + layer * RES_STRIDE;
+    const int li = lane & 15;
+    float s0[NMAX], s1[NMAX], sv[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
+        const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
+        const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            if (m >= nt) continue;
+            int i = (t0 + m) * 16 + li;
+            if (i >= rows.n) i = 0;
+            const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+            const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
+            const h4 xh = *(const h4*)(skw.hi + sl);
+            const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
+                y = y > 0.f ? y : 0.f;
+                s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
+                s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
+                sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
             }
         }
+    }
 #pragma unroll
-        for (int m = 0; m < NM; m++) {
-            float a = s0[m], c = s1[m], v = sv[m];
-            a += __shfl_xor(a, 16);
-            c += __shfl_xor(c, 16);
-            v += __shfl_xor(v, 16);
-            a += __shfl_xor(a, 32);
-            c += __shfl_xor(c, 32);
-            v += __shfl_xor(v, 32);
-            const int i = rowid[m];
-            if (lane < 16 && i < rows.n) {
-                hpart[(np * 3 + 0) * HP_ROWS + i] = a;
-                hpart[(np * 3 + 1) * HP_ROWS + i] = c;
-                hpart[(np * 3 + 2) * HP_ROWS + i] = v;
-            }
+    for (int m = 0; m < NMAX; m++) {
+        if (m >= nt) continue;
+        float a = s0[m], c = s1[m], v = sv[m];
+        a += __shfl_xor(a, 16);
+        c += __shfl_xor(c, 16);
+        v += __shfl_xor(v, 16);
+        a += __shfl_xor(a, 32);
+        c += __shfl_xor(c, 32);
+        v += __shfl_xor(v, 32);
+        const int i = (t0 + m) * 16 + li;
+        if (lane < 16 && i < rows.n) {
+            hpart[(np * 3 + 0) * HP_ROWS + i] = a;
+            hpart[(np * 3 + 1) * HP_ROWS + i] = c;
+            hpart[(np * 3 + 2) * HP_ROWS + i] = v;
         }
     }
 }
 
 __device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
 
-// list[0 .. *list_count): child leaves; meta[child] = its root's leaf index,
-// ord[root] = the root's map slot (maps written by pv_kernel_f16x3<true, true>);
-// hbuf: the per-board head-conv records (the root's is read, the child's written)
+// Children are processed in leaf order, each workgroup a contiguous chunk of the
+// leaf buffer: a root's children (stored right after it by the search) stay on one
+// CU, so the root's maps are read from that XCD's L2 after the first child.  A leaf
+// is a child here iff meta >= 0 and its root got a map slot (ord >= 0).
 __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restrict__ W,
                                                           const uint32_t* __restrict__ boards,
                                                           const int32_t* __restrict__ meta,
-                                                          const int32_t* __restrict__ ord,
-                                                          const int32_t* __restrict__ list,
-                                                          const int32_t* __restrict__ list_count,
+                                                          const int32_t* __restrict__ ord, int n,
+                                                          const int32_t* __restrict__ d_count,
                                                           const _Float16* __restrict__ maps, float* __restrict__ hbuf) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_C];
     const Win X0 = make_win(lds, OFF_X0, 3), Y1 = make_win(lds, OFF_Y1, 4);
     const Win X1 = make_win(lds, OFF_X1, 5), Y2 = make_win(lds, OFF_Y2, 6);
     float* hpart = (float*)(lds + OFF_HP);
     _Float16* col = (_Float16*)(lds + OFF_COL);
-    const int count = *list_count;
-    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int chunk = (count + gridDim.x - 1) / gridDim.x;
+    const int beg = blockIdx.x * chunk, end = beg + chunk < count ? beg + chunk : count;
+    for (int b = beg; b < end; b++) {
+        PI_T0();
+        const int rb = __builtin_amdgcn_readfirstlane(meta[b]);
+        if (rb < 0) continue;
+        const int o = __builtin_amdgcn_readfirstlane(ord[rb]);
+        if (o < 0) continue;
         const int tid = threadIdx.x, lane = tid & 63;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int b = __builtin_amdgcn_readfirstlane(list[it]);
-        const int rb = __builtin_amdgcn_readfirstlane(meta[b]);
-        const int o = __builtin_amdgcn_readfirstlane(ord[rb]);
         // the child's stone: the one bit where its board and the root's differ
         int cell = 0;
         const uint32_t* cb = boards + (size_t)b * 16;
@@ -311,11 +434,20 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
         }
         const int cr = cell / BN, cc = cell % BN;
         const _Float16* gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
+        PI_STAMP(0);
 
         // phase 0: the root's values around the recomputed windows; conv0's im2col
-        fill_window(X0, 1, gm, cr, cc, tid);
-        fill_window(Y1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
-        fill_window(X1, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
+        {
+            FillBuf<fill_items(P_X0)> f0;
+            FillBuf<fill_items(P_Y1)> f1;
+            FillBuf<fill_items(P_X1)> f2;
+            fill_load(f0, X0, 1, gm, cr, cc, tid);
+            fill_load(f1, Y1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
+            fill_load(f2, X1, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
+            fill_store(f0, X0, tid);
+            fill_store(f1, Y1, tid);
+            fill_store(f2, X1, tid);
+        }
         {
             const Rows r0w = make_rows(cr, cc, 1);
             const int row = tid >> 5, k = tid & 31;  // 16 rows x 32 k
@@ -333,6 +465,7 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
             col[row * 32 + k] = v;
         }
         __syncthreads();
+        PI_STAMP(1);
         // conv0 + BN + ReLU at the <= 9 positions around the stone (conv0_f16: wave = n-tile)
         {
             const Rows r0w = make_rows(cr, cc, 1);
@@ -362,15 +495,25 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
             }
         }
         __syncthreads();
-        child_layer<1, false, false>(X0, Y1, X0, cr, cc, 2, W, 0, wave, lane, hpart);  // y1
+        PI_STAMP(2);
+        child_map_layer<2, false>(X0, Y1, X0, cr, cc, 2, W, 0, wave, lane);  // y1
         __syncthreads();
-        child_layer<2, true, false>(Y1, X1, X0, cr, cc, 3, W, 1, wave, lane, hpart);   // x1 = relu(.. + x0)
+        PI_STAMP(3);
+        child_map_layer<4, true>(Y1, X1, X0, cr, cc, 3, W, 1, wave, lane);   // x1 = relu(.. + x0)
         __syncthreads();
-        fill_window(Y2, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);  // X0 / Y1 are dead
-        child_layer<3, false, false>(X1, Y2, X1, cr, cc, 4, W, 2, wave, lane, hpart);  // y2
+        PI_STAMP(4);
+        {
+            FillBuf<fill_items(P_Y2)> f3;  // X0 / Y1 are dead
+            fill_load(f3, Y2, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);
+            fill_store(f3, Y2, tid);
+        }
+        PI_STAMP(5);
+        child_map_layer<6, false>(X1, Y2, X1, cr, cc, 4, W, 2, wave, lane);  // y2
         __syncthreads();
-        child_layer<4, true, true>(Y2, Y2, X1, cr, cc, 5, W, 3, wave, lane, hpart);    // x2 -> head convs
+        PI_STAMP(6);
+        child_head_layer<4>(Y2, X1, cr, cc, W, wave, lane, hpart);  // x2 -> head convs
         __syncthreads();
+        PI_STAMP(7);
         // the child's head-conv record: recomputed positions from hpart (bias first, then
         // the 4 waves' partials in order, as the full kernel), the rest is the root's
         {
@@ -402,6 +545,10 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
                 h[j] = v;
             }
         }
+        PI_STAMP(8);
+#ifdef GZ_PVINC_STAMPS
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, 1ull);
+#endif
         // no barrier: the next child writes X0 / Y1 / X1 (read before the last barrier)
         // and hpart only after several more barriers
     }
@@ -421,23 +568,32 @@ __global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const
     ord[i] = o;
 }
 
-// lists: roots with a map slot (full forward + maps), children of such roots
-// (incremental), everything else (full forward)
+// lists: roots with a map slot (full forward + maps) and every board that is not
+// the child of such a root (full forward); one atomic per wave and list
+__device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list) {
+    const uint64_t m = __ballot(take);
+    if (!m) return;
+    int base = 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    if (lane == leader) base = atomicAdd(ctr, __popcll(m));
+    base = __shfl(base, leader);
+    if (take) list[base + __popcll(m & ((1ull << lane) - 1))] = i;
+}
+
 __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
                                   const int32_t* __restrict__ ord, int32_t* __restrict__ ctr,
-                                  int32_t* __restrict__ roots, int32_t* __restrict__ children,
-                                  int32_t* __restrict__ full) {
+                                  int32_t* __restrict__ roots, int32_t* __restrict__ full) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const int m = meta[i];
-    if (m == -1 && ord[i] >= 0) {
-        roots[atomicAdd(&ctr[1], 1)] = i;
-    } else if (m >= 0 && m < count && meta[m] == -1 && ord[m] >= 0) {
-        children[atomicAdd(&ctr[2], 1)] = i;
-    } else {
-        full[atomicAdd(&ctr[3], 1)] = i;
-    }
+    const bool valid = i < count;
+    const int m = valid ? meta[i] : -3;
+    const bool root = valid && m == -1 && ord[i] >= 0;
+    const bool child = valid && m >= 0 && m < count && meta[m] == -1 && ord[m] >= 0;
+    wave_append(root, i, ctr + 1, roots);
+    wave_append(valid && !root && !child, i, ctr + 3, full);
+    const uint64_t c = __ballot(child);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
 }
 
 }  // namespace
@@ -456,7 +612,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     }
     const int g = (n + 255) / 256;
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_ctr);
-    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_ctr, d_roots, d_children, d_full);
+    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_ctr, d_roots, d_full);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("tree classify: ") + hipGetErrorString(e)).c_str());
@@ -466,10 +622,10 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
 }
 
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
-                                         const int32_t* d_ord, const int32_t* d_children, const int32_t* d_nchildren,
+                                         const int32_t* d_ord, int32_t n, const int32_t* d_count,
                                          const _Float16* d_maps, float* d_hbuf, int grid, void* stream) {
-    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(d_weights, d_boards, d_meta, d_ord, d_children, d_nchildren,
-                                                           d_maps, d_hbuf);
+    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(d_weights, d_boards, d_meta, d_ord, n, d_count, d_maps,
+                                                           d_hbuf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_child_kernel: ") + hipGetErrorString(e)).c_str());
@@ -477,3 +633,17 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
     }
     return GZ_OK;
 }
+
+#ifdef GZ_PVINC_STAMPS
+// out[0..15] = ticks per phase, out[16] = children of workgroup 0
+extern "C" int gz_pvinc_stamps_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_pvinc_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(gz_pvinc_stamps_n), sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvinc_stamps), z, sizeof(z)) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvinc_stamps_n), z, sizeof(z[0])) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -942,7 +942,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
                                          int32_t* d_ord, int32_t* d_ctr, int32_t* d_roots, int32_t* d_children,
                                          int32_t* d_full, void* stream);
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
-                                         const int32_t* d_ord, const int32_t* d_children, const int32_t* d_nchildren,
+                                         const int32_t* d_ord, int32_t n, const int32_t* d_count,
                                          const _Float16* d_maps, float* d_hbuf, int grid, void* stream);
 
 namespace {
@@ -1002,8 +1002,7 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
                                                      t.ord, t.maps, root_cap);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
-    rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.children, t.ctr + 2, t.maps, t.hbuf, grid,
-                                   stream);
+    rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, n, d_count, t.maps, t.hbuf, grid, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);

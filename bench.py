@@ -40,13 +40,17 @@ import torch.distributed as dist  # noqa: E402
 
 from gzero import dist as gdist  # noqa: E402
 from gzero import weights  # noqa: E402
-from gzero.device import PVWeights  # noqa: E402
+from gzero.device import PVWeights, ptr, stream  # noqa: E402
 from gzero.selfplay import COUNTER_DTYPE, SelfPlayEngine  # noqa: E402
 
 METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2 dense peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (spec)
 PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
+# MFMA work a root child executes in the incremental forward (csrc/gz_pvinc.hip): the
+# residual convs over 2 + 4 + 6 + 8 row tiles of 16 (windows of radius 2..5, padded),
+# conv0 over one tile, the 1x1 head convs at the radius-5 window and the FC heads
+CHILD_FLOP_EXEC = 2 * (20 * 16 * 128 * 1152 + 16 * 128 * 27 + 121 * 128 * 3 + 450 * 225 + 225 * 64 + 64)
 
 
 def log(*a):
@@ -172,10 +176,14 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         eng.launch_pv()
         ev[1].record()
         ctr = eng.d_counters.clone()  # per-step counters, stays on the device
+        tst = None
+        if eng.tree:  # list sizes of the incremental forward (device copy, no sync)
+            tst = torch.zeros(4, dtype=torch.int32, device="cuda")
+            eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream())
         if ex is not None:
             ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
             ex.exchange()
-        return ev, ctr
+        return ev, ctr, tst
 
     if burn_in:
         eng.advance(burn_in)
@@ -191,7 +199,8 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
     barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c in recs]
+    ctrs = [np.frombuffer(c.cpu().numpy().tobytes(), COUNTER_DTYPE)[0] for _, c, _ in recs]
+    tree = [[int(x) for x in t.cpu()] for _, _, t in recs] if eng.tree else None
     moves = torch.tensor([float(sum(int(c["moves"]) for c in ctrs)), float(sum(int(c["mcts_moves"]) for c in ctrs))],
                          dtype=torch.float64, device="cuda")
     if ws > 1:
@@ -199,10 +208,10 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         dist.all_reduce(moves, op=dist.ReduceOp.SUM)
     T = float(elapsed.item())
     leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
-    pv_ms = [a.elapsed_time(b) for (a, b), _ in recs]
+    pv_ms = [a.elapsed_time(b) for (a, b), _, _ in recs]
     return {
         "T": T, "moves": float(moves[0].item()), "mcts": float(moves[1].item()),
-        "pv_ms": pv_ms, "leaves": leaves,
+        "pv_ms": pv_ms, "leaves": leaves, "tree": tree,
         "dropped": sum(int(c["leaves_dropped"]) + max(0, int(c["leaves"]) - eng.leaf_cap) for c in ctrs),
         "boards0": boards0, "gids0": gids0,
     }
@@ -211,7 +220,20 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
 def roofline_of(m, precision):
     mean_leaves = float(np.mean(m["leaves"]))
     mean_pv_s = float(np.mean(m["pv_ms"])) / 1e3
-    achieved = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
+    algorithmic = mean_leaves * PV_FLOP / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
+    achieved = algorithmic
+    tree = None
+    if m.get("tree"):
+        t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)  # roots seen, roots w/ maps, children, full
+        executed = (t[1] + t[3]) * PV_FLOP + t[2] * CHILD_FLOP_EXEC
+        achieved = executed / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
+        tree = {"roots": round(float(t[1]), 1), "children_incremental": round(float(t[2]), 1),
+                "full_other": round(float(t[3]), 1), "child_share": round(float(t[2] / max(1.0, mean_leaves)), 4),
+                "executed_flop_per_launch": round(float(executed), 0),
+                "algorithmic_tflops_full_forward_equivalent": round(algorithmic, 3),
+                "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child: "
+                         f"{CHILD_FLOP_EXEC / 1e6:.2f} MFLOP over its radius-2..5 windows) / kernel time; every node's "
+                         "logits, value, softmax and prior are bit-identical to the full forward's")}
     traffic, _ = load_traffic(mean_leaves) if precision == "f16x3" else (None, None)
     if precision == "fp32":
         peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
@@ -235,6 +257,10 @@ def roofline_of(m, precision):
                        "us_per_board": round(float(np.mean(m["pv_ms"])) * 1e3 / max(1.0, mean_leaves), 4)},
         "note": note,
     }
+    if tree:
+        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + deeper nodes, pv_child_kernel on "
+                       "root children, pv_heads_kernel, pv_prior_kernel)")
+        r["incremental"] = tree
     clk = load_clock("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32")
     if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
         r["clock"] = {"ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
@@ -256,7 +282,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--pv-precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="policy-value forward: 3-term fp16 split (f32 accumulate) or exact fp32 MFMA")
-    ap.add_argument("--pv-mode", default="full", choices=["full", "tree"],
+    ap.add_argument("--pv-mode", default="tree", choices=["full", "tree"],
                     help="full: one full forward per node; tree: the incremental forward of a root's children "
                          "(gz_pv_forward_tree, bit-identical outputs)")
     ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
@@ -338,7 +364,10 @@ def main():
                              f"beta={args.beta}, planner_steps={args.planner_steps}, continuous refill (timed after "
                              f"{burn_in} burn-in plies: the steady-state mix of game plies); policy-value "
                              "forward + masked prior on every non-terminal node the searches create "
-                             f"(reference-work mode, {args.pv_precision})"),
+                             f"(reference-work mode, {args.pv_precision}"
+                             + (", incremental forward of root children: bit-identical outputs" if eng.tree else "")
+                             + ")"),
+                "pv_mode": "tree" if eng.tree else "full",
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,

@@ -7,11 +7,12 @@ import os
 import sys
 
 d = sys.argv[1]
+name = sys.argv[2] if len(sys.argv) > 2 else "pv_kernel"  # kernel-name substring
 agg = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for f in glob.glob(os.path.join(d, "p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "pv_kernel" not in r["Kernel_Name"]:
+        if name not in r["Kernel_Name"]:
             continue
         k = r["Counter_Name"]
         agg[(os.path.basename(os.path.dirname(f)), k)] += float(r["Counter_Value"])

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the incremental policy-value forward (gz_pv_forward_tree).
+
+Plays --burn-in plies on --slots self-play slots (200 sims, no PV), then one
+step with the leaves gathered and tagged, and runs the tree forward (and, with
+--full, the full forward) --iters times on those same leaves.  Prints the list
+sizes, ms per launch and the bitwise check of the last launch against the full
+forward (--check).  Used with rocprofv3 (--kernel-trace / --pmc) to isolate
+pv_child_kernel.
+"""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "alphazero-gomoku_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gzero import _lib, weights  # noqa: E402
+from gzero.device import PVWeights, ptr, stream  # noqa: E402
+from gzero.selfplay import SelfPlayEngine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots", type=int, default=4096)
+    ap.add_argument("--burn-in", type=int, default=600)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--full", action="store_true", help="also time the full forward")
+    ap.add_argument("--check", type=int, default=1)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision="f16x3")
+    eng = SelfPlayEngine(n_slots=a.slots, num_simulations=200, beta=0.0, seed=1234, pv_weights=w, pv_mode="tree")
+    eng.advance(a.burn_in)
+    eng.step()
+    torch.cuda.synchronize()
+    n = int(eng.counters()["leaves"])
+    st = eng.tree_stats()
+    print(f"leaves {n}: roots {st[1]}, children {st[2]}, full {st[3]}", flush=True)
+    lib = eng.lib
+    d_count = eng.d_counters[4:8]
+
+    def tree():
+        _lib.check(lib.gz_pv_forward_tree(ptr(w.tensor), ptr(eng.d_leaves), ptr(eng.d_meta), eng.leaf_cap,
+                                          ptr(d_count), eng.root_cap, ptr(eng.d_logits), ptr(eng.d_value),
+                                          ptr(eng.d_probs), ptr(eng.d_prior), ptr(eng.d_tree_ws), stream()), "tree")
+
+    def timed(fn, label):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        fn()
+        torch.cuda.synchronize()
+        ev[0].record()
+        for _ in range(a.iters):
+            fn()
+        ev[1].record()
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / a.iters
+        print(f"{label}: {ms:.3f} ms per launch, {ms * 1e3 / n:.4f} us per board", flush=True)
+
+    stamps = hasattr(lib, "gz_pvinc_stamps_read")
+    if stamps:  # -DGZ_PVINC_STAMPS build (make -C tools variant VAR=pistamps EXTRA=-DGZ_PVINC_STAMPS)
+        import ctypes
+        lib.gz_pvinc_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        st = np.zeros(17, np.uint64)
+        tree()
+        torch.cuda.synchronize()
+        lib.gz_pvinc_stamps_read(st.ctypes.data, 1)
+    timed(tree, "tree")
+    if stamps:
+        lib.gz_pvinc_stamps_read(st.ctypes.data, 0)
+        names = ["meta+stone", "fill X0/Y1/X1 + im2col", "conv0", "y1 (L1)", "x1 (L2)", "fill Y2", "y2 (L3)",
+                 "x2 + heads (L4)", "record"]
+        kids = max(1, int(st[16]))
+        tot = sum(int(x) for x in st[:9])
+        print(f"pv_child_kernel workgroup 0: {kids} children, {tot / kids:.0f} s_memtime ticks per child")
+        for i, nm in enumerate(names):
+            print(f"  {nm:26s} {int(st[i]) / kids:9.0f}  {int(st[i]) / max(1, tot) * 100:5.1f}%")
+    if a.full or a.check:
+        out = [t[: n * k].clone() for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225),
+                                               (eng.d_prior, 225))]
+        ws = w.workspace_for(eng.leaf_cap)
+
+        def full():
+            _lib.check(lib.gz_pv_forward(ptr(w.tensor), ptr(eng.d_leaves), eng.leaf_cap, ptr(d_count),
+                                         ptr(eng.d_logits), ptr(eng.d_value), ptr(eng.d_probs), ptr(eng.d_prior),
+                                         ptr(ws), w.mode, stream()), "full")
+        if a.full:
+            timed(full, "full")
+        else:
+            full()
+        torch.cuda.synchronize()
+        ref = [t[: n * k] for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225), (eng.d_prior, 225))]
+        same = all(torch.equal(x, y) for x, y in zip(out, ref))
+        print(f"bitwise equal to the full forward: {same}", flush=True)
+        if not same:
+            sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
