@@ -76,21 +76,22 @@ constexpr int LDS_C = OFF_COL + 16 * 32 * 2;
 static_assert(OFF_Y1 + wbytes(P_Y1) <= OFF_HP, "X0 + Y1 fit in the Y2 region");
 static_assert(LDS_C <= 160 * 1024, "LDS budget");
 
-// A window of a map: radius r around the child's stone (cr, cc), width w = 2r+1,
-// P = w*w positions, hi plane then lo plane, each [16 cg][P][8].
+// A window of a map: radius R around the child's stone (cr, cc), width w = 2R+1,
+// P = w*w positions, hi plane then lo plane, each [16 cg][P][8].  The geometry is
+// compile-time, so window addressing folds into instruction offsets and constant
+// divisions.
+template <int R>
 struct Win {
+    static constexpr int r = R, w = 2 * R + 1, P = w * w;
     _Float16* hi;
-    int P, w, r;
-    __device__ int plane() const { return 16 * P * 8; }
-    __device__ int off(int ch0, int loc) const { return ((ch0 >> 3) * P + loc) * 8 + (ch0 & 7); }
+    __device__ static constexpr int plane() { return 16 * P * 8; }
+    __device__ static constexpr int off(int ch0, int loc) { return ((ch0 >> 3) * P + loc) * 8 + (ch0 & 7); }
 };
 
-__device__ inline Win make_win(char* lds, int off, int r) {
-    Win x;
+template <int R>
+__device__ inline Win<R> make_win(char* lds, int off) {
+    Win<R> x;
     x.hi = (_Float16*)(lds + off);
-    x.r = r;
-    x.w = 2 * r + 1;
-    x.P = x.w * x.w;
     return x;
 }
 
@@ -102,50 +103,44 @@ template <int IT>
 struct FillBuf {
     uint4 v[IT];
     uint32_t skip;  // bit k: item k is not stored (recomputed there, or past the window)
+    uint32_t zero;  // bit k: item k is off the board (stored as zeros)
 };
 
-// window item i -> (plane, cg, loc); board position; whether the fill writes it
-__device__ __forceinline__ bool fill_item(const Win& x, int rc, int cr, int cc, int i, int& plane, int& cg, int& loc,
-                                          int& pr, int& pc, bool& on) {
-    plane = i / (16 * x.P);
-    const int rem = i - plane * 16 * x.P;
-    cg = rem / x.P;
-    loc = rem - cg * x.P;
-    pr = cr - x.r + loc / x.w;
-    pc = cc - x.r + loc % x.w;
-    on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
-    const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-    return !(on && dr <= rc && dc <= rc);  // else written by the layer that recomputes it
-}
-
-template <int IT>
-__device__ __forceinline__ void fill_load(FillBuf<IT>& f, const Win& x, int rc, const _Float16* __restrict__ gm,
-                                          int cr, int cc, int tid) {
-    const int n = 2 * 16 * x.P;
+// Fill of window radius R (compile-time, so the index arithmetic divides by
+// constants).  Every item issues its load unconditionally (items that are skipped
+// or off the board read the map's first 16 bytes) through a buffer resource: no
+// branch between the loads, so all of a thread's loads are in flight together.
+template <int R, int IT>
+__device__ __forceinline__ void fill_load(FillBuf<IT>& f, int rc, const _Float16* __restrict__ gm, int cr, int cc,
+                                          int tid) {
+    constexpr int Wd = 2 * R + 1, P = Wd * Wd, n = 2 * 16 * P;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)gm, 0, 0x7fffffff, 0x00020000);
     f.skip = 0;
+    f.zero = 0;
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const int i = tid + k * NTC;
-        f.v[k] = make_uint4(0u, 0u, 0u, 0u);
-        int plane, cg, loc, pr, pc;
-        bool on;
-        if (i < n && fill_item(x, rc, cr, cc, i, plane, cg, loc, pr, pc, on)) {
-            if (on) f.v[k] = *(const uint4*)(gm + plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8);
-        } else {
-            f.skip |= 1u << k;
-        }
+        const int plane = i / (16 * P);
+        const int rem = i - plane * 16 * P;
+        const int cg = rem / P, loc = rem - cg * P;
+        const int pr = cr - R + loc / Wd, pc = cc - R + loc % Wd;
+        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
+        const bool keep = i < n && !(on && dr <= rc && dc <= rc);  // else the layer that recomputes it writes it
+        const int off = (keep && on) ? (plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8) * 2 : 0;
+        f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        f.skip |= keep ? 0u : (1u << k);
+        f.zero |= on ? 0u : (1u << k);
     }
 }
 
-template <int IT>
-__device__ __forceinline__ void fill_store(const FillBuf<IT>& f, const Win& x, int tid) {
+template <int R, int IT>
+__device__ __forceinline__ void fill_store(const FillBuf<IT>& f, const Win<R>& x, int tid) {
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         if (f.skip & (1u << k)) continue;
-        const int i = tid + k * NTC;
-        const int plane = i / (16 * x.P);
-        const int rem = i - plane * 16 * x.P;
-        *(uint4*)(x.hi + plane * x.plane() + rem * 8) = f.v[k];  // rem = cg * P + loc
+        const int i = tid + k * NTC;  // = plane * 16P + cg * P + loc: the window's own layout
+        *(uint4*)(x.hi + i * 8) = (f.zero & (1u << k)) ? make_uint4(0u, 0u, 0u, 0u) : f.v[k];
     }
 }
 
@@ -172,8 +167,8 @@ __device__ inline Rows make_rows(int cr, int cc, int rl) {
 // first nt (runtime, <= NMAX) M tiles: the k-steps, products and their order per
 // accumulator are those of f16_conv (gz_f16conv.h).  The weight fragments of the
 // next 4 k-steps are in flight (ring slot = cq, so the indexing stays static).
-template <int NTW, int NT, int NMAX>
-__device__ __forceinline__ void win_conv_nt(const Win& in, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
+template <int NTW, int NT, int NMAX, class WI>
+__device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
                                             int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
     constexpr int CQ = 4, KS = 9 * CQ;
     constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
@@ -184,9 +179,12 @@ __device__ __forceinline__ void win_conv_nt(const Win& in, const int (&ctr)[NMAX
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     const _Float16* lo_plane = in.hi + in.plane();
-    // weight ring: 4 k-steps in flight for one n-tile, 2 for two (their k-steps are
-    // twice as long); slot = cq % RING keeps the indexing static
-    constexpr int RING = NTW == 1 ? 4 : 2;
+    // weight ring: the next 4 k-steps' fragments in flight (an L2 hit takes longer
+    // than one short k-step); slot = cq % RING keeps the indexing static
+#ifndef PI_RING2
+#define PI_RING2 2
+#endif
+    constexpr int RING = NTW == 1 ? 4 : PI_RING2;
     h8 b[RING][NTW][2];
 #pragma unroll
     for (int c = 0; c < RING; c++)
@@ -195,33 +193,51 @@ __device__ __forceinline__ void win_conv_nt(const Win& in, const int (&ctr)[NMAX
             b[c][n][0] = wload(c, n, 0);
             b[c][n][1] = wload(c, n, 1);
         }
+    // activation fragments double-buffered: the next k-step's ds_reads are issued
+    // before this k-step's MFMAs (buffer = cq & 1; 4 k-steps per tap keep it static)
+    int nb[NT];
+#pragma unroll
+    for (int m = 0; m < NT; m++) nb[m] = (ctr[m] - in.w - 1 + q * in.P) * 8;  // tap 0 = (-1, -1)
+    h8 ah[2][NT], al[2][NT];
+#pragma unroll
+    for (int m = 0; m < NT; m++) {
+        ah[0][m] = *(const h8*)(in.hi + nb[m]);
+        al[0][m] = *(const h8*)(lo_plane + nb[m]);
+    }
 #pragma unroll 1
     for (int tap = 0; tap < 9; tap++) {
-        const int toff = (tap / 3 - 1) * in.w + (tap % 3 - 1);
-        int nb[NT];
-#pragma unroll
-        for (int m = 0; m < NT; m++) nb[m] = (ctr[m] + toff + q * in.P) * 8;
 #pragma unroll
         for (int cq = 0; cq < CQ; cq++) {
-            const int ao = cq * 4 * in.P * 8;
-            h8 ah[NT], al[NT];
+            const int cur = cq & 1, nxt = cur ^ 1;
+            if (cq < CQ - 1) {
+                const int ao = (cq + 1) * 4 * in.P * 8;
 #pragma unroll
-            for (int m = 0; m < NT; m++) {
-                ah[m] = *(const h8*)(in.hi + ao + nb[m]);
-                al[m] = *(const h8*)(lo_plane + ao + nb[m]);
+                for (int m = 0; m < NT; m++) {
+                    ah[nxt][m] = *(const h8*)(in.hi + ao + nb[m]);
+                    al[nxt][m] = *(const h8*)(lo_plane + ao + nb[m]);
+                }
+            } else {  // first k-step of the next tap (past the last: tap 0 again, unused)
+                const int t2 = tap + 1 < 9 ? tap + 1 : 0;
+                const int toff = (t2 / 3 - 1) * in.w + (t2 % 3 - 1);
+#pragma unroll
+                for (int m = 0; m < NT; m++) {
+                    nb[m] = (ctr[m] + toff + q * in.P) * 8;
+                    ah[nxt][m] = *(const h8*)(in.hi + nb[m]);
+                    al[nxt][m] = *(const h8*)(lo_plane + nb[m]);
+                }
             }
             const int sl = cq % RING;  // static once the cq loop is unrolled
 #pragma unroll
             for (int m = 0; m < NT; m++) {
 #pragma unroll
                 for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[m], acc[n][m], 0, 0, 0);
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[cur][m], acc[n][m], 0, 0, 0);
 #pragma unroll
                 for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[m], acc[n][m], 0, 0, 0);
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[cur][m], acc[n][m], 0, 0, 0);
 #pragma unroll
                 for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[m], acc[n][m], 0, 0, 0);
+                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[cur][m], acc[n][m], 0, 0, 0);
             }
             // refill this slot with k-step ks + RING (past the end: the first k-steps again, unused)
             const int ksr = tap * CQ + cq + RING;
@@ -238,42 +254,63 @@ __device__ __forceinline__ void win_conv_nt(const Win& in, const int (&ctr)[NMAX
 // win_conv_nt for the runtime tile count nt (1 <= nt <= NMAX): one branch per
 // layer, none inside the k-loop (a guard per tile there splits the loop into
 // basic blocks and the compiler then waits for every load at each boundary)
-template <int NTW, int NMAX>
-__device__ __forceinline__ void win_conv(const Win& in, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
+template <int NTW, int NMAX, class WI>
+__device__ __forceinline__ void win_conv(const WI& in, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
                                          int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
     static_assert(NMAX >= 1 && NMAX <= 6, "tile counts");
     switch (nt) {
-        case 1: win_conv_nt<NTW, 1, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
-        case 2: if constexpr (NMAX >= 2) win_conv_nt<NTW, 2, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
-        case 3: if constexpr (NMAX >= 3) win_conv_nt<NTW, 3, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
-        case 4: if constexpr (NMAX >= 4) win_conv_nt<NTW, 4, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
-        case 5: if constexpr (NMAX >= 5) win_conv_nt<NTW, 5, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
-        case 6: if constexpr (NMAX >= 6) win_conv_nt<NTW, 6, NMAX>(in, ctr, Wf, nt0, lane, acc); break;
+        case 1: win_conv_nt<NTW, 1, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 2: if constexpr (NMAX >= 2) win_conv_nt<NTW, 2, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 3: if constexpr (NMAX >= 3) win_conv_nt<NTW, 3, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 4: if constexpr (NMAX >= 4) win_conv_nt<NTW, 4, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 5: if constexpr (NMAX >= 5) win_conv_nt<NTW, 5, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 6: if constexpr (NMAX >= 6) win_conv_nt<NTW, 6, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
         default: break;
+    }
+}
+
+// Output positions of a wave's tiles: row i of the layer's recomputed square
+// (row-major) -> board (pr, pc); rows past the square recompute row 0 (discarded)
+template <int NMAX>
+struct TilePos {
+    int pr[NMAX], pc[NMAX];
+    bool valid[NMAX];
+};
+
+template <int NMAX>
+__device__ __forceinline__ void tile_positions(const Rows& rows, int t0, int lane, TilePos<NMAX>& tp) {
+    const int li = lane & 15;
+    const float inv = 1.0f / (float)rows.wr;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        int i = (t0 + m) * 16 + li;
+        tp.valid[m] = i < rows.n;
+        if (i >= rows.n) i = 0;
+        const int rr = (int)(((float)i + 0.5f) * inv);  // exact: i < 256, wr <= 11
+        tp.pr[m] = rows.r0 + rr;
+        tp.pc[m] = rows.c0 + (i - rr * rows.wr);
     }
 }
 
 // epilogue of a map layer: y = relu(acc*S + T (+ skip)) at the wave's rows into the
 // output window, hi/lo split (f16_put4)
-template <int NTW, int NMAX, bool SKIP>
-__device__ __forceinline__ void child_store(const f32x4 (&acc)[NTW][NMAX], const Rows& rows, int t0, int nt,
-                                            const Win& out, const Win& skw, int cr, int cc, const float* __restrict__ R,
+template <int NTW, int NMAX, bool SKIP, class WO, class WS>
+__device__ __forceinline__ void child_store(const f32x4 (&acc)[NTW][NMAX], const TilePos<NMAX>& tp, int nt,
+                                            const WO& out, const WS& skw, int cr, int cc, const float* __restrict__ R,
                                             int nt0, int lane) {
-    const int li = lane & 15;
 #pragma unroll
     for (int n = 0; n < NTW; n++) {
         const int ch0 = (nt0 + n) * 16 + 4 * (lane >> 4);
         const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
-            const int i = (t0 + m) * 16 + li;
-            if (m >= nt || i >= rows.n) continue;
-            const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
+            if (m >= nt || !tp.valid[m]) continue;
+            const int pr = tp.pr[m], pc = tp.pc[m];
             f32x4 sk = zero4();
             if (SKIP) {
-                const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
+                const int sl = WS::off(ch0, (pr - cr + WS::r) * WS::w + (pc - cc + WS::r));
                 const h4 xh = *(const h4*)(skw.hi + sl);
-                const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
+                const h4 xl = *(const h4*)(skw.hi + WS::plane() + sl);
 #pragma unroll
                 for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
             }
@@ -287,47 +324,64 @@ __device__ __forceinline__ void child_store(const f32x4 (&acc)[NTW][NMAX], const
                 hi[r] = h;
                 lo[r] = (_Float16)(y - (float)h);
             }
-            const int o = out.off(ch0, (pr - cr + out.r) * out.w + (pc - cc + out.r));
+            const int o = WO::off(ch0, (pr - cr + WO::r) * WO::w + (pc - cc + WO::r));
             *(h4*)(out.hi + o) = hi;
-            *(h4*)(out.hi + out.plane() + o) = lo;
+            *(h4*)(out.hi + WO::plane() + o) = lo;
         }
     }
 }
 
-template <int NMAX>
-__device__ __forceinline__ void tile_centres(const Win& in, const Rows& rows, int t0, int cr, int cc, int lane,
-                                             int (&ctr)[NMAX]) {
-    const int li = lane & 15;
+template <int NMAX, class WI>
+__device__ __forceinline__ void tile_centres(const TilePos<NMAX>& tp, int cr, int cc, int (&ctr)[NMAX]) {
 #pragma unroll
-    for (int m = 0; m < NMAX; m++) {
-        int i = (t0 + m) * 16 + li;
-        if (i >= rows.n) i = 0;  // padding rows recompute row 0 (discarded)
-        const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
-        ctr[m] = (pr - cr + in.r) * in.w + (pc - cc + in.r);
-    }
+    for (int m = 0; m < NMAX; m++) ctr[m] = (tp.pr[m] - cr + WI::r) * WI::w + (tp.pc[m] - cc + WI::r);
 }
 
-// a map layer (y1, x1, y2): wave w = n-tile w over all the layer's M tiles, so every
-// weight fragment is read once per child and feeds 3 x (tiles) MFMAs
-template <int NMAX, bool SKIP>
-__device__ __forceinline__ void child_map_layer(const Win& in, const Win& out, const Win& skw, int cr, int cc, int rl,
+// NTW = 1: wave w = n-tile w over all the layer's M tiles (each weight fragment read
+// once per child, each activation fragment feeds 3 MFMAs); NTW = 2: wave = (n-tile
+// pair, balanced M half), as the full kernel (activation fragments feed 6 MFMAs,
+// weights read by both halves).  NMAX = the layer's tiles per wave at most.
+template <int NTW, int NMAX, bool SKIP, class WI, class WO, class WS>
+__device__ __forceinline__ void child_map_layer(const WI& in, const WO& out, const WS& skw, int cr, int cc,
                                                 const float* __restrict__ W, int layer, int wave, int lane) {
-    const Rows rows = make_rows(cr, cc, rl);
-    const int nt = (rows.n + 15) >> 4;
+    const Rows rows = make_rows(cr, cc, WI::r - 1);
+    const int T = (rows.n + 15) >> 4;
+    int t0 = 0, nt = T, nt0 = wave;
+    if (NTW == 2) {
+        const int T0 = (T + 1) >> 1, mg = wave >> 2;
+        t0 = mg ? T0 : 0;
+        nt = mg ? T - T0 : T0;
+        nt0 = 2 * (wave & 3);
+    }
+    TilePos<NMAX> tp;
+    tile_positions<NMAX>(rows, t0, lane, tp);
     int ctr[NMAX];
-    tile_centres<NMAX>(in, rows, 0, cr, cc, lane, ctr);
-    f32x4 acc[1][NMAX];
+    tile_centres<NMAX, WI>(tp, cr, cc, ctr);
+    f32x4 acc[NTW][NMAX];
 #pragma unroll
-    for (int m = 0; m < NMAX; m++) acc[0][m] = zero4();
-    win_conv<1, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), wave, lane, acc);
-    child_store<1, NMAX, SKIP>(acc, rows, 0, nt, out, skw, cr, cc, W + RES0 + layer * RES_STRIDE, wave, lane);
+    for (int n = 0; n < NTW; n++)
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    if (nt > 0)
+        win_conv<NTW, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), nt0, lane, acc);
+    child_store<NTW, NMAX, SKIP>(acc, tp, nt, out, skw, cr, cc, W + RES0 + layer * RES_STRIDE, nt0, lane);
 }
+
+#ifndef PI_NTW1
+#define PI_NTW1 1  // n-tiles per wave of y1 / x1 / y2 (tools/Makefile variants)
+#endif
+#ifndef PI_NTW2
+#define PI_NTW2 1
+#endif
+#ifndef PI_NTW3
+#define PI_NTW3 2
+#endif
 
 // the last residual layer (x2): the 1x1 head convs' partial sums need a wave's
 // 32 channels (n-tiles 2np, 2np+1) in one fma chain per lane (f16_store_heads), so
 // here wave = (n-tile pair np, M half); the M tiles are split evenly
-template <int NMAX>
-__device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, int cr, int cc,
+template <int NMAX, class WI, class WS>
+__device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, int cr, int cc,
                                                  const float* __restrict__ W, int wave, int lane,
                                                  float* __restrict__ hpart) {
     constexpr int layer = 3;
@@ -336,14 +390,16 @@ __device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, 
     const int T = (rows.n + 15) >> 4;
     const int T0 = (T + 1) >> 1;
     const int t0 = mg ? T0 : 0, nt = mg ? T - T0 : T0;
+    TilePos<NMAX> tp;
+    tile_positions<NMAX>(rows, t0, lane, tp);
     int ctr[NMAX];
-    tile_centres<NMAX>(in, rows, t0, cr, cc, lane, ctr);
+    tile_centres<NMAX, WI>(tp, cr, cc, ctr);
     f32x4 acc[2][NMAX];
 #pragma unroll
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    win_conv<2, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
+    if (nt > 0) win_conv<2, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     const float* R = W + RES0 + layer * RES_STRIDE;
     const int li = lane & 15;
     float s0[NMAX], s1[NMAX], sv[NMAX];
@@ -358,12 +414,9 @@ __device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, 
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
             if (m >= nt) continue;
-            int i = (t0 + m) * 16 + li;
-            if (i >= rows.n) i = 0;
-            const int pr = rows.r0 + i / rows.wr, pc = rows.c0 + i % rows.wr;
-            const int sl = skw.off(ch0, (pr - cr + skw.r) * skw.w + (pc - cc + skw.r));
+            const int sl = WS::off(ch0, (tp.pr[m] - cr + WS::r) * WS::w + (tp.pc[m] - cc + WS::r));
             const h4 xh = *(const h4*)(skw.hi + sl);
-            const h4 xl = *(const h4*)(skw.hi + skw.plane() + sl);
+            const h4 xl = *(const h4*)(skw.hi + WS::plane() + sl);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
@@ -385,7 +438,7 @@ __device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, 
         c += __shfl_xor(c, 32);
         v += __shfl_xor(v, 32);
         const int i = (t0 + m) * 16 + li;
-        if (lane < 16 && i < rows.n) {
+        if (lane < 16 && tp.valid[m]) {
             hpart[(np * 3 + 0) * HP_ROWS + i] = a;
             hpart[(np * 3 + 1) * HP_ROWS + i] = c;
             hpart[(np * 3 + 2) * HP_ROWS + i] = v;
@@ -395,10 +448,8 @@ __device__ __forceinline__ void child_head_layer(const Win& in, const Win& skw, 
 
 __device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
 
-// Children are processed in leaf order, each workgroup a contiguous chunk of the
-// leaf buffer: a root's children (stored right after it by the search) stay on one
-// CU, so the root's maps are read from that XCD's L2 after the first child.  A leaf
-// is a child here iff meta >= 0 and its root got a map slot (ord >= 0).
+// Children are processed in leaf order (a root's children follow it in the leaf
+// buffer).  A leaf is a child here iff meta >= 0 and its root got a map slot (ord >= 0).
 __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restrict__ W,
                                                           const uint32_t* __restrict__ boards,
                                                           const int32_t* __restrict__ meta,
@@ -406,14 +457,23 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
                                                           const int32_t* __restrict__ d_count,
                                                           const _Float16* __restrict__ maps, float* __restrict__ hbuf) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_C];
-    const Win X0 = make_win(lds, OFF_X0, 3), Y1 = make_win(lds, OFF_Y1, 4);
-    const Win X1 = make_win(lds, OFF_X1, 5), Y2 = make_win(lds, OFF_Y2, 6);
+    const auto X0 = make_win<3>(lds, OFF_X0);
+    const auto Y1 = make_win<4>(lds, OFF_Y1);
+    const auto X1 = make_win<5>(lds, OFF_X1);
+    const auto Y2 = make_win<6>(lds, OFF_Y2);
     float* hpart = (float*)(lds + OFF_HP);
     _Float16* col = (_Float16*)(lds + OFF_COL);
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
-    const int chunk = (count + gridDim.x - 1) / gridDim.x;
-    const int beg = blockIdx.x * chunk, end = beg + chunk < count ? beg + chunk : count;
-    for (int b = beg; b < end; b++) {
+    // XCD-aware order: workgroup g runs on XCD g % 8 (round-robin dispatch); each XCD
+    // takes a contiguous eighth of the leaves and its workgroups interleave over it,
+    // so the CUs of one XCD work on neighbouring children -- the same root, whose
+    // maps then stay in that XCD's L2 (placement only affects speed, not results)
+    const int nx = gridDim.x >= 8 ? 8 : 1;
+    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
+    const int chunk = (count + nx - 1) / nx;
+    if (k >= per) return;  // grids that are not a multiple of 8: the remainder idles
+    const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
+    for (int b = beg; b < end; b += per) {
         PI_T0();
         const int rb = __builtin_amdgcn_readfirstlane(meta[b]);
         if (rb < 0) continue;
@@ -441,12 +501,12 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
             FillBuf<fill_items(P_X0)> f0;
             FillBuf<fill_items(P_Y1)> f1;
             FillBuf<fill_items(P_X1)> f2;
-            fill_load(f0, X0, 1, gm, cr, cc, tid);
-            fill_load(f1, Y1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
-            fill_load(f2, X1, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
-            fill_store(f0, X0, tid);
-            fill_store(f1, Y1, tid);
-            fill_store(f2, X1, tid);
+            fill_load<3>(f0, 1, gm, cr, cc, tid);
+            fill_load<4>(f1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
+            fill_load<5>(f2, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
+            fill_store<3>(f0, X0, tid);
+            fill_store<4>(f1, Y1, tid);
+            fill_store<5>(f2, X1, tid);
         }
         {
             const Rows r0w = make_rows(cr, cc, 1);
@@ -496,19 +556,19 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
         }
         __syncthreads();
         PI_STAMP(2);
-        child_map_layer<2, false>(X0, Y1, X0, cr, cc, 2, W, 0, wave, lane);  // y1
+        child_map_layer<PI_NTW1, 2 / PI_NTW1, false>(X0, Y1, X0, cr, cc, W, 0, wave, lane);  // y1
         __syncthreads();
         PI_STAMP(3);
-        child_map_layer<4, true>(Y1, X1, X0, cr, cc, 3, W, 1, wave, lane);   // x1 = relu(.. + x0)
+        child_map_layer<PI_NTW2, 4 / PI_NTW2, true>(Y1, X1, X0, cr, cc, W, 1, wave, lane);  // x1 = relu(.. + x0)
         __syncthreads();
         PI_STAMP(4);
         {
             FillBuf<fill_items(P_Y2)> f3;  // X0 / Y1 are dead
-            fill_load(f3, Y2, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);
-            fill_store(f3, Y2, tid);
+            fill_load<6>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);
+            fill_store<6>(f3, Y2, tid);
         }
         PI_STAMP(5);
-        child_map_layer<6, false>(X1, Y2, X1, cr, cc, 4, W, 2, wave, lane);  // y2
+        child_map_layer<PI_NTW3, 6 / PI_NTW3, false>(X1, Y2, X1, cr, cc, W, 2, wave, lane);  // y2
         __syncthreads();
         PI_STAMP(6);
         child_head_layer<4>(Y2, X1, cr, cc, W, wave, lane, hpart);  // x2 -> head convs

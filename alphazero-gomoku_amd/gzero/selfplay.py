@@ -146,6 +146,15 @@ class SelfPlayEngine:
                    "gz_pv_tree_stats")
         return [int(x) for x in out.cpu()]
 
+    def tree_exec_flops(self):
+        """(executed MFMA FLOP of the last tree forward, its node count): roots and
+        deeper nodes run the full forward, a root child the row tiles of its windows
+        (csrc/gz_pvinc.hip).  Reads the leaves and tags (synchronising)."""
+        n = min(int(self.counters()["leaves"]), self.leaf_cap)
+        rows = self.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
+        meta = self.d_meta[:n].cpu().numpy()
+        return tree_exec_flops(rows, meta), n
+
     # ---- host views (synchronising)
     def counters(self):
         return np.frombuffer(self.d_counters.cpu().numpy().tobytes(), COUNTER_DTYPE)[0]
@@ -187,3 +196,38 @@ def records_to_replay(recs):
     cells = words_to_cells(recs["black"], recs["white"]).reshape(-1, 15, 15)
     planes = np.stack([(cells == 1), (cells == 2), (cells == 0)], axis=1).astype(np.float32)
     return planes, recs["move"].astype(np.int64), recs["player"].astype(np.int64), recs["z"].astype(np.int64)
+
+
+PV_FLOP_FULL = 2 * 133690114  # one full forward (gzero.weights.PV_MACS)
+
+
+def _window_rows(rc, r):
+    lo = np.maximum(rc - r, 0)
+    hi = np.minimum(rc + r, 14)
+    return hi - lo + 1
+
+
+def tree_exec_flops(rows, meta):
+    """MFMA FLOP the tree forward executes for leaves `rows` ([n,16] uint32) tagged
+    `meta`: 2 x (MACs of every 16-row tile it runs), fp32-equivalent like the full
+    forward's 267.38 MFLOP.  A root child at (r, c) runs, per residual conv L = 1..4
+    (window radius L + 1), ceil(rows_L / 16) tiles of 16 positions x 128 channels x
+    1152, one conv0 tile, the 1x1 heads at radius 5 and the FC heads."""
+    meta = np.asarray(meta)
+    kids = np.flatnonzero(meta >= 0)
+    full = len(meta) - len(kids)
+    if len(kids) == 0:
+        return float(full * PV_FLOP_FULL)
+    diff = rows[kids] ^ rows[meta[kids]]
+    both = diff[:, :8] | diff[:, 8:]
+    word = np.argmax(both != 0, axis=1)
+    bitv = both[np.arange(len(kids)), word]
+    bit = word * 32 + np.log2(bitv.astype(np.float64)).astype(np.int64)
+    r, c = bit // 16, bit % 16
+    macs = np.zeros(len(kids), np.float64)
+    for L in range(1, 5):
+        n_rows = _window_rows(r, L + 1) * _window_rows(c, L + 1)
+        macs += np.ceil(n_rows / 16.0) * 16 * 128 * 1152
+    n4 = _window_rows(r, 5) * _window_rows(c, 5)
+    macs += 16 * 128 * 27 + n4 * 128 * 3 + 450 * 225 + 225 * 64 + 64
+    return float(full * PV_FLOP_FULL + 2.0 * macs.sum())

@@ -47,10 +47,7 @@ METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2 dense peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (spec)
 PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
-# MFMA work a root child executes in the incremental forward (csrc/gz_pvinc.hip): the
-# residual convs over 2 + 4 + 6 + 8 row tiles of 16 (windows of radius 2..5, padded),
-# conv0 over one tile, the 1x1 head convs at the radius-5 window and the FC heads
-CHILD_FLOP_EXEC = 2 * (20 * 16 * 128 * 1152 + 16 * 128 * 27 + 121 * 128 * 3 + 450 * 225 + 225 * 64 + 64)
+
 
 
 def log(*a):
@@ -208,10 +205,14 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         dist.all_reduce(moves, op=dist.ReduceOp.SUM)
     T = float(elapsed.item())
     leaves = [min(int(c["leaves"]), eng.leaf_cap) for c in ctrs]
+    exec_per_board = None
+    if eng.tree:
+        fl, nl = eng.tree_exec_flops()
+        exec_per_board = fl / max(1, nl)
     pv_ms = [a.elapsed_time(b) for (a, b), _, _ in recs]
     return {
         "T": T, "moves": float(moves[0].item()), "mcts": float(moves[1].item()),
-        "pv_ms": pv_ms, "leaves": leaves, "tree": tree,
+        "pv_ms": pv_ms, "leaves": leaves, "tree": tree, "exec_per_board": exec_per_board,
         "dropped": sum(int(c["leaves_dropped"]) + max(0, int(c["leaves"]) - eng.leaf_cap) for c in ctrs),
         "boards0": boards0, "gids0": gids0,
     }
@@ -225,15 +226,18 @@ def roofline_of(m, precision):
     tree = None
     if m.get("tree"):
         t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)  # roots seen, roots w/ maps, children, full
-        executed = (t[1] + t[3]) * PV_FLOP + t[2] * CHILD_FLOP_EXEC
+        # executed MFMA FLOP per board, from the last step's leaves (tree_exec_flops)
+        executed = m["exec_per_board"] * mean_leaves
         achieved = executed / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
         tree = {"roots": round(float(t[1]), 1), "children_incremental": round(float(t[2]), 1),
                 "full_other": round(float(t[3]), 1), "child_share": round(float(t[2] / max(1.0, mean_leaves)), 4),
                 "executed_flop_per_launch": round(float(executed), 0),
                 "algorithmic_tflops_full_forward_equivalent": round(algorithmic, 3),
+                "executed_mflop_per_child": round((m["exec_per_board"] * mean_leaves - (t[1] + t[3]) * PV_FLOP)
+                                                  / max(1.0, t[2]) / 1e6, 2),
                 "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child: "
-                         f"{CHILD_FLOP_EXEC / 1e6:.2f} MFLOP over its radius-2..5 windows) / kernel time; every node's "
-                         "logits, value, softmax and prior are bit-identical to the full forward's")}
+                         "the 16-row tiles of its radius-2..5 windows, clipped at the board edge) / kernel time; "
+                         "every node's logits, value, softmax and prior are bit-identical to the full forward's")}
     traffic, _ = load_traffic(mean_leaves) if precision == "f16x3" else (None, None)
     if precision == "fp32":
         peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"

@@ -32,4 +32,5 @@ if g:
 w = c.get("SQ_WAVE_CYCLES", 0)
 if w:
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
-        print(f"{k:32s} {c[k] / w * 100:.1f}% of wave cycles")
+        if k in c:
+            print(f"{k:32s} {c[k] / w * 100:.1f}% of wave cycles")
