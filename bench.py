@@ -54,14 +54,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_traffic(boards):
-    """HBM bytes per PV launch of `boards` boards: rocprof FETCH_SIZE + WRITE_SIZE per board
-    (profiles/pv_traffic.json, collected by profiles/collect.sh) x boards, or None."""
+def load_traffic(boards, mode):
+    """HBM bytes per PV launch of `boards` boards: rocprof 2 x FETCH_SIZE + WRITE_SIZE per
+    board of the same PV mode (profiles/pv_traffic.json, profiles/collect.sh) x boards, or None."""
     p = os.path.join(REPO, "profiles", "pv_traffic.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        if d.get("bytes_per_board"):
+        if d.get("bytes_per_board") and d.get("pv_mode", "full") == mode:
             return round(d["bytes_per_board"] * boards, 1), d
     return None, None
 
@@ -238,7 +238,8 @@ def roofline_of(m, precision):
                 "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child: "
                          "the 16-row tiles of its radius-2..5 windows, clipped at the board edge) / kernel time; "
                          "every node's logits, value, softmax and prior are bit-identical to the full forward's")}
-    traffic, _ = load_traffic(mean_leaves) if precision == "f16x3" else (None, None)
+    traffic, _ = load_traffic(mean_leaves, "tree" if m.get("tree") else "full") if precision == "f16x3" \
+        else (None, None)
     if precision == "fp32":
         peak, note = FP32_MFMA_PEAK_TFLOPS, "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
     else:

@@ -5,11 +5,11 @@
 # Usage: profiles/collect.sh <round-tag> [bench args...]
 set -u
 tag=${1:-r01}; shift || true
-args=${*:-"--steps 2 --warmup 7 --no-cpu-baseline --elided-warmup 60 --elided-plies 30"}
+args=${*:-"--steps 8 --warmup 2 --no-cpu-baseline --config4-steps 0 --fp32-steps 0 --no-elided"}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py $args > $out/bench_trace.json 2> $out/bench_trace.err || exit $?
-timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o run -- python3 bench.py $args --no-elided > $out/bench_fetch.json 2> $out/bench_fetch.err || exit $?
-timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- python3 bench.py $args --no-elided > $out/bench_write.json 2> $out/bench_write.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py $args > $out/bench_trace.json 2> $out/bench_trace.err || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o run -- python3 bench.py $args > $out/bench_fetch.json 2> $out/bench_fetch.err || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- python3 bench.py $args > $out/bench_write.json 2> $out/bench_write.err || exit $?
 echo collected
