@@ -107,12 +107,15 @@ struct FillBuf {
 };
 
 // Fill of window radius R (compile-time, so the index arithmetic divides by
-// constants).  Every item issues its load unconditionally (items that are skipped
-// or off the board read the map's first 16 bytes) through a buffer resource: no
+// constants) from the root's map gm.  Every item issues its load unconditionally
+// (items that are skipped or off the board read the map's first 16 bytes): no
 // branch between the loads, so all of a thread's loads are in flight together.
-template <int R, int IT>
+// Skipped: the positions the layer recomputes (on the board within rc of the stone)
+// and, for a grandchild, the square of radius rcp around its parent's stone (r1, c1),
+// which patch_fill takes from the parent's patch.
+template <int R, int IT, bool GC>
 __device__ __forceinline__ void fill_load(FillBuf<IT>& f, int rc, const _Float16* __restrict__ gm, int cr, int cc,
-                                          int tid) {
+                                          int tid, int r1 = 0, int c1 = 0, int rcp = -1) {
     constexpr int Wd = 2 * R + 1, P = Wd * Wd, n = 2 * 16 * P;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)gm, 0, 0x7fffffff, 0x00020000);
     f.skip = 0;
@@ -126,11 +129,58 @@ __device__ __forceinline__ void fill_load(FillBuf<IT>& f, int rc, const _Float16
         const int pr = cr - R + loc / Wd, pc = cc - R + loc % Wd;
         const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
         const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-        const bool keep = i < n && !(on && dr <= rc && dc <= rc);  // else the layer that recomputes it writes it
+        bool keep = i < n && !(on && dr <= rc && dc <= rc);  // else the layer that recomputes it writes it
+        if (GC) {
+            const int er = pr > r1 ? pr - r1 : r1 - pr, ec = pc > c1 ? pc - c1 : c1 - pc;
+            keep = keep && !(er <= rcp && ec <= rcp);
+        }
         const int off = (keep && on) ? (plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8) * 2 : 0;
         f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         f.skip |= keep ? 0u : (1u << k);
         f.zero |= on ? 0u : (1u << k);
+    }
+}
+
+// A grandchild's values of window x (radius R) in the square of radius RC around
+// its parent's stone (r1, c1): the parent's patch pt of that map
+// ([plane][16 cg][(2RC+1)^2][8], off-board entries zero), except the positions
+// this layer recomputes (on the board within rc of the grandchild's stone).
+template <int R, int RC>
+struct PatchFill {
+    static constexpr int S = 2 * RC + 1, n = 2 * 16 * S * S, IT = (n + NTC - 1) / NTC;
+    uint4 v[IT];
+    uint32_t put;
+};
+template <int R, int RC>
+__device__ __forceinline__ void patch_load(PatchFill<R, RC>& f, const _Float16* __restrict__ pt, int rc, int cr,
+                                           int cc, int r1, int c1, int tid) {
+    using F = PatchFill<R, RC>;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pt, 0, 0x7fffffff, 0x00020000);
+    f.put = 0;
+#pragma unroll
+    for (int k = 0; k < F::IT; k++) {
+        const int i = tid + k * NTC;
+        const int loc = i % (F::S * F::S);
+        const int pr = r1 - RC + loc / F::S, pc = c1 - RC + loc % F::S;
+        const int wr = pr - cr + R, wc = pc - cc + R;
+        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
+        const bool put = i < F::n && wr >= 0 && wr <= 2 * R && wc >= 0 && wc <= 2 * R && !(on && dr <= rc && dc <= rc);
+        f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i < F::n ? i : 0) * 16, 0, 0));
+        f.put |= put ? (1u << k) : 0u;
+    }
+}
+template <int R, int RC>
+__device__ __forceinline__ void patch_store(const PatchFill<R, RC>& f, const Win<R>& x, int cr, int cc, int r1, int c1,
+                                            int tid) {
+    using F = PatchFill<R, RC>;
+#pragma unroll
+    for (int k = 0; k < F::IT; k++) {
+        if (!(f.put & (1u << k))) continue;
+        const int i = tid + k * NTC;
+        const int pcg = i / (F::S * F::S), loc = i - pcg * (F::S * F::S);  // pcg = plane * 16 + cg
+        const int wl = (r1 - RC + loc / F::S - cr + R) * x.w + (c1 - RC + loc % F::S - cc + R);
+        *(uint4*)(x.hi + (pcg * x.P + wl) * 8) = f.v[k];
     }
 }
 
@@ -145,6 +195,7 @@ __device__ __forceinline__ void fill_store(const FillBuf<IT>& f, const Win<R>& x
 }
 
 constexpr int fill_items(int P) { return (2 * 16 * P + NTC - 1) / NTC; }
+static_assert(fill_items(169) <= 32, "skip / zero masks are 32-bit");
 
 // the recomputed rows of one layer: the square of radius rl around (cr, cc),
 // clipped, row-major
@@ -448,21 +499,235 @@ __device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, in
 
 __device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
 
-// Children are processed in leaf order (a root's children follow it in the leaf
-// buffer).  A leaf is a child here iff meta >= 0 and its root got a map slot (ord >= 0).
-__global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restrict__ W,
-                                                          const uint32_t* __restrict__ boards,
-                                                          const int32_t* __restrict__ meta,
-                                                          const int32_t* __restrict__ ord, int n,
-                                                          const int32_t* __restrict__ d_count,
-                                                          const _Float16* __restrict__ maps, float* __restrict__ hbuf) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
+// A parent's patch for its grandchildren: the recomputed squares of its maps
+// (x0 r1, y1 r2, x1 r3, y2 r4), [plane][16 cg][(2r+1)^2][8] each, in that order
+constexpr int PATCH_R[4] = {1, 2, 3, 4};
+constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // halves
+constexpr int PATCH_HALVES = 164 * 256;
+
+// the stone where boards a and b differ (one bit): cell r*15 + c
+__device__ inline int stone_between(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
+    int cell = 0;
+    for (int k = 0; k < 16; k++) {
+        const uint32_t d = __builtin_amdgcn_readfirstlane(a[k] ^ b[k]);
+        if (d) {
+            const int bit = (k & 7) * 32 + __builtin_ctz(d);
+            cell = (bit >> 4) * BN + (bit & 15);
+        }
+    }
+    return cell;
+}
+
+// copy the square of radius RC around (cr, cc) of window x into patch slot pt
+template <int R, int RC>
+__device__ __forceinline__ void patch_dump(const Win<R>& x, _Float16* __restrict__ pt, int tid) {
+    constexpr int S = 2 * RC + 1, n = 2 * 16 * S * S;
+    for (int i = tid; i < n; i += NTC) {
+        const int pc_ = i / (S * S), loc = i - pc_ * (S * S);  // pc_ = plane * 16 + cg
+        const int wl = (loc / S - RC + R) * x.w + (loc % S - RC + R);
+        *(uint4*)(pt + i * 8) = *(const uint4*)(x.hi + (pc_ * x.P + wl) * 8);
+    }
+}
+
+struct TreeArgs {
+    const float* W;
+    const uint32_t* boards;
+    const int32_t* meta;
+    const int32_t* ord;
+    const int32_t* pslot;
+    const _Float16* maps;
+    _Float16* patches;
+    float* hbuf;
+};
+
+// The incremental forward of node b relative to node base (its parent): the root
+// child of root rb (GC = false; base = rb) or the grandchild of root rb through the
+// root child base (GC = true: the parent's maps are the root's overlaid with the
+// parent's patch).  dump >= 0: also store b's patch in slot dump (b has grandchildren).
+template <bool GC>
+__device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, int base, int rb, int dump) {
+    const float* W = A.W;
+    // opaque per node (bit 0: child kernel, bit 1: grandchild kernel): keeps the
+    // compiler from hoisting every layer's per-lane weight addresses out of the node
+    // loop (they would stay live, and spill, across it)
+#ifndef PI_OPQ_W
+#define PI_OPQ_W 3
+#endif
+#ifndef PI_OPQ_T
+#define PI_OPQ_T 2
+#endif
+    if (PI_OPQ_W & (GC ? 2 : 1)) asm volatile("" : "+s"(W));
     const auto X0 = make_win<3>(lds, OFF_X0);
     const auto Y1 = make_win<4>(lds, OFF_Y1);
     const auto X1 = make_win<5>(lds, OFF_X1);
     const auto Y2 = make_win<6>(lds, OFF_Y2);
     float* hpart = (float*)(lds + OFF_HP);
     _Float16* col = (_Float16*)(lds + OFF_COL);
+    PI_T0();
+    const int o = __builtin_amdgcn_readfirstlane(A.ord[rb]);
+    int tid = threadIdx.x;
+    if (PI_OPQ_T & (GC ? 2 : 1)) asm volatile("" : "+v"(tid));  // likewise the fills' index arithmetic
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t* cb = A.boards + (size_t)b * 16;
+    const int cell = stone_between(cb, A.boards + (size_t)base * 16);
+    const int cr = cell / BN, cc = cell % BN;
+    int r1 = 0, c1 = 0;
+    const _Float16* pt = nullptr;
+    if (GC) {
+        const int c1cell = stone_between(A.boards + (size_t)base * 16, A.boards + (size_t)rb * 16);
+        r1 = c1cell / BN;
+        c1 = c1cell % BN;
+        pt = A.patches + (size_t)__builtin_amdgcn_readfirstlane(A.pslot[base]) * PATCH_HALVES;
+    }
+    const _Float16* gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
+    PI_STAMP(0);
+
+    // phase 0: the parent's values around the recomputed windows; conv0's im2col
+    {
+        FillBuf<fill_items(P_X0)> f0;
+        FillBuf<fill_items(P_Y1)> f1;
+        FillBuf<fill_items(P_X1)> f2;
+        fill_load<3, fill_items(P_X0), GC>(f0, 1, gm, cr, cc, tid, r1, c1, PATCH_R[0]);
+        fill_load<4, fill_items(P_Y1), GC>(f1, 2, gm + PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[1]);
+        fill_load<5, fill_items(P_X1), GC>(f2, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[2]);
+        if (GC) {  // the parent's recomputed squares (disjoint from the positions above)
+            PatchFill<3, PATCH_R[0]> p0;
+            PatchFill<4, PATCH_R[1]> p1;
+            PatchFill<5, PATCH_R[2]> p2;
+            patch_load(p0, pt + PATCH_OFF[0], 1, cr, cc, r1, c1, tid);
+            patch_load(p1, pt + PATCH_OFF[1], 2, cr, cc, r1, c1, tid);
+            patch_load(p2, pt + PATCH_OFF[2], 3, cr, cc, r1, c1, tid);
+            patch_store(p0, X0, cr, cc, r1, c1, tid);
+            patch_store(p1, Y1, cr, cc, r1, c1, tid);
+            patch_store(p2, X1, cr, cc, r1, c1, tid);
+        }
+        fill_store<3>(f0, X0, tid);
+        fill_store<4>(f1, Y1, tid);
+        fill_store<5>(f2, X1, tid);
+    }
+    {
+        const Rows r0w = make_rows(cr, cc, 1);
+        const int row = tid >> 5, k = tid & 31;  // 16 rows x 32 k
+        _Float16 v = (_Float16)0.f;
+        if (row < r0w.n && k < 27) {
+            const int pr = r0w.r0 + row / r0w.wr, pc = r0w.c0 + row % r0w.wr;
+            const int tap = k / 3, cin = k % 3;
+            const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
+            if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
+                const int bit = bit_of_board(rr, c2);
+                const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+                v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
+            }
+        }
+        col[row * 32 + k] = v;
+    }
+    __syncthreads();
+    PI_STAMP(1);
+    // conv0 + BN + ReLU at the <= 9 positions around the stone (conv0_f16: wave = n-tile)
+    {
+        const Rows r0w = make_rows(cr, cc, 1);
+        const int li = lane & 15, q = lane >> 4, nt = wave;
+        const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
+        const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
+        const int ch0 = nt * 16 + 4 * q;
+        const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
+        const h8 a = *(const h8*)(col + li * 32 + 8 * q);
+        f32x4 acc = zero4();
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
+        if (li < r0w.n) {
+            const int pr = r0w.r0 + li / r0w.wr, pc = r0w.c0 + li % r0w.wr;
+            h4 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = __builtin_fmaf(acc[r], s[r], t[r]);
+                y = y > 0.f ? y : 0.f;
+                const _Float16 h = (_Float16)y;
+                hi[r] = h;
+                lo[r] = (_Float16)(y - (float)h);
+            }
+            const int off = X0.off(ch0, (pr - cr + 3) * 7 + (pc - cc + 3));
+            *(h4*)(X0.hi + off) = hi;
+            *(h4*)(X0.hi + X0.plane() + off) = lo;
+        }
+    }
+    __syncthreads();
+    PI_STAMP(2);
+    child_map_layer<PI_NTW1, 2 / PI_NTW1, false>(X0, Y1, X0, cr, cc, W, 0, wave, lane);  // y1
+    __syncthreads();
+    PI_STAMP(3);
+    child_map_layer<PI_NTW2, 4 / PI_NTW2, true>(Y1, X1, X0, cr, cc, W, 1, wave, lane);  // x1 = relu(.. + x0)
+    __syncthreads();
+    if (!GC && dump >= 0) {  // b has grandchildren: keep its x0 / y1 / x1 squares before Y2 reuses X0 / Y1
+        _Float16* ps = A.patches + (size_t)dump * PATCH_HALVES;
+        patch_dump<3, 1>(X0, ps + PATCH_OFF[0], tid);
+        patch_dump<4, 2>(Y1, ps + PATCH_OFF[1], tid);
+        patch_dump<5, 3>(X1, ps + PATCH_OFF[2], tid);
+        __syncthreads();
+    }
+    PI_STAMP(4);
+    {
+        FillBuf<fill_items(P_Y2)> f3;  // X0 / Y1 are dead
+        fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
+        if (GC) {
+            PatchFill<6, PATCH_R[3]> p3;
+            patch_load(p3, pt + PATCH_OFF[3], 4, cr, cc, r1, c1, tid);
+            patch_store(p3, Y2, cr, cc, r1, c1, tid);
+        }
+        fill_store<6>(f3, Y2, tid);
+    }
+    PI_STAMP(5);
+    child_map_layer<PI_NTW3, 6 / PI_NTW3, false>(X1, Y2, X1, cr, cc, W, 2, wave, lane);  // y2
+    __syncthreads();
+    if (!GC && dump >= 0) patch_dump<6, 4>(Y2, A.patches + (size_t)dump * PATCH_HALVES + PATCH_OFF[3], tid);
+    PI_STAMP(6);
+    child_head_layer<4>(Y2, X1, cr, cc, W, wave, lane, hpart);  // x2 -> head convs
+    __syncthreads();
+    PI_STAMP(7);
+    // b's head-conv record: recomputed positions from hpart (bias first, then the 4
+    // waves' partials in order, as the full kernel), the rest is the parent's
+    {
+        const Rows r4 = make_rows(cr, cc, 5);
+        const float* hr = A.hbuf + (size_t)base * HSTRIDE;
+        float* h = A.hbuf + (size_t)b * HSTRIDE;
+        for (int j = tid; j < HSTRIDE; j += NTC) {
+            float v = hr[j];
+            int pos = -1, which = 0;
+            if (j < POS) {
+                pos = j;
+            } else if (j < 2 * POS) {
+                pos = j - POS;
+                which = 1;
+            } else if (j >= HV_OFF && j < HV_OFF + POS) {
+                pos = j - HV_OFF;
+                which = 2;
+            }
+            if (pos >= 0) {
+                const int pr = pos / BN, pc = pos % BN;
+                if (pr >= r4.r0 && pr < r4.r0 + r4.n / r4.wr && pc >= r4.c0 && pc < r4.c0 + r4.wr) {
+                    const int i = (pr - r4.r0) * r4.wr + (pc - r4.c0);
+                    float acc = which == 0 ? W[P_B] : (which == 1 ? W[P_B + 1] : W[V_B]);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) acc += hpart[(q * 3 + which) * HP_ROWS + i];
+                    v = acc;
+                }
+            }
+            h[j] = v;
+        }
+    }
+    PI_STAMP(8);
+#ifdef GZ_PVINC_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, 1ull);
+#endif
+    // no barrier: the next node writes X0 / Y1 / X1 (read before the last barrier)
+    // and hpart only after several more barriers
+}
+
+// Root children, in leaf order (a root's children follow it in the leaf buffer): a
+// leaf is one iff meta >= 0 names a root with a map slot (ord >= 0).
+__global__ __launch_bounds__(NTC, 1) void pv_child_kernel(TreeArgs A, int n, const int32_t* __restrict__ d_count) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     // XCD-aware order: workgroup g runs on XCD g % 8 (round-robin dispatch); each XCD
     // takes a contiguous eighth of the leaves and its workgroups interleave over it,
@@ -474,149 +739,31 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(const float* __restric
     if (k >= per) return;  // grids that are not a multiple of 8: the remainder idles
     const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
     for (int b = beg; b < end; b += per) {
-        PI_T0();
-        const int rb = __builtin_amdgcn_readfirstlane(meta[b]);
+        const int rb = __builtin_amdgcn_readfirstlane(A.meta[b]);
         if (rb < 0) continue;
-        const int o = __builtin_amdgcn_readfirstlane(ord[rb]);
-        if (o < 0) continue;
-        const int tid = threadIdx.x, lane = tid & 63;
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        // the child's stone: the one bit where its board and the root's differ
-        int cell = 0;
-        const uint32_t* cb = boards + (size_t)b * 16;
-        const uint32_t* rbd = boards + (size_t)rb * 16;
-        for (int k = 0; k < 16; k++) {
-            const uint32_t d = __builtin_amdgcn_readfirstlane(cb[k] ^ rbd[k]);
-            if (d) {
-                const int bit = (k & 7) * 32 + __builtin_ctz(d);
-                cell = (bit >> 4) * BN + (bit & 15);
-            }
-        }
-        const int cr = cell / BN, cc = cell % BN;
-        const _Float16* gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
-        PI_STAMP(0);
-
-        // phase 0: the root's values around the recomputed windows; conv0's im2col
-        {
-            FillBuf<fill_items(P_X0)> f0;
-            FillBuf<fill_items(P_Y1)> f1;
-            FillBuf<fill_items(P_X1)> f2;
-            fill_load<3>(f0, 1, gm, cr, cc, tid);
-            fill_load<4>(f1, 2, gm + PV_MAP_HALVES, cr, cc, tid);
-            fill_load<5>(f2, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid);
-            fill_store<3>(f0, X0, tid);
-            fill_store<4>(f1, Y1, tid);
-            fill_store<5>(f2, X1, tid);
-        }
-        {
-            const Rows r0w = make_rows(cr, cc, 1);
-            const int row = tid >> 5, k = tid & 31;  // 16 rows x 32 k
-            _Float16 v = (_Float16)0.f;
-            if (row < r0w.n && k < 27) {
-                const int pr = r0w.r0 + row / r0w.wr, pc = r0w.c0 + row % r0w.wr;
-                const int tap = k / 3, cin = k % 3;
-                const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
-                if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
-                    const int bit = bit_of_board(rr, c2);
-                    const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
-                    v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
-                }
-            }
-            col[row * 32 + k] = v;
-        }
-        __syncthreads();
-        PI_STAMP(1);
-        // conv0 + BN + ReLU at the <= 9 positions around the stone (conv0_f16: wave = n-tile)
-        {
-            const Rows r0w = make_rows(cr, cc, 1);
-            const int li = lane & 15, q = lane >> 4, nt = wave;
-            const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
-            const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
-            const int ch0 = nt * 16 + 4 * q;
-            const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
-            const h8 a = *(const h8*)(col + li * 32 + 8 * q);
-            f32x4 acc = zero4();
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
-            if (li < r0w.n) {
-                const int pr = r0w.r0 + li / r0w.wr, pc = r0w.c0 + li % r0w.wr;
-                h4 hi, lo;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float y = __builtin_fmaf(acc[r], s[r], t[r]);
-                    y = y > 0.f ? y : 0.f;
-                    const _Float16 h = (_Float16)y;
-                    hi[r] = h;
-                    lo[r] = (_Float16)(y - (float)h);
-                }
-                const int off = X0.off(ch0, (pr - cr + 3) * 7 + (pc - cc + 3));
-                *(h4*)(X0.hi + off) = hi;
-                *(h4*)(X0.hi + X0.plane() + off) = lo;
-            }
-        }
-        __syncthreads();
-        PI_STAMP(2);
-        child_map_layer<PI_NTW1, 2 / PI_NTW1, false>(X0, Y1, X0, cr, cc, W, 0, wave, lane);  // y1
-        __syncthreads();
-        PI_STAMP(3);
-        child_map_layer<PI_NTW2, 4 / PI_NTW2, true>(Y1, X1, X0, cr, cc, W, 1, wave, lane);  // x1 = relu(.. + x0)
-        __syncthreads();
-        PI_STAMP(4);
-        {
-            FillBuf<fill_items(P_Y2)> f3;  // X0 / Y1 are dead
-            fill_load<6>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid);
-            fill_store<6>(f3, Y2, tid);
-        }
-        PI_STAMP(5);
-        child_map_layer<PI_NTW3, 6 / PI_NTW3, false>(X1, Y2, X1, cr, cc, W, 2, wave, lane);  // y2
-        __syncthreads();
-        PI_STAMP(6);
-        child_head_layer<4>(Y2, X1, cr, cc, W, wave, lane, hpart);  // x2 -> head convs
-        __syncthreads();
-        PI_STAMP(7);
-        // the child's head-conv record: recomputed positions from hpart (bias first, then
-        // the 4 waves' partials in order, as the full kernel), the rest is the root's
-        {
-            const Rows r4 = make_rows(cr, cc, 5);
-            const float* hr = hbuf + (size_t)rb * HSTRIDE;
-            float* h = hbuf + (size_t)b * HSTRIDE;
-            for (int j = tid; j < HSTRIDE; j += NTC) {
-                float v = hr[j];
-                int pos = -1, which = 0;
-                if (j < POS) {
-                    pos = j;
-                } else if (j < 2 * POS) {
-                    pos = j - POS;
-                    which = 1;
-                } else if (j >= HV_OFF && j < HV_OFF + POS) {
-                    pos = j - HV_OFF;
-                    which = 2;
-                }
-                if (pos >= 0) {
-                    const int pr = pos / BN, pc = pos % BN;
-                    if (pr >= r4.r0 && pr < r4.r0 + r4.n / r4.wr && pc >= r4.c0 && pc < r4.c0 + r4.wr) {
-                        const int i = (pr - r4.r0) * r4.wr + (pc - r4.c0);
-                        float acc = which == 0 ? W[P_B] : (which == 1 ? W[P_B + 1] : W[V_B]);
-#pragma unroll
-                        for (int q = 0; q < 4; q++) acc += hpart[(q * 3 + which) * HP_ROWS + i];
-                        v = acc;
-                    }
-                }
-                h[j] = v;
-            }
-        }
-        PI_STAMP(8);
-#ifdef GZ_PVINC_STAMPS
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, 1ull);
-#endif
-        // no barrier: the next child writes X0 / Y1 / X1 (read before the last barrier)
-        // and hpart only after several more barriers
+        if (__builtin_amdgcn_readfirstlane(A.ord[rb]) < 0) continue;  // not a root, or a root without maps
+        tree_node<false>(A, lds, b, rb, rb, __builtin_amdgcn_readfirstlane(A.pslot[b]));
     }
 }
 
-// one thread per leaf: roots (meta -1) take the next map slot (ord), others -1
+// Grandchildren (children of root children whose patch was stored), from their list
+__global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const int32_t* __restrict__ list,
+                                                               const int32_t* __restrict__ list_count) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
+    const int count = *list_count;
+    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+        const int b = __builtin_amdgcn_readfirstlane(list[it]);
+        const int p = __builtin_amdgcn_readfirstlane(A.meta[b]);
+        const int rb = __builtin_amdgcn_readfirstlane(A.meta[p]);
+        tree_node<true>(A, lds, b, p, rb, -1);
+    }
+}
+
+// one thread per leaf: roots (meta -1) take the next map slot (ord), others -1;
+// no patch slot yet
 __global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
-                                  int root_cap, int32_t* __restrict__ ord, int32_t* __restrict__ ctr) {
+                                  int root_cap, int32_t* __restrict__ ord, int32_t* __restrict__ pslot,
+                                  int32_t* __restrict__ ctr) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -626,10 +773,34 @@ __global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const
         if (o >= root_cap) o = -1;
     }
     ord[i] = o;
+    pslot[i] = -1;
 }
 
-// lists: roots with a map slot (full forward + maps) and every board that is not
-// the child of such a root (full forward); one atomic per wave and list
+// node classes (ord: roots' map slots): a root child = meta m >= 0 with ord[m] >= 0;
+// a grandchild = meta m >= 0 whose m is such a root child
+__device__ inline bool is_child(const int32_t* meta, const int32_t* ord, int m, int count) {
+    return m >= 0 && m < count && ord[m] >= 0;
+}
+
+// one thread per grandchild: its parent claims a patch slot (first come; -2 while
+// being claimed, -3 once the slots are exhausted)
+__global__ void tree_patch_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
+                                  const int32_t* __restrict__ ord, int patch_cap, int32_t* __restrict__ pslot,
+                                  int32_t* __restrict__ ctr) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int m = meta[i];
+    if (m < 0 || m >= count || !is_child(meta, ord, meta[m], count)) return;
+    if (atomicCAS(&pslot[m], -1, -2) == -1) {
+        const int s = atomicAdd(&ctr[5], 1);
+        pslot[m] = s < patch_cap ? s : -3;
+    }
+}
+
+// lists: roots with a map slot (full forward + maps), grandchildren whose parent
+// has a patch (incremental), every board that is neither these nor a root child
+// (full forward); one atomic per wave and list
 __device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list) {
     const uint64_t m = __ballot(take);
     if (!m) return;
@@ -642,16 +813,19 @@ __device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list
 }
 
 __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
-                                  const int32_t* __restrict__ ord, int32_t* __restrict__ ctr,
-                                  int32_t* __restrict__ roots, int32_t* __restrict__ full) {
+                                  const int32_t* __restrict__ ord, const int32_t* __restrict__ pslot,
+                                  int32_t* __restrict__ ctr, int32_t* __restrict__ roots, int32_t* __restrict__ full,
+                                  int32_t* __restrict__ grand) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < count;
     const int m = valid ? meta[i] : -3;
     const bool root = valid && m == -1 && ord[i] >= 0;
-    const bool child = valid && m >= 0 && m < count && meta[m] == -1 && ord[m] >= 0;
+    const bool child = valid && is_child(meta, ord, m, count);
+    const bool gc = valid && !child && m >= 0 && m < count && is_child(meta, ord, meta[m], count) && pslot[m] >= 0;
     wave_append(root, i, ctr + 1, roots);
-    wave_append(valid && !root && !child, i, ctr + 3, full);
+    wave_append(gc, i, ctr + 4, grand);
+    wave_append(valid && !root && !child && !gc, i, ctr + 3, full);
     const uint64_t c = __ballot(child);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
 }
@@ -663,16 +837,17 @@ extern "C" void gz_internal_set_error(const char* msg);
 // Launches of the incremental forward's own kernels (called by gz_pv_forward_tree in
 // gz_pvnet.hip, which runs the full kernel on the root and full lists in between).
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
-                                         int32_t* d_ord, int32_t* d_ctr, int32_t* d_roots, int32_t* d_children,
-                                         int32_t* d_full, void* stream) {
+                                         int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
+                                         int32_t* d_roots, int32_t* d_full, int32_t* d_grand, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess) {
         gz_internal_set_error("gz_pv_forward_tree: memset");
         return GZ_ERR_HIP;
     }
     const int g = (n + 255) / 256;
-    tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_ctr);
-    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_ctr, d_roots, d_full);
+    tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
+    tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, patch_cap, d_pslot, d_ctr);
+    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_ctr, d_roots, d_full, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("tree classify: ") + hipGetErrorString(e)).c_str());
@@ -682,10 +857,13 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
 }
 
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
-                                         const int32_t* d_ord, int32_t n, const int32_t* d_count,
-                                         const _Float16* d_maps, float* d_hbuf, int grid, void* stream) {
-    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(d_weights, d_boards, d_meta, d_ord, n, d_count, d_maps,
-                                                           d_hbuf);
+                                         const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
+                                         const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
+                                         float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand, int grid,
+                                         void* stream) {
+    TreeArgs A{d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
+    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, n, d_count);
+    pv_grandchild_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_child_kernel: ") + hipGetErrorString(e)).c_str());

@@ -939,44 +939,49 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
 
 // ============================================================ incremental forward (gz_pvinc.hip)
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
-                                         int32_t* d_ord, int32_t* d_ctr, int32_t* d_roots, int32_t* d_children,
-                                         int32_t* d_full, void* stream);
+                                         int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
+                                         int32_t* d_roots, int32_t* d_full, int32_t* d_grand, void* stream);
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
-                                         const int32_t* d_ord, int32_t n, const int32_t* d_count,
-                                         const _Float16* d_maps, float* d_hbuf, int grid, void* stream);
+                                         const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
+                                         const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
+                                         float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand, int grid,
+                                         void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr int PV_PATCH_HALVES = 164 * 256;  // a root child's recomputed squares (gz_pvinc.hip)
+inline int32_t patch_cap_of(int32_t root_cap) { return 32 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;
-    int32_t *ord, *roots, *children, *full, *ctr;
+    int32_t *ord, *pslot, *roots, *full, *grand, *ctr;
     _Float16* maps;
+    _Float16* patches;
 };
-TreeWs tree_carve(void* ws, int32_t n) {
+TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
     char* p = (char*)ws;
     TreeWs t;
     t.hbuf = (float*)p;
     p += al256(m * HSTRIDE * sizeof(float));
-    t.ord = (int32_t*)p;
-    p += al256(m * 4);
-    t.roots = (int32_t*)p;
-    p += al256(m * 4);
-    t.children = (int32_t*)p;
-    p += al256(m * 4);
-    t.full = (int32_t*)p;
-    p += al256(m * 4);
+    int32_t** arrays[5] = {&t.ord, &t.pslot, &t.roots, &t.full, &t.grand};
+    for (auto a : arrays) {
+        *a = (int32_t*)p;
+        p += al256(m * 4);
+    }
     t.ctr = (int32_t*)p;
     p += 256;
     t.maps = (_Float16*)p;
+    p += (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16);
+    t.patches = (_Float16*)p;
     return t;
 }
 }  // namespace
 
 extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
-    return al256(m * HSTRIDE * sizeof(float)) + 4 * al256(m * 4) + 256 +
-           (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16);
+    return al256(m * HSTRIDE * sizeof(float)) + 5 * al256(m * 4) + 256 +
+           (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
+           (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16);
 }
 
 extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
@@ -992,17 +997,20 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     }
     if (n == 0) return GZ_OK;
     hipStream_t s = (hipStream_t)stream;
-    TreeWs t = tree_carve(d_workspace, n);
-    int rc = gz_internal_tree_classify(d_meta, n, d_count, root_cap, t.ord, t.ctr, t.roots, t.children, t.full, stream);
+    TreeWs t = tree_carve(d_workspace, n, root_cap);
+    int rc = gz_internal_tree_classify(d_meta, n, d_count, root_cap, patch_cap_of(root_cap), t.ord, t.pslot, t.ctr,
+                                       t.roots, t.full, t.grand, stream);
     if (rc) return rc;
     const int grid = pv_grid(n);
-    // roots (full forward, maps stored), then every board without a stored root (full
-    // forward), then the roots' children (incremental); ctr = [roots seen, #roots, #children, #full]
+    // roots (full forward, maps stored), then every board without a stored root or
+    // patch (full forward), then the roots' children and their children (incremental);
+    // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed]
     pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
                                                      t.ord, t.maps, root_cap);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
-    rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, n, d_count, t.maps, t.hbuf, grid, stream);
+    rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
+                                   t.grand, t.ctr + 4, grid, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
@@ -1014,10 +1022,11 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     return GZ_OK;
 }
 
-// counts of the last tree forward's lists: [roots seen, roots with maps, children, full]
-extern "C" int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out4, void* stream) {
-    TreeWs t = tree_carve((void*)d_workspace, n);
-    if (hipMemcpyAsync(d_out4, t.ctr, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) {
+// counts of the last tree forward's lists: [roots seen, roots with maps, children, full,
+// grandchildren, patch slots claimed]
+extern "C" int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out6, void* stream) {
+    TreeWs t = tree_carve((void*)d_workspace, n, 0);
+    if (hipMemcpyAsync(d_out6, t.ctr, 6 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) {
         gz_internal_set_error("gz_pv_tree_stats: copy");
         return GZ_ERR_HIP;
     }

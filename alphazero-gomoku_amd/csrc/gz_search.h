@@ -167,8 +167,8 @@ struct LeafSink {
     uint32_t* leaves;
     int32_t cap;
     int32_t* count;
-    int32_t* meta;  // optional, per leaf: -1 root, >= 0 the root's leaf index (a root
-                    // child), -2 any other node (gz_pv_forward_tree)
+    int32_t* meta;  // optional, per leaf: -1 root, >= 0 the parent's leaf index (a root
+                    // child, or a child of one), -2 any other node (gz_pv_forward_tree)
 };
 
 __device__ inline void leaf_meta(const LeafSink& s, int idx, int32_t v) {

@@ -121,8 +121,10 @@ __device__ __forceinline__ int mcts(RootShared* rs, int64_t game_id, const gz_se
     }
     __syncthreads();
     so.predicts = 1 + nonterm;  // root + every non-terminal child runs predict
+    int root_bidx = -1;  // the root's leaf index (the tree forward's tags)
     if (gather) {
         int bidx = leaf_reserve(sink, 1 + nonterm);
+        root_bidx = bidx;
         if (lane == 0) {
             leaf_write(sink, bidx, lds_bb(rs->black), lds_bb(rs->white));
             leaf_meta(sink, bidx, -1);
@@ -318,9 +320,22 @@ __device__ __forceinline__ int mcts(RootShared* rs, int64_t game_id, const gz_se
                     so.predicts++;
                     if (gather) {
                         int bidx = leaf_reserve(sink, 1);
+                        // a child of a root child of the parallel phase: tag it with
+                        // that node's leaf index (root + 1 + its rank among the live
+                        // root children), else -2
+                        int tag = -2;
+                        if (sink.meta && root_bidx >= 0 && x >= 1 && x < n_par) {
+                            int rank = 0;
+                            for (int base = 1; base < x; base += WAVE) {
+                                const int j = base + lane;
+                                rank += __popcll(ballot(j < x && t.term[j] == 0));
+                            }
+                            const int pidx = root_bidx + 1 + rank;
+                            if (pidx < sink.cap) tag = pidx;
+                        }
                         if (lane == 0) {
                             leaf_write(sink, bidx, cbk, cwh);
-                            leaf_meta(sink, bidx, -2);
+                            leaf_meta(sink, bidx, tag);
                         }
                     }
                 }

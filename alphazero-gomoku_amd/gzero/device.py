@@ -213,7 +213,8 @@ def pv_forward(weights, leaf_rows, want_prior=False):
 
 def pv_forward_tree(weights, leaf_rows, meta, root_cap=None):
     """Host convenience for gz_pv_forward_tree: [n,16] uint32 leaf rows and their
-    int32 meta (-1 root, >= 0 the root's index for a root child, -2 other) ->
+    int32 meta (-1 root, >= 0 the parent's index for a root child or a child of
+    one, -2 other) ->
     (logits [n,225], value [n], probs [n,225], prior [n,225], list sizes)."""
     lib = require_gpu()
     rows = np.ascontiguousarray(leaf_rows, np.uint32).reshape(-1, 16)
@@ -230,7 +231,7 @@ def pv_forward_tree(weights, leaf_rows, meta, root_cap=None):
     ws = torch.empty(lib.gz_pv_tree_workspace_bytes(n, root_cap), dtype=torch.uint8, device="cuda")
     _lib.check(lib.gz_pv_forward_tree(ptr(weights.tensor), ptr(d_b), ptr(d_m), n, None, int(root_cap), ptr(d_lg),
                                       ptr(d_v), ptr(d_p), ptr(d_pr), ptr(ws), stream()), "gz_pv_forward_tree")
-    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    st = torch.zeros(6, dtype=torch.int32, device="cuda")
     _lib.check(lib.gz_pv_tree_stats(ptr(ws), n, ptr(st), stream()), "gz_pv_tree_stats")
     torch.cuda.synchronize()
     return (d_lg.cpu().numpy().reshape(n, 225), d_v.cpu().numpy(), d_p.cpu().numpy().reshape(n, 225),

@@ -140,16 +140,17 @@ class SelfPlayEngine:
 
     def tree_stats(self):
         """List sizes of the last tree forward: roots seen, roots with maps,
-        incremental children, full-forward boards (synchronising)."""
-        out = torch.zeros(4, dtype=torch.int32, device="cuda")
+        incremental root children, full-forward boards, incremental grandchildren,
+        patch slots claimed (synchronising)."""
+        out = torch.zeros(6, dtype=torch.int32, device="cuda")
         _lib.check(self.lib.gz_pv_tree_stats(ptr(self.d_tree_ws), self.leaf_cap, ptr(out), stream()),
                    "gz_pv_tree_stats")
         return [int(x) for x in out.cpu()]
 
     def tree_exec_flops(self):
         """(executed MFMA FLOP of the last tree forward, its node count): roots and
-        deeper nodes run the full forward, a root child the row tiles of its windows
-        (csrc/gz_pvinc.hip).  Reads the leaves and tags (synchronising)."""
+        deeper nodes run the full forward, a root child or grandchild the row tiles
+        of its windows (csrc/gz_pvinc.hip).  Reads the leaves and tags (synchronising)."""
         n = min(int(self.counters()["leaves"]), self.leaf_cap)
         rows = self.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
         meta = self.d_meta[:n].cpu().numpy()
@@ -210,7 +211,8 @@ def _window_rows(rc, r):
 def tree_exec_flops(rows, meta):
     """MFMA FLOP the tree forward executes for leaves `rows` ([n,16] uint32) tagged
     `meta`: 2 x (MACs of every 16-row tile it runs), fp32-equivalent like the full
-    forward's 267.38 MFLOP.  A root child at (r, c) runs, per residual conv L = 1..4
+    forward's 267.38 MFLOP.  A tagged node (meta >= 0: a root child or a child of
+    one; assumes no map / patch slot ran out) whose stone is at (r, c) runs, per residual conv L = 1..4
     (window radius L + 1), ceil(rows_L / 16) tiles of 16 positions x 128 channels x
     1152, one conv0 tile, the 1x1 heads at radius 5 and the FC heads."""
     meta = np.asarray(meta)

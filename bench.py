@@ -175,7 +175,7 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         ctr = eng.d_counters.clone()  # per-step counters, stays on the device
         tst = None
         if eng.tree:  # list sizes of the incremental forward (device copy, no sync)
-            tst = torch.zeros(4, dtype=torch.int32, device="cuda")
+            tst = torch.zeros(6, dtype=torch.int32, device="cuda")
             eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream())
         if ex is not None:
             ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
@@ -225,17 +225,21 @@ def roofline_of(m, precision):
     achieved = algorithmic
     tree = None
     if m.get("tree"):
-        t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)  # roots seen, roots w/ maps, children, full
+        # roots seen, roots w/ maps, children, full, grandchildren, patch slots
+        t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)
         # executed MFMA FLOP per board, from the last step's leaves (tree_exec_flops)
         executed = m["exec_per_board"] * mean_leaves
         achieved = executed / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
         tree = {"roots": round(float(t[1]), 1), "children_incremental": round(float(t[2]), 1),
-                "full_other": round(float(t[3]), 1), "child_share": round(float(t[2] / max(1.0, mean_leaves)), 4),
+                "grandchildren_incremental": round(float(t[4]), 1), "patches": round(float(t[5]), 1),
+                "full_other": round(float(t[3]), 1),
+                "child_share": round(float((t[2] + t[4]) / max(1.0, mean_leaves)), 4),
                 "executed_flop_per_launch": round(float(executed), 0),
                 "algorithmic_tflops_full_forward_equivalent": round(algorithmic, 3),
                 "executed_mflop_per_child": round((m["exec_per_board"] * mean_leaves - (t[1] + t[3]) * PV_FLOP)
-                                                  / max(1.0, t[2]) / 1e6, 2),
-                "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child: "
+                                                  / max(1.0, t[2] + t[4]) / 1e6, 2),
+                "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child "
+                         "or grandchild: "
                          "the 16-row tiles of its radius-2..5 windows, clipped at the board edge) / kernel time; "
                          "every node's logits, value, softmax and prior are bit-identical to the full forward's")}
     traffic, _ = load_traffic(mean_leaves, "tree" if m.get("tree") else "full") if precision == "f16x3" \

@@ -5,8 +5,11 @@ stored maps; every recomputed position takes the full kernel's products in the
 full kernel's order, so the outputs -- logits, value, softmax, masked prior --
 must equal the full forward's (gz_pv_forward, f16x3) BIT FOR BIT, for children
 on every cell (corners and edges clip the windows), several roots in one launch,
-deeper nodes (full forward), roots beyond the map capacity (their children fall
-back to the full forward), and the leaves of real 200-simulation searches.
+grandchildren (a child of a root child: its windows come from the root's maps
+overlaid with the parent's recomputed squares) on every cell around parents at
+corners, edges and the centre, deeper nodes (full forward), roots beyond the map
+capacity and parents beyond the patch capacity (full forward), and the leaves of
+real 200-simulation searches.
 """
 import numpy as np
 import pytest
@@ -61,7 +64,7 @@ def test_tree_children_on_every_cell_bitwise(pvw):
         meta.append(-1)
         cells += kids
         meta += [r] * len(kids)
-        for k in kids[:5]:  # grandchildren: two stones from the root -> full forward
+        for k in kids[:5]:  # untagged grandchildren (meta -2) -> full forward
             g = k.copy()
             g[np.flatnonzero(g == 0)[0]] = 3 - (1 if ns % 2 == 0 else 2)
             cells.append(g)
@@ -69,11 +72,84 @@ def test_tree_children_on_every_cell_bitwise(pvw):
     rows = _rows(cells)
     full = device.pv_forward(pvw, rows, want_prior=True)
     tree = device.pv_forward_tree(pvw, rows, meta)
-    assert tree[4] == [3, 3, len(cells) - 3 - 15, 15]
+    assert tree[4] == [3, 3, len(cells) - 3 - 15, 15, 0, 0]
     for name, a, b in zip(("logits", "value", "probs", "prior"), full, tree[:4]):
         bad = np.flatnonzero(~np.all(np.asarray(a).reshape(len(cells), -1) == np.asarray(b).reshape(len(cells), -1),
                                      axis=1))
         assert len(bad) == 0, (name, bad[:10], np.abs(np.asarray(a) - np.asarray(b)).max())
+
+
+def _grand_family(rng, n_stones, parent_cells, every=1):
+    """A root, its children on every empty cell, and for the children whose stone is
+    on `parent_cells` a grandchild (the other side's stone) on every `every`-th empty
+    cell; meta tags as the search writes them."""
+    root, kids = _root_family(rng, n_stones)
+    mover = 1 if n_stones % 2 == 0 else 2
+    empties = np.flatnonzero(root == 0)
+    cells, meta = [root], [-1]
+    cells += kids
+    meta += [0] * len(kids)
+    for pc in parent_cells:
+        if root[pc] != 0:
+            continue
+        p = 1 + int(np.flatnonzero(empties == pc)[0])
+        for c in np.flatnonzero(cells[p] == 0)[::every]:
+            g = cells[p].copy()
+            g[c] = 3 - mover
+            cells.append(g)
+            meta.append(p)
+    return cells, meta
+
+
+def _concat(fams):
+    cells, meta = [], []
+    for c, m in fams:
+        base = len(cells)
+        cells += c
+        meta += [x + base if x >= 0 else x for x in m]
+    return cells, meta
+
+
+def test_tree_grandchildren_every_cell_bitwise(pvw):
+    """Grandchildren on every empty cell around parents at the corners, edges, next
+    to each other and in the centre (parent and grandchild windows overlap, clip,
+    or are disjoint), under 3 roots: tree forward == full forward, bitwise."""
+    from gzero import device
+    rng = np.random.default_rng(SEED + 2)
+    corners = [0, 14, 210, 224]
+    fams = [_grand_family(rng, 6, corners + [112, 113, 97]),
+            _grand_family(rng, 41, [7, 105, 119, 217, 16], every=2),
+            _grand_family(rng, 120, list(range(0, 225, 11)), every=5)]
+    cells, meta = _concat(fams)
+    meta_a = np.asarray(meta)
+    n_kids = sum(1 for i, m in enumerate(meta) if m >= 0 and meta[m] == -1)
+    n_grand = sum(1 for i, m in enumerate(meta) if m >= 0 and meta[m] >= 0)
+    n_par = len(np.unique(meta_a[[i for i, m in enumerate(meta) if m >= 0 and meta[m] >= 0]]))
+    rows = _rows(cells)
+    full = device.pv_forward(pvw, rows, want_prior=True)
+    tree = device.pv_forward_tree(pvw, rows, meta)
+    assert tree[4] == [3, 3, n_kids, 0, n_grand, n_par], (tree[4], n_kids, n_grand, n_par)
+    for name, a, b in zip(("logits", "value", "probs", "prior"), full, tree[:4]):
+        bad = np.flatnonzero(~np.all(np.asarray(a).reshape(len(cells), -1) == np.asarray(b).reshape(len(cells), -1),
+                                     axis=1))
+        assert len(bad) == 0, (name, bad[:10], np.abs(np.asarray(a) - np.asarray(b)).max())
+
+
+def test_tree_patch_capacity_fallback(pvw):
+    """More parents with grandchildren than patch slots (32 per map slot): the
+    grandchildren of parents without a slot take the full forward; results unchanged."""
+    from gzero import device
+    rng = np.random.default_rng(SEED + 3)
+    cells, meta = _concat([_grand_family(rng, 30, list(range(0, 225, 3)), every=60)])
+    n_grand = sum(1 for m in meta if m >= 0 and meta[m] >= 0)
+    n_par = len({m for m in meta if m >= 0 and meta[m] >= 0})
+    assert n_par > 32
+    rows = _rows(cells)
+    full = device.pv_forward(pvw, rows, want_prior=True)
+    tree = device.pv_forward_tree(pvw, rows, meta, root_cap=1)
+    st = tree[4]
+    assert st[5] == n_par and 0 < st[4] < n_grand and st[3] == n_grand - st[4], st
+    assert _same(full, tree[:4])
 
 
 def test_tree_root_capacity_fallback(pvw):
@@ -111,7 +187,8 @@ def test_tree_forward_of_real_searches_bitwise(pvw):
         n = int(c["leaves"])
         assert c["leaves_dropped"] == 0 and 0 < n <= eng.leaf_cap
         st = eng.tree_stats()
-        assert st[1] == st[0] and st[1] + st[2] + st[3] == n and st[2] > 0.5 * n
+        assert st[1] == st[0] and st[1] + st[2] + st[3] + st[4] == n and st[2] > 0.5 * n
+        assert st[4] > 0  # grandchildren of parents with a patch slot
         rows = eng.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
         full = device.pv_forward(pvw, rows, want_prior=True)
         got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),

@@ -40,7 +40,8 @@ def main():
     torch.cuda.synchronize()
     n = int(eng.counters()["leaves"])
     st = eng.tree_stats()
-    print(f"leaves {n}: roots {st[1]}, children {st[2]}, full {st[3]}", flush=True)
+    print(f"leaves {n}: roots {st[1]}, children {st[2]}, grandchildren {st[4]} ({st[5]} patches), full {st[3]}",
+          flush=True)
     lib = eng.lib
     d_count = eng.d_counters[4:8]
 
