@@ -26,6 +26,7 @@
 // convolution's padding).  X0 and Y1 are dead once x1 is computed, so Y2 reuses
 // their space: 62 KB (X1) + 86.5 KB (Y2) + 7 KB.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <string>
 
@@ -235,7 +236,14 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
 #ifndef PI_RING2
 #define PI_RING2 2
 #endif
-    constexpr int RING = NTW == 1 ? 4 : PI_RING2;
+#ifndef PI_RING1
+#define PI_RING1 4
+#endif
+#ifndef PI_RING_L1
+#define PI_RING_L1 PI_RING1
+#endif
+    constexpr int RING = NTW == 1 ? (NMAX <= 2 ? PI_RING_L1 : PI_RING1) : PI_RING2;
+    static_assert(RING == 1 || RING == 2 || RING == 4 || RING == 8, "ring depth");
     h8 b[RING][NTW][2];
 #pragma unroll
     for (int c = 0; c < RING; c++)
@@ -255,8 +263,10 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
         ah[0][m] = *(const h8*)(in.hi + nb[m]);
         al[0][m] = *(const h8*)(lo_plane + nb[m]);
     }
-#pragma unroll 1
-    for (int tap = 0; tap < 9; tap++) {
+    // one tap's 4 k-steps; PAR = tap parity (an 8-deep ring holds two taps: slot =
+    // 4 PAR + cq, so the taps run in unrolled pairs and the indexing stays static)
+    auto tap_body = [&](int tap, auto par) {
+        constexpr int PAR = decltype(par)::value;
 #pragma unroll
         for (int cq = 0; cq < CQ; cq++) {
             const int cur = cq & 1, nxt = cur ^ 1;
@@ -277,7 +287,7 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
                     al[nxt][m] = *(const h8*)(lo_plane + nb[m]);
                 }
             }
-            const int sl = cq % RING;  // static once the cq loop is unrolled
+            const int sl = (RING == 8 ? 4 * PAR : 0) + cq % (RING < 4 ? RING : 4);  // static
 #pragma unroll
             for (int m = 0; m < NT; m++) {
 #pragma unroll
@@ -299,6 +309,17 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
                 b[sl][n][1] = wload(kn, n, 1);
             }
         }
+    };
+    if constexpr (RING == 8) {
+#pragma unroll 1
+        for (int tap = 0; tap < 8; tap += 2) {
+            tap_body(tap, std::integral_constant<int, 0>{});
+            tap_body(tap + 1, std::integral_constant<int, 1>{});
+        }
+        tap_body(8, std::integral_constant<int, 0>{});
+    } else {
+#pragma unroll 1
+        for (int tap = 0; tap < 9; tap++) tap_body(tap, std::integral_constant<int, 0>{});
     }
 }
 
@@ -321,22 +342,43 @@ __device__ __forceinline__ void win_conv(const WI& in, const int (&ctr)[NMAX], i
 }
 
 // Output positions of a wave's tiles: row i of the layer's recomputed square
-// (row-major) -> board (pr, pc); rows past the square recompute row 0 (discarded)
+// (row-major) -> board (pr, pc); rows past the square recompute the tile's first row
+// (discarded).  Lane li of tile t takes row 16 t + perm(li): the permutation of the
+// input window of radius R that spreads a tile's 16 window slots over the LDS banks
+// (ds_read_b128 serves lanes {0-3, 12-15} with {4-11} of the next channel group, and
+// a square row that wraps inside a tile puts two lanes on one bank); found by a
+// local search over every stone cell's tiles, it cuts the modelled LDS cycles per
+// activation read from 8.6 / 8.2 / 9.8 / 9.9 to 7.2 / 7.2 / 7.6 / 7.7 (R = 3..6,
+// conflict-free = 4).  Only the lane <-> row assignment changes: every output is
+// computed exactly as before.  Measured 1 % SLOWER on the tree forward (the layers
+// are not LDS-bound), so off by default (PI_PERM=1 builds it).
+#ifndef PI_PERM
+#define PI_PERM 0
+#endif
+constexpr uint64_t tile_perm(int R) {
+    return !PI_PERM ? 0xfedcba9876543210ull
+                    : R == 3 ? 0xfba980531276e4cdull
+                    : R == 4 ? 0xdb9a742015638fceull
+                    : R == 5 ? 0xabcd50384612e97full
+                             : 0xfb8d534912706aecull;
+}
+
 template <int NMAX>
 struct TilePos {
-    int pr[NMAX], pc[NMAX];
+    int pr[NMAX], pc[NMAX], row[NMAX];
     bool valid[NMAX];
 };
 
-template <int NMAX>
+template <int NMAX, int R>
 __device__ __forceinline__ void tile_positions(const Rows& rows, int t0, int lane, TilePos<NMAX>& tp) {
-    const int li = lane & 15;
+    const int pl = (int)((tile_perm(R) >> (4 * (lane & 15))) & 15ull);
     const float inv = 1.0f / (float)rows.wr;
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
-        int i = (t0 + m) * 16 + li;
+        int i = (t0 + m) * 16 + pl;
+        tp.row[m] = i;
         tp.valid[m] = i < rows.n;
-        if (i >= rows.n) i = 0;
+        if (i >= rows.n) i = (t0 + m) * 16;
         const int rr = (int)(((float)i + 0.5f) * inv);  // exact: i < 256, wr <= 11
         tp.pr[m] = rows.r0 + rr;
         tp.pc[m] = rows.c0 + (i - rr * rows.wr);
@@ -405,7 +447,7 @@ __device__ __forceinline__ void child_map_layer(const WI& in, const WO& out, con
         nt0 = 2 * (wave & 3);
     }
     TilePos<NMAX> tp;
-    tile_positions<NMAX>(rows, t0, lane, tp);
+    tile_positions<NMAX, WI::r>(rows, t0, lane, tp);
     int ctr[NMAX];
     tile_centres<NMAX, WI>(tp, cr, cc, ctr);
     f32x4 acc[NTW][NMAX];
@@ -442,7 +484,7 @@ __device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, in
     const int T0 = (T + 1) >> 1;
     const int t0 = mg ? T0 : 0, nt = mg ? T - T0 : T0;
     TilePos<NMAX> tp;
-    tile_positions<NMAX>(rows, t0, lane, tp);
+    tile_positions<NMAX, WI::r>(rows, t0, lane, tp);
     int ctr[NMAX];
     tile_centres<NMAX, WI>(tp, cr, cc, ctr);
     f32x4 acc[2][NMAX];
@@ -452,7 +494,6 @@ __device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, in
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
     if (nt > 0) win_conv<2, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     const float* R = W + RES0 + layer * RES_STRIDE;
-    const int li = lane & 15;
     float s0[NMAX], s1[NMAX], sv[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
@@ -488,7 +529,7 @@ __device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, in
         a += __shfl_xor(a, 32);
         c += __shfl_xor(c, 32);
         v += __shfl_xor(v, 32);
-        const int i = (t0 + m) * 16 + li;
+        const int i = tp.row[m];
         if (lane < 16 && tp.valid[m]) {
             hpart[(np * 3 + 0) * HP_ROWS + i] = a;
             hpart[(np * 3 + 1) * HP_ROWS + i] = c;
@@ -525,7 +566,15 @@ __device__ __forceinline__ void patch_dump(const Win<R>& x, _Float16* __restrict
     for (int i = tid; i < n; i += NTC) {
         const int pc_ = i / (S * S), loc = i - pc_ * (S * S);  // pc_ = plane * 16 + cg
         const int wl = (loc / S - RC + R) * x.w + (loc % S - RC + R);
-        *(uint4*)(pt + i * 8) = *(const uint4*)(x.hi + (pc_ * x.P + wl) * 8);
+#ifndef PI_PATCH_NT
+#define PI_PATCH_NT 1
+#endif
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = *(const u32x4*)(x.hi + (pc_ * x.P + wl) * 8);
+        if (PI_PATCH_NT)  // streamed out: keeps the roots' maps in L2
+            __builtin_nontemporal_store(v, (u32x4*)(pt + i * 8));
+        else
+            *(u32x4*)(pt + i * 8) = v;
     }
 }
 
@@ -751,7 +800,15 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
                                                                const int32_t* __restrict__ list_count) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_C];
     const int count = *list_count;
-    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+    // XCD-aware, as pv_child_kernel: a contiguous eighth of the list per XCD, so the
+    // grandchildren of one root (adjacent in the list) share that XCD's L2 copy of
+    // the root's maps
+    const int nx = gridDim.x >= 8 ? 8 : 1;
+    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
+    const int chunk = (count + nx - 1) / nx;
+    if (k >= per) return;
+    const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
+    for (int it = beg; it < end; it += per) {
         const int b = __builtin_amdgcn_readfirstlane(list[it]);
         const int p = __builtin_amdgcn_readfirstlane(A.meta[b]);
         const int rb = __builtin_amdgcn_readfirstlane(A.meta[p]);
