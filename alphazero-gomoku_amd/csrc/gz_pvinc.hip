@@ -855,9 +855,10 @@ __global__ void tree_patch_kernel(const int32_t* __restrict__ meta, int n, const
     }
 }
 
-// lists: roots with a map slot (full forward + maps), grandchildren whose parent
-// has a patch (incremental), every board that is neither these nor a root child
-// (full forward); one atomic per wave and list
+// lists: roots with a map slot (full forward + maps), every board that is neither
+// a root child nor a grandchild whose parent has a patch (full forward); one atomic
+// per wave and list.  Grandchildren are chained per parent (ghead / gnext) for
+// tree_grand_order_kernel
 __device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list) {
     const uint64_t m = __ballot(take);
     if (!m) return;
@@ -872,7 +873,7 @@ __device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list
 __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
                                   const int32_t* __restrict__ ord, const int32_t* __restrict__ pslot,
                                   int32_t* __restrict__ ctr, int32_t* __restrict__ roots, int32_t* __restrict__ full,
-                                  int32_t* __restrict__ grand) {
+                                  int32_t* __restrict__ ghead, int32_t* __restrict__ gnext) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < count;
@@ -881,10 +882,40 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
     const bool child = valid && is_child(meta, ord, m, count);
     const bool gc = valid && !child && m >= 0 && m < count && is_child(meta, ord, meta[m], count) && pslot[m] >= 0;
     wave_append(root, i, ctr + 1, roots);
-    wave_append(gc, i, ctr + 4, grand);
     wave_append(valid && !root && !child && !gc, i, ctr + 3, full);
+    if (gc) gnext[i] = atomicExch(&ghead[pslot[m]], i);  // per parent, any order
     const uint64_t c = __ballot(child);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
+}
+
+// the grandchild list in PARENT order: one thread per leaf; a parent with a patch
+// appends its grandchildren (its ghead / gnext chain), a wave's parents in lane
+// order.  A root's children are adjacent leaves, so a root's grandchildren end up
+// adjacent in the list (the search reserves them one by one during its sequential
+// phase, interleaved with every other game's), and pv_grandchild_kernel's
+// XCD-contiguous chunks then keep each root's maps in one L2
+__global__ void tree_grand_order_kernel(int n, const int32_t* __restrict__ d_count, const int32_t* __restrict__ pslot,
+                                        const int32_t* __restrict__ ghead, const int32_t* __restrict__ gnext,
+                                        int32_t* __restrict__ ctr, int32_t* __restrict__ grand) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ps = i < count ? pslot[i] : -1;
+    const int h = ps >= 0 ? ghead[ps] : -1;
+    int k = 0;
+    for (int g = h; g >= 0; g = gnext[g]) k++;
+    // wave prefix sum of k, one atomic per wave
+    const int lane = threadIdx.x & 63;
+    int incl = k;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    int base = 0;
+    if (lane == 63 && total) base = atomicAdd(ctr + 4, total);
+    base = __shfl(base, 63);
+    int at = base + incl - k;
+    for (int g = h; g >= 0; g = gnext[g]) grand[at++] = g;
 }
 
 }  // namespace
@@ -895,16 +926,19 @@ extern "C" void gz_internal_set_error(const char* msg);
 // gz_pvnet.hip, which runs the full kernel on the root and full lists in between).
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
                                          int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
-                                         int32_t* d_roots, int32_t* d_full, int32_t* d_grand, void* stream) {
+                                         int32_t* d_roots, int32_t* d_full, int32_t* d_grand, int32_t* d_ghead,
+                                         int32_t* d_gnext, void* stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess) {
+    if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess ||
+        (patch_cap > 0 && hipMemsetAsync(d_ghead, 0xff, (size_t)patch_cap * sizeof(int32_t), s) != hipSuccess)) {
         gz_internal_set_error("gz_pv_forward_tree: memset");
         return GZ_ERR_HIP;
     }
     const int g = (n + 255) / 256;
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
     tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, patch_cap, d_pslot, d_ctr);
-    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_ctr, d_roots, d_full, d_grand);
+    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_ctr, d_roots, d_full, d_ghead, d_gnext);
+    tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("tree classify: ") + hipGetErrorString(e)).c_str());

@@ -6,23 +6,32 @@ empty board, 200 simulations per move, medium difficulty (c_puct 1.6,
 exploration 0.05), beta = 0, planner_steps = 0, random-init network weights
 (numpy default_rng(0)), continuous refill of finished games.
 
-Measured in steady state: every slot first plays --burn-in plies (default 96)
+Measured in steady state: every slot first plays --burn-in plies (default 600)
 without the PV forward -- the moves are the same, the search never reads the
 priors -- so the timed window sees continuous refill's mix of game plies (opening
-plies included) rather than the synchronised start of 4096 fresh games.
+plies included) rather than the synchronised start of 4096 fresh games (the two
+halves of the timed window agree within 0.3 %).
 
 One "step" = every game slot plays `--plies-per-step` plies (one kernel launch,
 one wavefront per game) followed by the policy-value forward of EVERY node
 those searches created -- the GomokuModel.predict calls the reference makes
-(ai_agent.py:522-523) -- on the MFMA kernel (default: 3-term fp16 split with
-f32 accumulation, within the 1e-4 logit tolerance; --pv-precision fp32 for the
-exact-f32 kernel), and (N > 1) the RCCL
-all-gather of the finished games' (s, pi, z) records.  `value` counts every
-ply played by every rank.
+(ai_agent.py:522-523) -- logits, value, softmax and the masked prior
+(ai_agent.py:564-582), and (N > 1) the sync-free all-gather of the finished
+games' (s, pi, z) records (gzero.dist.RecordExchange, RCCL).  `value` counts
+every ply played by every rank.
 
-Also reported: the roofline of the dominant kernel (the PV forward), the
-prior-elided MCTS-only rate (the search never reads the priors, so moves are
-identical without them), and the C oracle ("port") timed on the host cores.
+The PV forward (default --pv-mode tree) is gz_pv_forward_tree: each search
+root runs the full f16x3 tower (3-term fp16 split on MFMA, f32 accumulate) and
+keeps its maps; each root child and grandchild recomputes only the windows its
+new stone changes, with the full kernel's products in the full kernel's order,
+so every output is bit-identical to the full forward's (--pv-mode full).
+--pv-precision fp32 runs the exact-f32 MFMA kernel.
+
+Also reported: the roofline of the PV forward (executed MFMA FLOP / kernel time,
+and the full-forward-equivalent rate), config 4 (planner plies) and the exact-fp32
+run as labelled secondaries, the prior-elided MCTS-only rate (moves identical
+without the priors), and the CPU baseline: the C oracle + torch-fp32 forwards
+("port") in 16 single-thread processes on the host cores.
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torchrun.
 """
 import argparse
@@ -67,11 +76,15 @@ def load_traffic(boards, mode):
 
 
 def load_clock(kernel):
-    """Measured shader clock and MFMA-busy share of `kernel` under load, or None."""
-    p = os.path.join(REPO, "profiles", "r01", "clock.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f).get("kernels", {}).get(kernel)
+    """Measured shader clock and MFMA-busy share of `kernel` under load (newest
+    profiles/rNN/clock.json that has it), or None."""
+    for rnd in ("r02", "r01"):
+        p = os.path.join(REPO, "profiles", rnd, "clock.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                k = json.load(f).get("kernels", {}).get(kernel)
+            if k:
+                return dict(k, source=f"profiles/{rnd}/clock.json (rocprofv3 GRBM_GUI_ACTIVE / duration)")
     return None
 
 
@@ -267,15 +280,16 @@ def roofline_of(m, precision):
         "note": note,
     }
     if tree:
-        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + deeper nodes, pv_child_kernel on "
-                       "root children, pv_heads_kernel, pv_prior_kernel)")
+        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + untagged nodes, pv_child_kernel on "
+                       "root children, pv_grandchild_kernel on their children, pv_heads_kernel, pv_prior_kernel)")
         r["incremental"] = tree
-    clk = load_clock("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32")
+    dominant = "pv_child_kernel" if tree else ("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32")
+    clk = load_clock(dominant)
     if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
-        r["clock"] = {"ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
+        r["clock"] = {"kernel": dominant, "ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
                       "peak_at_clock": round(peak * clk["median_ghz"] / 2.4, 1),
                       "frac_at_clock": round(achieved / (peak * clk["median_ghz"] / 2.4), 4),
-                      "source": "profiles/r01/clock.json (rocprofv3 GRBM_GUI_ACTIVE / duration)"}
+                      "source": clk["source"]}
     return r
 
 
