@@ -137,8 +137,9 @@ int gz_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t
  * call advances every slot by n_plies plies; a finished game's tuples (with z)
  * are appended to d_records and the slot restarts from the empty board.
  * d_leaf_meta (optional, [leaf_cap] int32) tags every gathered leaf for
- * gz_pv_forward_tree: -1 = a search root, i >= 0 = a child of the root at leaf
- * index i (one stone more), -2 = any deeper node. */
+ * gz_pv_forward_tree: -1 = a search root, i >= 0 = a child of the node at leaf
+ * index i (one stone more; that node is the root or one of its children), -2 =
+ * any deeper node. */
 size_t gz_slot_bytes(int32_t num_simulations);
 int gz_selfplay_init(void* d_slots, int32_t n_slots, int32_t num_simulations, int64_t game_id_base,
                      int64_t game_id_stride, void* stream);
@@ -182,19 +183,22 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
 
 /* Incremental forward of the nodes of MCTS searches (MCTSNode.__init__ ->
  * GomokuModel.predict, ai_agent.py:522-523; neural_network.py:132-159), f16x3:
- * d_meta as written by gz_selfplay_run.  Roots and deeper nodes run the full
+ * d_meta as written by gz_selfplay_run.  Roots and untagged nodes run the full
  * forward (roots also keep their intermediate maps, at most root_cap of them);
  * a root's children recompute only the windows around their one new stone
- * (radius 1..5 per layer) from the root's maps.  Outputs are bit-identical to
+ * (radius 1..5 per layer) from the root's maps, and the children of a root child
+ * (grandchildren) from the root's maps overlaid with their parent's recomputed
+ * squares (at most 32 * root_cap parents).  Outputs are bit-identical to
  * gz_pv_forward(..., GZ_PV_F16X3, ...) of the same boards.  d_workspace:
- * gz_pv_tree_workspace_bytes(n, root_cap) bytes (524 KB per root). */
+ * gz_pv_tree_workspace_bytes(n, root_cap) bytes (~3.3 MB per root: maps 512 KB + 32 patches of 84 KB). */
 size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap);
 int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
                        const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value, float* d_probs,
                        double* d_prior, void* d_workspace, void* stream);
-/* d_out4 (device int32[4]) = the last tree forward's list sizes: roots seen, roots
- * with stored maps, incremental children, full-forward boards. */
-int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out4, void* stream);
+/* d_out6 (device int32[6]) = the last tree forward's list sizes: roots seen, roots
+ * with stored maps, incremental children, full-forward boards, incremental
+ * grandchildren, parents that claimed a patch slot. */
+int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out6, void* stream);
 
 /* ---- K7: BG planner nets (bg_planner.py:22-78, BGPlannerAI.get_move :243-250) ----
  * d_weights: packed blob of gz_gn_weight_floats() floats (csrc/gz_gnet.h,
