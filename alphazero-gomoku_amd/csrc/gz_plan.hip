@@ -43,7 +43,8 @@ struct PlanCtx {  // 256-byte header, then the tree (tree_bytes_for(S))
     int32_t x;      // leaf of the pending sequential simulation
     int32_t n_nodes, predicts, main_draws, move;
     uint32_t dm;
-    int32_t pad[32];
+    int32_t root_leaf;  // the root's leaf index (leaf tags for gz_pv_forward_tree), -1 none
+    int32_t pad[31];
 };
 static_assert(sizeof(PlanCtx) == 256, "ctx header");
 
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
     const int S = p.num_simulations;
     PlanCtx* cx = ctx_at(w, g, S);
     Tree t = ctx_tree(cx, S);
+    if (lane == 0) cx->root_leaf = -1;
     const gz_board_state bs = boards[g];
     BB black, white;
     load_bb(black, bs.black);
@@ -425,7 +427,11 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
                 predicts = 1 + nonterm;
                 if (gather) {
                     const int bidx = leaf_reserve(sink, 1 + nonterm);
-                    if (lane == 0) leaf_write(sink, bidx, black, white);
+                    if (lane == 0) {
+                        leaf_write(sink, bidx, black, white);
+                        leaf_meta(sink, bidx, -1);
+                        cx->root_leaf = bidx;
+                    }
                     int off = 1;
                     for (int base = 1; base < n_par; base += WAVE) {
                         const int j = base + lane;
@@ -437,6 +443,7 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
                             if (player == 1) bb_set(cbk, bit);
                             else bb_set(cwh, bit);
                             leaf_write(sink, bidx + off + rank_in(msk), cbk, cwh);
+                            leaf_meta(sink, bidx + off + rank_in(msk), bidx);
                         }
                         off += __popcll(msk);
                     }
@@ -663,7 +670,22 @@ __global__ __launch_bounds__(WAVE) void plan_resume_kernel(int n, gz_search_para
                     predicts++;
                     if (gather) {
                         const int bidx = leaf_reserve(sink, 1);
-                        if (lane == 0) leaf_write(sink, bidx, cbk, cwh);
+                        // a child of a root child: its parent's leaf index (root + 1 + the
+                        // parent's rank among the live root children), as mcts() does
+                        int tag = -2;
+                        const int rl = cx->root_leaf, np = cx->n_par;
+                        if (sink.meta && rl >= 0 && x >= 1 && x < np) {
+                            int rank = 0;
+                            for (int base = 1; base < x; base += WAVE) {
+                                const int j = base + lane;
+                                rank += __popcll(ballot(j < x && t.term[j] == 0));
+                            }
+                            if (rl + 1 + rank < sink.cap) tag = rl + 1 + rank;
+                        }
+                        if (lane == 0) {
+                            leaf_write(sink, bidx, cbk, cwh);
+                            leaf_meta(sink, bidx, tag);
+                        }
                     }
                 }
                 x = c;
@@ -825,10 +847,12 @@ extern "C" size_t gz_plan_workspace_bytes(int32_t n, int32_t num_simulations) {
     return workspace_bytes(n < 1 ? 1 : n, num_simulations);
 }
 
-extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
-                              const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
-                              void* d_workspace, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
-                              uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, void* stream) {
+// gz_plan_search with optional leaf tags (d_leaf_meta, [leaf_cap]: gz_selfplay_plan_run)
+extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
+                                       const gz_search_params* p, const gz_planner_params* pp,
+                                       const float* d_gn_weights, void* d_workspace, void* d_trees, int32_t* d_moves,
+                                       gz_search_stats* d_stats, uint32_t* d_leaves, int32_t leaf_cap,
+                                       int32_t* d_leaf_count, int32_t* d_leaf_meta, void* stream) {
     if (!p || !pp) return plan_fail(GZ_ERR_ARG, "gz_plan_search: params are NULL");
     if (p->num_simulations < 1 || p->num_simulations > GZ_MAX_SIMULATIONS)
         return plan_fail(GZ_ERR_ARG, "gz_plan_search: num_simulations out of range [1, 4095]");
@@ -845,7 +869,7 @@ extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_g
     hipStream_t s = (hipStream_t)stream;
     const int S = p->num_simulations;
     Workspace w = carve(d_workspace, n, S);
-    LeafSink sink{d_leaves, leaf_cap, d_leaf_count, nullptr};
+    LeafSink sink{d_leaves, leaf_cap, d_leaf_count, gather ? d_leaf_meta : nullptr};
     const int n_jobs = n * S;
     const int jb = (n_jobs + 255) / 256;
     int rc;
@@ -884,6 +908,14 @@ extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_g
     }
     plan_finish_kernel<<<n, WAVE, 0, s>>>(n, S, w, d_moves, d_stats, (char*)d_trees);
     return plan_check("plan_finish_kernel");
+}
+
+extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
+                              const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
+                              void* d_workspace, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
+                              uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, void* stream) {
+    return gz_internal_plan_search(d_boards, d_game_ids, n, p, pp, d_gn_weights, d_workspace, d_trees, d_moves,
+                                   d_stats, d_leaves, leaf_cap, d_leaf_count, nullptr, stream);
 }
 
 extern "C" int gz_planner_move(const gz_board_state* d_boards, const int32_t* d_ai, const uint64_t* d_keys,

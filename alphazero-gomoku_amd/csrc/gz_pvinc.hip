@@ -227,8 +227,14 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
+    // PI_WPROBE (wrong results, timing probe only): 1 = every weight load reads k-step 0
+    // (L1-resident: no weight stream), 2 = only the pair layers' second M half does
+#ifndef PI_WPROBE
+#define PI_WPROBE 0
+#endif
+    const bool wprobe = PI_WPROBE == 1 || (PI_WPROBE == 2 && NTW == 2 && (threadIdx.x >> 8));
     auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (wprobe ? 0 : ks * KS_BYTES) + n * 1024 + lo * LO_BYTES, 0));
     };
     const _Float16* lo_plane = in.hi + in.plane();
     // weight ring: the next 4 k-steps' fragments in flight (an L2 hit takes longer
@@ -706,6 +712,13 @@ __device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, i
     child_map_layer<PI_NTW1, 2 / PI_NTW1, false>(X0, Y1, X0, cr, cc, W, 0, wave, lane);  // y1
     __syncthreads();
     PI_STAMP(3);
+    // Y2's values from the root's map: loaded before x1 so their latency hides behind
+    // it (44 VGPRs held across the layer), stored once X0 / Y1 are dead
+#ifndef PI_Y2EARLY
+#define PI_Y2EARLY 0
+#endif
+    FillBuf<fill_items(P_Y2)> f3;
+    if (PI_Y2EARLY) fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
     child_map_layer<PI_NTW2, 4 / PI_NTW2, true>(Y1, X1, X0, cr, cc, W, 1, wave, lane);  // x1 = relu(.. + x0)
     __syncthreads();
     if (!GC && dump >= 0) {  // b has grandchildren: keep its x0 / y1 / x1 squares before Y2 reuses X0 / Y1
@@ -716,9 +729,8 @@ __device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, i
         __syncthreads();
     }
     PI_STAMP(4);
-    {
-        FillBuf<fill_items(P_Y2)> f3;  // X0 / Y1 are dead
-        fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
+    {  // X0 / Y1 are dead
+        if (!PI_Y2EARLY) fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
         if (GC) {
             PatchFill<6, PATCH_R[3]> p3;
             patch_load(p3, pt + PATCH_OFF[3], 4, cr, cc, r1, c1, tid);

@@ -942,10 +942,17 @@ size_t gz_selfplay_plan_workspace_bytes(int32_t n_slots, int32_t num_simulations
     return a + b + c + gz_plan_workspace_bytes(n_slots, num_simulations);
 }
 
+// gz_plan_search with leaf tags (gz_plan.hip)
+int gz_internal_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
+                            const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
+                            void* d_workspace, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
+                            uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, int32_t* d_leaf_meta,
+                            void* stream);
+
 int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params* p, const gz_planner_params* pp,
                          const float* d_gn_weights, void* d_workspace, int32_t n_plies, gz_record* d_records,
-                         int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, gz_selfplay_counters* d_counters,
-                         void* stream) {
+                         int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_meta,
+                         gz_selfplay_counters* d_counters, void* stream) {
     if (!p || !pp || !d_slots || n_slots <= 0 || n_plies < 0 || !d_counters || !d_records || record_cap < 0 ||
         !d_workspace || !d_gn_weights)
         return fail(GZ_ERR_ARG, "gz_selfplay_plan_run: bad arguments");
@@ -963,8 +970,9 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
         selfplay_boards_kernel<<<(n_slots + 255) / 256, 256, 0, st>>>((const char*)d_slots, n_slots, d_boards, d_gids);
         int rc = check_launch("selfplay_boards_kernel");
         if (rc) return rc;
-        rc = gz_plan_search(d_boards, d_gids, n_slots, p, pp, d_gn_weights, ws, nullptr, d_moves, nullptr,
-                            gather ? d_leaves : nullptr, leaf_cap, gather ? &d_counters->leaves : nullptr, stream);
+        rc = gz_internal_plan_search(d_boards, d_gids, n_slots, p, pp, d_gn_weights, ws, nullptr, d_moves, nullptr,
+                                     gather ? d_leaves : nullptr, leaf_cap, gather ? &d_counters->leaves : nullptr,
+                                     gather ? d_leaf_meta : nullptr, stream);
         if (rc) return rc;
         selfplay_commit_kernel<<<n_slots, WAVE, 0, st>>>((char*)d_slots, n_slots, d_moves, d_records, record_cap,
                                                          d_counters);

@@ -107,7 +107,7 @@ SIGNATURES = {
     "gz_plan_search": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _P]),
     "gz_planner_move_workspace_bytes": (_SZ, [_I32]),
     "gz_selfplay_plan_workspace_bytes": (_SZ, [_I32, _I32]),
-    "gz_selfplay_plan_run": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I32, _P, _I32, _P, _I32, _P, _P]),
+    "gz_selfplay_plan_run": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I32, _P, _I32, _P, _I32, _P, _P, _P]),
     "gz_planner_move": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "gz_knowledge_scores": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
     "gz_dataset_build": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P]),

@@ -31,9 +31,9 @@ class SelfPlayEngine:
         """planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
         planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights.
         pv_mode: "full" = one full forward per node (gz_pv_forward); "tree" = the
-        incremental forward (gz_pv_forward_tree: a root's children recompute only
-        the windows around their new stone; bit-identical outputs; f16x3 and
-        planner_steps == 0 only)."""
+        incremental forward (gz_pv_forward_tree: a root's children and grandchildren
+        recompute only the windows around their new stone; bit-identical outputs;
+        f16x3 only)."""
         self.lib = require_gpu()
         self.n_slots = int(n_slots)
         self.plies_per_step = int(plies_per_step)
@@ -53,8 +53,8 @@ class SelfPlayEngine:
         if pv_mode not in ("full", "tree"):
             raise ValueError(f"pv_mode must be 'full' or 'tree', not {pv_mode!r}")
         self.tree = pv_mode == "tree" and self.gather
-        if self.tree and (self.planner_steps or self.pv_weights.mode != _lib.GZ_PV_F16X3):
-            raise ValueError("pv_mode='tree' needs f16x3 weights and planner_steps == 0")
+        if self.tree and self.pv_weights.mode != _lib.GZ_PV_F16X3:
+            raise ValueError("pv_mode='tree' needs f16x3 weights")
         S = self.params.num_simulations
         slot_bytes = self.lib.gz_slot_bytes(S)
         self.d_slots = torch.zeros(self.n_slots * slot_bytes, dtype=torch.uint8, device="cuda")
@@ -93,8 +93,8 @@ class SelfPlayEngine:
             _lib.check(self.lib.gz_selfplay_plan_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params),
                                                      ctypes.byref(self.pparams), ptr(self.gn_weights.tensor),
                                                      ptr(self.d_plan_ws), n, ptr(self.d_records), self.record_cap,
-                                                     ptr(self.d_leaves), self.leaf_cap, ptr(self.d_counters),
-                                                     stream()), "gz_selfplay_plan_run")
+                                                     ptr(self.d_leaves), self.leaf_cap, ptr(self.d_meta),
+                                                     ptr(self.d_counters), stream()), "gz_selfplay_plan_run")
             return
         _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),

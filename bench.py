@@ -356,8 +356,7 @@ def main():
                               planner_difficulty="medium", gn_weights=gnw if planner_steps else None,
                               pv_mode=mode)
 
-    eng = engine(args.beta, args.planner_steps, w,
-                 args.pv_mode if (args.pv_precision == "f16x3" and not args.planner_steps) else "full")
+    eng = engine(args.beta, args.planner_steps, w, args.pv_mode if args.pv_precision == "f16x3" else "full")
     # N > 1: the per-step RCCL all-gather of finished games' (s, pi, z) records,
     # fixed-size and sync-free (gzero.dist.RecordExchange: counts stay on the device)
     ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda") if ws > 1 else None
@@ -388,7 +387,8 @@ def main():
                              f"{burn_in} burn-in plies: the steady-state mix of game plies); policy-value "
                              "forward + masked prior on every non-terminal node the searches create "
                              f"(reference-work mode, {args.pv_precision}"
-                             + (", incremental forward of root children: bit-identical outputs" if eng.tree else "")
+                             + (", incremental forward of root children and grandchildren: bit-identical outputs"
+                                if eng.tree else "")
                              + ")"),
                 "pv_mode": "tree" if eng.tree else "full",
                 "games_per_gpu": args.slots,
@@ -417,12 +417,13 @@ def main():
 
     # ---- N = 1 secondaries: config 4 and the exact-fp32 forward (same burn-in)
     if ws == 1 and args.config4_steps and not args.planner_steps:
-        e4 = engine(0.2, 5, w)
+        e4 = engine(0.2, 5, w, args.pv_mode if args.pv_precision == "f16x3" else "full")
         m4 = measure(e4, args.config4_steps, 2, burn_in, 1)
         out["config4"] = {
             "value": round(m4["moves"] / m4["T"], 3), "unit": "moves/s", "steps": args.config4_steps, "warmup": 2,
             "ms_per_step": round(m4["T"] / args.config4_steps * 1e3, 3),
             "pv_boards_per_step": round(float(np.mean(m4["leaves"])), 1),
+            "pv_mode": "tree" if e4.tree else "full",
             "workload": (f"BASELINE config 4: {args.slots} games, {args.sims} sims/move, beta 0.2, planner_steps 5 "
                          "(every rollout starts with 5 BGPlannerAI plies: GraphNet + OpponentDQN forward, knowledge "
                          f"search, top-k compose), PV forward + prior on every node; burn-in {burn_in} plies "

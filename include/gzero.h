@@ -148,12 +148,13 @@ int gz_selfplay_run(void* d_slots, int32_t n_slots, const gz_search_params* p, i
                     int32_t* d_leaf_meta, gz_selfplay_counters* d_counters, void* stream);
 /* gz_selfplay_run with BG-planner rollout plies (p->planner_steps > 0): each ply
  * is one gz_plan_search over all slots (host-driven, synchronises the stream
- * once per simulation round) followed by the same record / restart logic.
+ * once per simulation round) followed by the same record / restart logic;
+ * d_leaf_meta (optional) as for gz_selfplay_run.
  * d_workspace: gz_selfplay_plan_workspace_bytes(n_slots, num_simulations). */
 size_t gz_selfplay_plan_workspace_bytes(int32_t n_slots, int32_t num_simulations);
 int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params* p, const gz_planner_params* pp,
                          const float* d_gn_weights, void* d_workspace, int32_t n_plies, gz_record* d_records,
-                         int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap,
+                         int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_meta,
                          gz_selfplay_counters* d_counters, void* stream);
 /* current board of every slot (for inspection / tests) */
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations,

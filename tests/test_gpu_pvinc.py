@@ -194,3 +194,27 @@ def test_tree_forward_of_real_searches_bitwise(pvw):
         got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),
                eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225), eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225))
         assert _same(full, got)
+
+
+def test_tree_forward_of_planner_searches_bitwise(pvw):
+    """Config-4 searches (BG-planner rollout plies, beta 0.2): the planner pipeline
+    tags its leaves like the fused search (root, root children, their children), and
+    the engine's tree forward equals the full forward of the same leaves, bitwise."""
+    from gzero import device, planner_nets
+    from gzero.selfplay import SelfPlayEngine
+    gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
+    eng = SelfPlayEngine(n_slots=64, num_simulations=200, beta=0.2, seed=SEED, pv_weights=pvw, plies_per_step=1,
+                         planner_steps=2, gn_weights=gnw, pv_mode="tree")
+    eng.advance(40)
+    for _ in range(2):
+        eng.step()
+        c = eng.counters()
+        n = int(c["leaves"])
+        assert c["leaves_dropped"] == 0 and 0 < n <= eng.leaf_cap
+        st = eng.tree_stats()
+        assert st[1] == st[0] > 0 and st[1] + st[2] + st[3] + st[4] == n and st[2] > 0.5 * n and st[4] > 0, st
+        rows = eng.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
+        full = device.pv_forward(pvw, rows, want_prior=True)
+        got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),
+               eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225), eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225))
+        assert _same(full, got)
