@@ -951,7 +951,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr int PV_PATCH_HALVES = 164 * 256;  // a root child's recomputed squares (gz_pvinc.hip)
-inline int32_t patch_cap_of(int32_t root_cap) { return 32 * (root_cap < 0 ? 0 : root_cap); }
+inline int32_t patch_cap_of(int32_t root_cap) { return 16 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;
     int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *ghead, *ctr;

@@ -162,11 +162,15 @@ def play_one_game(ai_black, ai_white, step_timeout: float = 10.0,
 
 def selfplay(n_games: int, num_simulations: int = 200, difficulty: str = "medium", beta: float = 0.2,
              seed: int = 0, n_slots: int = 4096, game_id_base: int = 0, model=None,
-             plies_per_step: int = 16, planner_steps: int = 0, planner=None) -> Tuple[SimpleReplay, dict]:
+             plies_per_step: int = 16, planner_steps: int = 0, planner=None,
+             pv_mode: str = "tree") -> Tuple[SimpleReplay, dict]:
     """Play game ids [game_id_base, game_id_base + n_games) concurrently on the GPU.
 
     With ``model`` (a GomokuModel) the policy-value network is evaluated on every
-    node the searches create, as the reference does.  ``planner_steps > 0`` adds
+    node the searches create, as the reference does -- by default incrementally
+    (``pv_mode="tree"``: each root's children and grandchildren recompute only the
+    windows their stone changes, outputs bit-identical; f16x3 models only, at most
+    4 plies per step to bound its workspace).  ``planner_steps > 0`` adds
     BG-planner plies to every rollout (the reference's default AI, planner_steps=5);
     ``planner`` is the BGPlannerAI whose nets they use (a fresh one if None)."""
     from gzero.selfplay import SelfPlayEngine
@@ -178,10 +182,13 @@ def selfplay(n_games: int, num_simulations: int = 200, difficulty: str = "medium
             from bg_planner import BGPlannerAI
             planner = BGPlannerAI(1, difficulty)
         gnw = planner.device_weights()
+    pvw = model.device_weights() if model is not None else None
+    tree = pv_mode == "tree" and pvw is not None and pvw.precision == "f16x3"
     eng = SelfPlayEngine(n_slots=slots, num_simulations=num_simulations, c_puct=c_puct, exploration=expl,
-                         beta=beta, seed=seed, pv_weights=model.device_weights() if model is not None else None,
-                         plies_per_step=plies_per_step, game_id_base=game_id_base, planner_steps=planner_steps,
-                         planner_difficulty=difficulty, gn_weights=gnw)
+                         beta=beta, seed=seed, pv_weights=pvw,
+                         plies_per_step=min(plies_per_step, 4) if tree else plies_per_step,
+                         game_id_base=game_id_base, planner_steps=planner_steps,
+                         planner_difficulty=difficulty, gn_weights=gnw, pv_mode="tree" if tree else "full")
     replay = SimpleReplay()
     done = {}
     moves = 0

@@ -189,9 +189,9 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
  * a root's children recompute only the windows around their one new stone
  * (radius 1..5 per layer) from the root's maps, and the children of a root child
  * (grandchildren) from the root's maps overlaid with their parent's recomputed
- * squares (at most 32 * root_cap parents).  Outputs are bit-identical to
+ * squares (at most 16 * root_cap parents).  Outputs are bit-identical to
  * gz_pv_forward(..., GZ_PV_F16X3, ...) of the same boards.  d_workspace:
- * gz_pv_tree_workspace_bytes(n, root_cap) bytes (~3.3 MB per root: maps 512 KB + 32 patches of 84 KB). */
+ * gz_pv_tree_workspace_bytes(n, root_cap) bytes (~1.9 MB per root: maps 512 KB + 16 patches of 84 KB). */
 size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap);
 int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
                        const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value, float* d_probs,

@@ -136,7 +136,7 @@ def test_tree_grandchildren_every_cell_bitwise(pvw):
 
 
 def test_tree_patch_capacity_fallback(pvw):
-    """More parents with grandchildren than patch slots (32 per map slot): the
+    """More parents with grandchildren than patch slots (16 per map slot): the
     grandchildren of parents without a slot take the full forward; results unchanged."""
     from gzero import device
     rng = np.random.default_rng(SEED + 3)
