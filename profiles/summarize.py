@@ -104,7 +104,8 @@ if PVK and all("hbm_bytes_per_step" in summary["kernels"][k] for k in PVK):
                "pv_mode": bench["config"].get("pv_mode", "full"),
                "note": ("2 x FETCH_SIZE + WRITE_SIZE (tools/hbm_calib.hip calibration), every kernel of one PV "
                         "forward; includes the tower -> heads record (2,816 B written and read per board) and, in "
-                        "tree mode, the roots' stored maps and the children's window reads"),
+                        "tree mode, the roots' stored maps, the children's and grandchildren's window reads and "
+                        "the parents' patches"),
                "kernels": PVK, "source": src},
               open(os.path.join(os.path.dirname(dst.rstrip("/")), "pv_traffic.json"), "w"), indent=1)
 summary["pv_forward"] = pvf
