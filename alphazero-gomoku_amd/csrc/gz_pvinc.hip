@@ -552,18 +552,6 @@ constexpr int PATCH_R[4] = {1, 2, 3, 4};
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // halves
 constexpr int PATCH_HALVES = 164 * 256;
 
-// the stone where boards a and b differ (one bit): cell r*15 + c
-__device__ inline int stone_between(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
-    int cell = 0;
-    for (int k = 0; k < 16; k++) {
-        const uint32_t d = __builtin_amdgcn_readfirstlane(a[k] ^ b[k]);
-        if (d) {
-            const int bit = (k & 7) * 32 + __builtin_ctz(d);
-            cell = (bit >> 4) * BN + (bit & 15);
-        }
-    }
-    return cell;
-}
 
 // copy the square of radius RC around (cr, cc) of window x into patch slot pt
 template <int R, int RC>
@@ -585,6 +573,7 @@ __device__ __forceinline__ void patch_dump(const Win<R>& x, _Float16* __restrict
 }
 
 struct TreeArgs {
+    const int32_t* cinfo;  // per leaf (tree_lists_kernel): -1, or (GC << 30) | (root map slot << 8) | stone cell
     const float* W;
     const uint32_t* boards;
     const int32_t* meta;
@@ -600,7 +589,8 @@ struct TreeArgs {
 // root child base (GC = true: the parent's maps are the root's overlaid with the
 // parent's patch).  dump >= 0: also store b's patch in slot dump (b has grandchildren).
 template <bool GC>
-__device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, int base, int rb, int dump) {
+__device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, int base, int rb, int ci, int c1cell,
+                                          int dump) {
     const float* W = A.W;
     // opaque per node (bit 0: child kernel, bit 1: grandchild kernel): keeps the
     // compiler from hoisting every layer's per-lane weight addresses out of the node
@@ -619,18 +609,17 @@ __device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, i
     float* hpart = (float*)(lds + OFF_HP);
     _Float16* col = (_Float16*)(lds + OFF_COL);
     PI_T0();
-    const int o = __builtin_amdgcn_readfirstlane(A.ord[rb]);
+    const int o = (ci >> 8) & 0x3fffff;  // the root's map slot
     int tid = threadIdx.x;
     if (PI_OPQ_T & (GC ? 2 : 1)) asm volatile("" : "+v"(tid));  // likewise the fills' index arithmetic
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t* cb = A.boards + (size_t)b * 16;
-    const int cell = stone_between(cb, A.boards + (size_t)base * 16);
+    const int cell = ci & 0xff;  // the stone b adds to base (tree_lists_kernel)
     const int cr = cell / BN, cc = cell % BN;
     int r1 = 0, c1 = 0;
     const _Float16* pt = nullptr;
     if (GC) {
-        const int c1cell = stone_between(A.boards + (size_t)base * 16, A.boards + (size_t)rb * 16);
         r1 = c1cell / BN;
         c1 = c1cell % BN;
         pt = A.patches + (size_t)__builtin_amdgcn_readfirstlane(A.pslot[base]) * PATCH_HALVES;
@@ -800,10 +789,12 @@ __global__ __launch_bounds__(NTC, 1) void pv_child_kernel(TreeArgs A, int n, con
     if (k >= per) return;  // grids that are not a multiple of 8: the remainder idles
     const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
     for (int b = beg; b < end; b += per) {
+        // one round of independent loads per leaf: its tag word and parent
+        const int ci = __builtin_amdgcn_readfirstlane(A.cinfo[b]);
         const int rb = __builtin_amdgcn_readfirstlane(A.meta[b]);
-        if (rb < 0) continue;
-        if (__builtin_amdgcn_readfirstlane(A.ord[rb]) < 0) continue;  // not a root, or a root without maps
-        tree_node<false>(A, lds, b, rb, rb, __builtin_amdgcn_readfirstlane(A.pslot[b]));
+        const int ps = __builtin_amdgcn_readfirstlane(A.pslot[b]);
+        if (ci < 0 || (ci & (1 << 30))) continue;  // not a root child with a mapped root
+        tree_node<false>(A, lds, b, rb, rb, ci, 0, ps);
     }
 }
 
@@ -823,8 +814,10 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
     for (int it = beg; it < end; it += per) {
         const int b = __builtin_amdgcn_readfirstlane(list[it]);
         const int p = __builtin_amdgcn_readfirstlane(A.meta[b]);
+        const int ci = __builtin_amdgcn_readfirstlane(A.cinfo[b]);
         const int rb = __builtin_amdgcn_readfirstlane(A.meta[p]);
-        tree_node<true>(A, lds, b, p, rb, -1);
+        const int c1cell = __builtin_amdgcn_readfirstlane(A.cinfo[p]) & 0xff;
+        tree_node<true>(A, lds, b, p, rb, ci, c1cell, -1);
     }
 }
 
@@ -882,10 +875,25 @@ __device__ inline void wave_append(bool take, int i, int32_t* ctr, int32_t* list
     if (take) list[base + __popcll(m & ((1ull << lane) - 1))] = i;
 }
 
+// the cell of the one stone where boards a and b (16-word leaf rows) differ
+__device__ inline int stone_cell(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
+    int cell = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t d = a[k] ^ b[k];
+        if (d) {
+            const int bit = (k & 7) * 32 + __builtin_ctz(d);
+            cell = (bit >> 4) * BN + (bit & 15);
+        }
+    }
+    return cell;
+}
+
 __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
                                   const int32_t* __restrict__ ord, const int32_t* __restrict__ pslot,
-                                  int32_t* __restrict__ ctr, int32_t* __restrict__ roots, int32_t* __restrict__ full,
-                                  int32_t* __restrict__ ghead, int32_t* __restrict__ gnext) {
+                                  const uint32_t* __restrict__ boards, int32_t* __restrict__ ctr,
+                                  int32_t* __restrict__ roots, int32_t* __restrict__ full, int32_t* __restrict__ ghead,
+                                  int32_t* __restrict__ gnext, int32_t* __restrict__ cinfo) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < count;
@@ -896,6 +904,14 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
     wave_append(root, i, ctr + 1, roots);
     wave_append(valid && !root && !child && !gc, i, ctr + 3, full);
     if (gc) gnext[i] = atomicExch(&ghead[pslot[m]], i);  // per parent, any order
+    if (valid) {  // the incremental kernels' per-leaf word: root map slot and stone cell
+        int ci = -1;
+        if (child || gc) {
+            const int o = ord[child ? m : meta[m]];
+            ci = (gc ? 1 << 30 : 0) | (o << 8) | stone_cell(boards + (size_t)i * 16, boards + (size_t)m * 16);
+        }
+        cinfo[i] = ci;
+    }
     const uint64_t c = __ballot(child);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
 }
@@ -939,7 +955,7 @@ extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
                                          int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
                                          int32_t* d_roots, int32_t* d_full, int32_t* d_grand, int32_t* d_ghead,
-                                         int32_t* d_gnext, void* stream) {
+                                         int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess ||
         (patch_cap > 0 && hipMemsetAsync(d_ghead, 0xff, (size_t)patch_cap * sizeof(int32_t), s) != hipSuccess)) {
@@ -949,7 +965,8 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     const int g = (n + 255) / 256;
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
     tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, patch_cap, d_pslot, d_ctr);
-    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_ctr, d_roots, d_full, d_ghead, d_gnext);
+    tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_boards, d_ctr, d_roots, d_full, d_ghead,
+                                        d_gnext, d_cinfo);
     tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -962,9 +979,9 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
-                                         float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand, int grid,
-                                         void* stream) {
-    TreeArgs A{d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
+                                         float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
+                                         const int32_t* d_cinfo, int grid, void* stream) {
+    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
     pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, n, d_count);
     pv_grandchild_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();
