@@ -1,5 +1,5 @@
-// gz_pvinc.hip -- incremental policy-value forward of a search's sibling nodes
-// (AlphaZeroGomokuNet, neural_network.py:74-159, f16x3 precision).
+// gz_pvinc.hip -- incremental policy-value forward of a search's root children and
+// their children (AlphaZeroGomokuNet, neural_network.py:74-159, f16x3 precision).
 //
 // MCTSNode.__init__ runs GomokuModel.predict for every new node (ai_agent.py:
 // 522-523).  A root child differs from the root by one stone at cell m, so in
@@ -17,8 +17,13 @@
 // column operands, so the child's logits, value, softmax and prior are bit for
 // bit those of a full forward of the child's board (tests/test_gpu_pvinc.py).
 //
-// One 512-thread workgroup per child at a time (8 waves, wave = n-tile pair x M
-// half, as the full kernel).  LDS holds the layer inputs as windows around m in
+// Grandchildren (a child of a root child, one more stone at m2): the parent also
+// stores its recomputed squares (its "patch"), and the grandchild's windows are the
+// root's maps overlaid with the parent's patch around the parent's stone; the rest
+// is the same computation around m2 (pv_grandchild_kernel).
+//
+// One 512-thread workgroup per node at a time (8 waves; per layer wave = n-tile, or
+// n-tile pair x M half as the full kernel).  LDS holds the layer inputs as windows around m in
 // the full kernel's hi/lo plane layout ([16 channel groups][P positions][8]):
 //   X0 r3 (7x7)  Y1 r4 (9x9)  X1 r5 (11x11)  Y2 r6 (13x13)
 // -- the input of layer L needs the previous map at radius L+2; positions outside
@@ -42,7 +47,7 @@ using namespace gzc;
 
 constexpr int NTC = 512;
 
-// Phase stamps (tools/pvinc_stamps.py only): -DGZ_PVINC_STAMPS accumulates s_memtime
+// Phase stamps (tools/pvinc_bench.py only): -DGZ_PVINC_STAMPS accumulates s_memtime
 // deltas of workgroup 0 / wave 0 per phase (vector atomics); compiled out otherwise.
 #ifdef GZ_PVINC_STAMPS
 __device__ unsigned long long gz_pvinc_stamps[16];
