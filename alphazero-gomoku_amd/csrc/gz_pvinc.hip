@@ -845,20 +845,31 @@ __global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const
 
 // node classes (ord: roots' map slots): a root child = meta m >= 0 with ord[m] >= 0;
 // a grandchild = meta m >= 0 whose m is such a root child
-__device__ inline bool is_child(const int32_t* meta, const int32_t* ord, int m, int count) {
-    return m >= 0 && m < count && ord[m] >= 0;
+// boards i and j differ in exactly one bit (one cell changed).  The tags are the
+// caller's claim; a leaf whose board does not differ from its tagged parent by one
+// cell simply takes the full forward, so a wrong tag costs time, never results
+__device__ inline bool one_cell(const uint32_t* __restrict__ boards, int i, int j) {
+    int bits = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) bits += __popc(boards[(size_t)i * 16 + k] ^ boards[(size_t)j * 16 + k]);
+    return bits == 1;
+}
+
+// leaf i is a child of the mapped root m
+__device__ inline bool is_child(const int32_t* ord, const uint32_t* boards, int i, int m, int count) {
+    return m >= 0 && m < count && ord[m] >= 0 && one_cell(boards, i, m);
 }
 
 // one thread per grandchild: its parent claims a patch slot (first come; -2 while
 // being claimed, -3 once the slots are exhausted)
 __global__ void tree_patch_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
-                                  const int32_t* __restrict__ ord, int patch_cap, int32_t* __restrict__ pslot,
-                                  int32_t* __restrict__ ctr) {
+                                  const int32_t* __restrict__ ord, const uint32_t* __restrict__ boards, int patch_cap,
+                                  int32_t* __restrict__ pslot, int32_t* __restrict__ ctr) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const int m = meta[i];
-    if (m < 0 || m >= count || !is_child(meta, ord, meta[m], count)) return;
+    if (m < 0 || m >= count || !is_child(ord, boards, m, meta[m], count) || !one_cell(boards, i, m)) return;
     if (atomicCAS(&pslot[m], -1, -2) == -1) {
         const int s = atomicAdd(&ctr[5], 1);
         pslot[m] = s < patch_cap ? s : -3;
@@ -904,8 +915,9 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
     const bool valid = i < count;
     const int m = valid ? meta[i] : -3;
     const bool root = valid && m == -1 && ord[i] >= 0;
-    const bool child = valid && is_child(meta, ord, m, count);
-    const bool gc = valid && !child && m >= 0 && m < count && is_child(meta, ord, meta[m], count) && pslot[m] >= 0;
+    const bool child = valid && is_child(ord, boards, i, m, count);
+    const bool gc = valid && !child && m >= 0 && m < count && pslot[m] >= 0 && is_child(ord, boards, m, meta[m], count) &&
+                    one_cell(boards, i, m);
     wave_append(root, i, ctr + 1, roots);
     wave_append(valid && !root && !child && !gc, i, ctr + 3, full);
     if (gc) gnext[i] = atomicExch(&ghead[pslot[m]], i);  // per parent, any order
@@ -969,7 +981,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     }
     const int g = (n + 255) / 256;
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
-    tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, patch_cap, d_pslot, d_ctr);
+    tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_boards, patch_cap, d_pslot, d_ctr);
     tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_boards, d_ctr, d_roots, d_full, d_ghead,
                                         d_gnext, d_cinfo);
     tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);

@@ -189,8 +189,10 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
  * a root's children recompute only the windows around their one new stone
  * (radius 1..5 per layer) from the root's maps, and the children of a root child
  * (grandchildren) from the root's maps overlaid with their parent's recomputed
- * squares (at most 16 * root_cap parents).  Outputs are bit-identical to
- * gz_pv_forward(..., GZ_PV_F16X3, ...) of the same boards.  d_workspace:
+ * squares (at most 16 * root_cap parents).  A tag whose board does not differ
+ * from its parent's by exactly one cell is ignored (full forward), so the tags
+ * only decide speed.  Outputs are bit-identical to gz_pv_forward(...,
+ * GZ_PV_F16X3, ...) of the same boards.  d_workspace:
  * gz_pv_tree_workspace_bytes(n, root_cap) bytes (~1.9 MB per root: maps 512 KB + 16 patches of 84 KB). */
 size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap);
 int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,

@@ -218,3 +218,43 @@ def test_tree_forward_of_planner_searches_bitwise(pvw):
         got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),
                eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225), eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225))
         assert _same(full, got)
+
+
+def test_tree_wrong_tags_take_the_full_forward(pvw):
+    """The tags are the caller's claim: a 'child' two stones from its root, a
+    'grandchild' of such a node, and a node tagged with a non-root, non-child
+    parent take the full forward -- the outputs stay bitwise those of the full
+    forward; only the valid children are incremental."""
+    from gzero import device
+    rng = np.random.default_rng(SEED + 4)
+    root, kids = _root_family(rng, 20)
+    mover = 1  # 20 stones: black to move
+    cells, meta = [root], [-1]
+    cells += kids[:40]
+    meta += [0] * 40
+    bad = []
+    for k in kids[40:50]:  # two stones more than the root, tagged as its children
+        g = k.copy()
+        g[np.flatnonzero(g == 0)[0]] = 3 - mover
+        bad.append(len(cells))
+        cells.append(g)
+        meta.append(0)
+    for p in bad[:3]:  # children of the invalid nodes
+        g = cells[p].copy()
+        g[np.flatnonzero(g == 0)[-1]] = mover
+        cells.append(g)
+        meta.append(p)
+    g = cells[1].copy()  # valid grandchild of a valid child ...
+    g[np.flatnonzero(g == 0)[-1]] = 3 - mover
+    cells.append(g)
+    meta.append(1)
+    g2 = g.copy()  # ... and a node tagged with that grandchild as its parent (depth 3)
+    g2[np.flatnonzero(g2 == 0)[-1]] = mover
+    cells.append(g2)
+    meta.append(len(cells) - 2)
+    rows = _rows(cells)
+    full = device.pv_forward(pvw, rows, want_prior=True)
+    tree = device.pv_forward_tree(pvw, rows, meta)
+    st = tree[4]
+    assert st[:5] == [1, 1, 40, 10 + 3 + 1, 1], st
+    assert _same(full, tree[:4])
