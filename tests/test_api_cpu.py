@@ -91,3 +91,39 @@ def test_device_paths_fail_loudly_without_gpu():
     ai = AlphaZeroGomokuAI(1, planner_steps=0, seed=1)
     with pytest.raises(_lib.GzeroUnavailable):
         ai.get_move(GomokuBoard())
+
+
+def test_tree_exec_flops_counts_window_tiles():
+    """bench.py's executed-FLOP count of the tree forward (gzero.selfplay.tree_exec_flops):
+    a root costs a full forward; a tagged node whose stone is at (r, c) runs, per
+    residual conv L = 1..4, ceil(rows / 16) tiles over the radius-(L+1) square clipped
+    to the board, plus conv0, the 1x1 heads at radius 5 and the FC heads -- counted
+    here by brute force over the squares."""
+    from gzero import boards
+    from gzero.selfplay import PV_FLOP_FULL, tree_exec_flops
+
+    def macs(r, c):
+        m = 0
+        for L in range(1, 5):
+            rows = sum(1 for pr in range(15) for pc in range(15) if abs(pr - r) <= L + 1 and abs(pc - c) <= L + 1)
+            m += -(-rows // 16) * 16 * 128 * 1152
+        n5 = sum(1 for pr in range(15) for pc in range(15) if abs(pr - r) <= 5 and abs(pc - c) <= 5)
+        return m + 16 * 128 * 27 + n5 * 128 * 3 + 450 * 225 + 225 * 64 + 64
+
+    root = np.zeros(225, np.int8)
+    root[[112, 113]] = [1, 2]
+    cells, meta, want = [root], [-1], float(PV_FLOP_FULL)
+    for cell in (0, 7, 14, 100, 112 - 15, 224):
+        if root[cell]:
+            continue
+        k = root.copy()
+        k[cell] = 1
+        cells.append(k)
+        meta.append(0)
+        want += 2.0 * macs(cell // 15, cell % 15)
+    cells.append(root.copy())
+    meta.append(-2)  # an untagged node: a full forward
+    want += PV_FLOP_FULL
+    bl, wh = boards.cells_to_words(np.asarray(cells, np.int8))
+    rows = boards.leaf_words(bl, wh)
+    assert tree_exec_flops(rows, np.asarray(meta)) == pytest.approx(want, rel=1e-12)
