@@ -237,6 +237,9 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
 #ifndef PI_WPROBE
 #define PI_WPROBE 0
 #endif
+#if PI_WPROBE
+#warning "PI_WPROBE is a timing probe: the tree forward's results are wrong in this build"
+#endif
     const bool wprobe = PI_WPROBE == 1 || (PI_WPROBE == 2 && NTW == 2 && (threadIdx.x >> 8));
     auto wload = [&](int ks, int n, int lo) -> h8 {
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (wprobe ? 0 : ks * KS_BYTES) + n * 1024 + lo * LO_BYTES, 0));
