@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 #include <type_traits>
 
+#include <cstdlib>
 #include <string>
 
 #include "gz_f16conv.h"
@@ -136,9 +137,9 @@ __device__ __forceinline__ void fill_load(FillBuf<IT>& f, int rc, const _Float16
         const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
         const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
         bool keep = i < n && !(on && dr <= rc && dc <= rc);  // else the layer that recomputes it writes it
-        if (GC) {
+        if (GC) {  // on-board positions of the parent's square come from its patch (off-board: zeros here)
             const int er = pr > r1 ? pr - r1 : r1 - pr, ec = pc > c1 ? pc - c1 : c1 - pc;
-            keep = keep && !(er <= rcp && ec <= rcp);
+            keep = keep && !(on && er <= rcp && ec <= rcp);
         }
         const int off = (keep && on) ? (plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8) * 2 : 0;
         f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -171,7 +172,9 @@ __device__ __forceinline__ void patch_load(PatchFill<R, RC>& f, const _Float16* 
         const int wr = pr - cr + R, wc = pc - cc + R;
         const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
         const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-        const bool put = i < F::n && wr >= 0 && wr <= 2 * R && wc >= 0 && wc <= 2 * R && !(on && dr <= rc && dc <= rc);
+        // off-board entries of a patch are never read (the window fill stores zeros there),
+        // so a patch need only hold its on-board positions
+        const bool put = i < F::n && on && wr >= 0 && wr <= 2 * R && wc >= 0 && wc <= 2 * R && !(dr <= rc && dc <= rc);
         f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i < F::n ? i : 0) * 16, 0, 0));
         f.put |= put ? (1u << k) : 0u;
     }
@@ -343,7 +346,7 @@ __device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX]
 template <int NTW, int NMAX, class WI>
 __device__ __forceinline__ void win_conv(const WI& in, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
                                          int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
-    static_assert(NMAX >= 1 && NMAX <= 6, "tile counts");
+    static_assert(NMAX >= 1 && NMAX <= 12, "tile counts");
     switch (nt) {
         case 1: win_conv_nt<NTW, 1, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
         case 2: if constexpr (NMAX >= 2) win_conv_nt<NTW, 2, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
@@ -351,6 +354,12 @@ __device__ __forceinline__ void win_conv(const WI& in, const int (&ctr)[NMAX], i
         case 4: if constexpr (NMAX >= 4) win_conv_nt<NTW, 4, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
         case 5: if constexpr (NMAX >= 5) win_conv_nt<NTW, 5, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
         case 6: if constexpr (NMAX >= 6) win_conv_nt<NTW, 6, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 7: if constexpr (NMAX >= 7) win_conv_nt<NTW, 7, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 8: if constexpr (NMAX >= 8) win_conv_nt<NTW, 8, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 9: if constexpr (NMAX >= 9) win_conv_nt<NTW, 9, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 10: if constexpr (NMAX >= 10) win_conv_nt<NTW, 10, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 11: if constexpr (NMAX >= 11) win_conv_nt<NTW, 11, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
+        case 12: if constexpr (NMAX >= 12) win_conv_nt<NTW, 12, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
         default: break;
     }
 }
@@ -829,6 +838,708 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
     }
 }
 
+// ============================================================ sibling-batched incremental forward
+// pv_sib_kernel: the same node computation as tree_node, scheduled so that one pass
+// over a layer's weights serves several nodes.  tree_node streams each layer's 576 KB
+// of hi/lo weight fragments from L2 once per node (twice on the pair layers) for 25-121
+// output rows, which made pv_child_kernel bound by the L2 -> CU rate (3.86 MB per node,
+// MFMA busy 0.44).  Here a workgroup takes a chunk of up to SIB_G consecutive nodes (a
+// root's children are adjacent leaves, so a chunk usually shares one root) and runs the
+// tower layer-major over the chunk:
+//   y1: one pass over all 6 nodes (6 X0 r3 windows in LDS, up to 150 rows)
+//   x1: two passes of 3 (Y1 r4 windows), y2: three passes of 2 (X1 r5), x2 + heads: 1 (Y2 r6)
+// The rows of a pass are the nodes' recomputed squares packed back to back in 16-row
+// M tiles (no per-node tile padding).  Each node's recomputed squares (x0 r1, y1 r2, x1
+// r3, y2 r4: the patch layout) go to global memory between layers -- into its patch
+// slot if it has grandchildren, else into the workgroup's scratch -- and the next
+// layer's windows are filled from the root's maps overlaid with them.  Four waves, one
+// per SIMD: wave np owns n-tiles {2np, 2np+1} over ALL M tiles of the pass, so each
+// weight fragment is read once per pass and each activation fragment feeds 6 MFMAs.
+// Weight bytes per node: 576 KB x (1/6 + 1/3 + 1/2 + 1) = 1.15 MB (was 3.7 MB).
+// Every output element takes the full kernel's products in the full kernel's order
+// (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
+// those of the full forward.
+constexpr int NTS = 256;
+constexpr int SIB_G = 6;
+constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
+static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
+constexpr int SIB_HP = SIB_WIN;                     // head partials [4 pairs][3][HP_ROWS]
+constexpr int SIB_U = SIB_HP + 4 * 3 * HP_ROWS * 4;  // unit table
+constexpr int LDS_S = SIB_U + SIB_G * 128;  // SibUnit: 128 B
+static_assert(LDS_S <= 160 * 1024, "LDS budget");
+
+// phase stamps of pv_sib_kernel (workgroup 0, thread 0; -DGZ_PVINC_STAMPS builds only)
+struct SibStamp {
+#ifdef GZ_PVINC_STAMPS
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    __device__ void operator()(int i) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+            atomicAdd(&gz_pvinc_stamps[i], t_ - t);
+            t = t_;
+        }
+    }
+#else
+    __device__ void operator()(int) {}
+#endif
+};
+
+struct SibUnit {
+    const _Float16* gm;   // the root's maps x0, y1, x1, y2
+    _Float16* own;        // this node's recomputed squares (patch layout)
+    const _Float16* par;  // grandchild: the parent's patch
+    int leaf, base, cell, pcell;  // node, record base (root / parent), stone, parent's stone
+    int pad[6];
+    uint32_t board[16];   // the node's bit-plane board (conv0's input)
+};
+static_assert(sizeof(SibUnit) == 128, "unit size");
+
+__device__ inline int iabs(int x) { return x < 0 ? -x : x; }
+
+// The value of map MAP (0..3 = x0, y1, x1, y2) at on-board position (pr, pc) for unit
+// u, channels ch0..ch0+3: the node's own recomputed square (radius MAP+1 around its
+// stone), a grandchild's parent's square, else the root's map.  hi and lo pointers.
+template <int MAP, bool GC>
+__device__ __forceinline__ void map_src(const SibUnit& u, int pr, int pc, int ch0, const _Float16*& hi,
+                                        const _Float16*& lo) {
+    constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
+    const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+    if (iabs(pr - cr) <= rc && iabs(pc - cc) <= rc) {
+        hi = u.own + PATCH_OFF[MAP] + ((ch0 >> 3) * SS + (pr - cr + rc) * S + (pc - cc + rc)) * 8 + (ch0 & 7);
+        lo = hi + 16 * SS * 8;
+        return;
+    }
+    if (GC) {
+        const int r1 = u.pcell / BN, c1 = u.pcell - (u.pcell / BN) * BN;
+        if (iabs(pr - r1) <= rc && iabs(pc - c1) <= rc) {
+            hi = u.par + PATCH_OFF[MAP] + ((ch0 >> 3) * SS + (pr - r1 + rc) * S + (pc - c1 + rc)) * 8 + (ch0 & 7);
+            lo = hi + 16 * SS * 8;
+            return;
+        }
+    }
+    hi = u.gm + MAP * PV_MAP_HALVES + ((ch0 >> 3) * 256 + pr * BN + pc) * 8 + (ch0 & 7);
+    lo = hi + PV_MAP_PLANE;
+}
+
+// Windows (radius R = MAP + 3) of map MAP for units [u0, u0 + ng) at LDS offset 0, one
+// after another in the [plane][16 cg][P][8] layout: each position from map_src, zeros
+// (a zero source) off the board.  LDS-DMA (global_load_lds_dwordx4: item i of a unit's
+// window lands at byte 16 i, wave-uniform base + 16 lane), so a fill holds no
+// registers and all its loads are in flight at once; the caller's __syncthreads drains
+// it.  Unit by unit, with the unit's fields in scalar registers.  The x0 windows (MAP
+// 0) load the root's values at the node's own square too; conv0 overwrites them
+// after the barrier.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+__device__ uint4 gz_sib_zero16[1];  // zero-initialised
+
+// uniform copy of a unit's fields (SGPRs)
+struct SibU {
+    const _Float16 *gm, *own, *par;
+    int cr, cc, r1, c1;
+};
+__device__ __forceinline__ const _Float16* rfl_ptr(const _Float16* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const _Float16*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ SibU sib_uniform(const SibUnit& u) {
+    SibU s;
+    s.gm = rfl_ptr(u.gm);
+    s.own = rfl_ptr(u.own);
+    s.par = rfl_ptr(u.par);
+    const int cell = __builtin_amdgcn_readfirstlane(u.cell), pcell = __builtin_amdgcn_readfirstlane(u.pcell);
+    s.cr = cell / BN;
+    s.cc = cell - s.cr * BN;
+    s.r1 = pcell / BN;
+    s.c1 = pcell - s.r1 * BN;
+    return s;
+}
+
+template <int MAP, bool GC>
+__device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, int ng, int tid) {
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P, IT = (PER + NTS - 1) / NTS;
+    constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
+    const int wb = tid & ~63;
+    for (int g = 0; g < ng; g++) {
+        const SibU u = sib_uniform(U[u0 + g]);
+        char* dst = lds + (size_t)g * PER * 16;
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = tid + k * NTS;
+            if ((k + 1) * NTS > PER && i >= PER) continue;  // past this unit's window (EXEC-masked)
+            const int pcg = i / P, loc = i - pcg * P;        // pcg = plane * 16 + cg
+            const int dr = loc / Wd - R, dc = loc % Wd - R;  // relative to the stone
+            const int pr = u.cr + dr, pc = u.cc + dc;
+            const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+            const bool own = on && iabs(dr) <= rc && iabs(dc) <= rc;
+            const void* src = on ? (const void*)(u.gm + MAP * PV_MAP_HALVES + (pcg >> 4) * PV_MAP_PLANE +
+                                                 ((pcg & 15) * 256 + pr * BN + pc) * 8)
+                                 : (const void*)gz_sib_zero16;
+            if (MAP > 0 && own) src = u.own + PATCH_OFF[MAP] + (pcg * SS + (dr + rc) * S + (dc + rc)) * 8;
+            if (GC && on && !own && iabs(pr - u.r1) <= rc && iabs(pc - u.c1) <= rc)
+                src = u.par + PATCH_OFF[MAP] + (pcg * SS + (pr - u.r1 + rc) * S + (pc - u.c1 + rc)) * 8;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + (size_t)(wb + k * NTS) * 16), 16, 0, 0);
+        }
+    }
+}
+
+// The k-loop of a pass for the wave's n-tiles {nt0, nt0+1} over NT M tiles: win_conv_nt's
+// k-steps, products and accumulation order, with one wave per SIMD: each tile's
+// activation fragments for the next k-step are read right after its MFMAs (the other
+// tiles' MFMAs cover the LDS latency), weight fragments 4 k-steps ahead.  act = the
+// pass's windows (each [plane][16 cg][P][8]); ctr[m] = the lane's window-local row
+// (unit offset included).
+#ifndef SIB_RING
+#define SIB_RING 4
+#endif
+template <int NT, int NMAX, int R>
+__device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
+                                            int nt0, int lane, f32x4 (&acc)[2][NMAX]) {
+    constexpr int Wd = 2 * R + 1, P = Wd * Wd, CQ = 4, KS = 9 * CQ, PLANE = 16 * P * 8;
+    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES, RING = SIB_RING;
+    static_assert(RING == 4, "ring depth");
+    // Weight fragments 3 k-steps ahead: at the START of k-step j, k-step j + 3 is loaded
+    // into the slot k-step j - 1 has just released.  So at the tap loop's back-edge --
+    // where the compiler waits for every outstanding load (vmcnt(0)) -- the newest
+    // loads were issued a whole k-step of MFMAs earlier.
+    const int q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = (nt0 * 64 + lane) * 16;
+    auto wload = [&](int ks, int n, int lo) -> h8 {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+    };
+    h8 b[RING][2][2];
+#pragma unroll
+    for (int c = 0; c < RING - 1; c++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            b[c][n][0] = wload(c, n, 0);
+            b[c][n][1] = wload(c, n, 1);
+        }
+    // the accumulators as an exact-size local array (the caller's has NMAX entries):
+    // keeps the register allocator from shuffling partial tuples inside the loop
+    f32x4 c[2][NT];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NT; m++) c[n][m] = acc[n][m];
+    int nb[NT];
+    h8 ah[NT], al[NT];
+#pragma unroll
+    for (int m = 0; m < NT; m++) {
+        nb[m] = (ctr[m] - Wd - 1 + q * P) * 8;  // tap 0 = (-1, -1)
+        ah[m] = *(const h8*)(act + nb[m]);
+        al[m] = *(const h8*)(act + PLANE + nb[m]);
+    }
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap++) {
+        const int t2 = tap + 1 < 9 ? tap + 1 : 0;  // past the last tap: tap 0 again (unused)
+        const int toff = (t2 / 3 - 1) * Wd + (t2 % 3 - 1);
+#pragma unroll
+        for (int cq = 0; cq < CQ; cq++) {
+            const int sl = cq, sr = (cq + 3) & 3;
+            {  // k-step ks + 3 into the slot of ks - 1 (past the end: the first k-steps again, unused)
+                const int ksr = tap * CQ + cq + 3;
+                const int kn = ksr < KS ? ksr : ksr - KS;
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    b[sr][n][0] = wload(kn, n, 0);
+                    b[sr][n][1] = wload(kn, n, 1);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[m], c[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[m], c[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[m], c[n][m], 0, 0, 0);
+                int o;
+                if (cq < CQ - 1) {
+                    o = nb[m] + (cq + 1) * 4 * P * 8;
+                } else {
+                    nb[m] = (ctr[m] + toff + q * P) * 8;
+                    o = nb[m];
+                }
+                ah[m] = *(const h8*)(act + o);
+                al[m] = *(const h8*)(act + PLANE + o);
+            }
+            // pin the order (the default scheduler sinks each read to its use and then
+            // waits for it there): the weight refill, then per tile its 6 MFMAs and its
+            // 2 reads for the next k-step
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);  // VMEM read
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NT; m++) acc[n][m] = c[n][m];
+}
+
+template <int NMAX, int R>
+__device__ __forceinline__ void sib_conv(const _Float16* act, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
+                                         int nt0, int lane, f32x4 (&acc)[2][NMAX]) {
+    static_assert(NMAX >= 1 && NMAX <= 12, "tile counts");
+    switch (nt) {
+        case 1: sib_conv_nt<1, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 2: if constexpr (NMAX >= 2) sib_conv_nt<2, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 3: if constexpr (NMAX >= 3) sib_conv_nt<3, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 4: if constexpr (NMAX >= 4) sib_conv_nt<4, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 5: if constexpr (NMAX >= 5) sib_conv_nt<5, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 6: if constexpr (NMAX >= 6) sib_conv_nt<6, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 7: if constexpr (NMAX >= 7) sib_conv_nt<7, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 8: if constexpr (NMAX >= 8) sib_conv_nt<8, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 9: if constexpr (NMAX >= 9) sib_conv_nt<9, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 10: if constexpr (NMAX >= 10) sib_conv_nt<10, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 11: if constexpr (NMAX >= 11) sib_conv_nt<11, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        case 12: if constexpr (NMAX >= 12) sib_conv_nt<12, NMAX, R>(act, ctr, Wf, nt0, lane, acc); break;
+        default: break;
+    }
+}
+
+// conv0 + BN + ReLU at the <= 9 positions around each unit's stone (the im2col of the
+// node's board built per lane: row li, k = 8q..8q+7, exactly the columns tree_node
+// stages in LDS), wave np: n-tiles 2np, 2np+1; into the unit's X0 window and its x0 square
+template <int G>
+__device__ __forceinline__ void sib_conv0(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
+                                          int lane) {
+    const int li = lane & 15, q = lane >> 4;
+    constexpr int WIN = wbytes(P_X0) / 2;  // halves per X0 window
+    h8 wh[2], wl[2];
+    f32x4 ws[2], wt[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int nt = 2 * np + n, ch0 = nt * 16 + 4 * q;
+        const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
+        wh[n] = *(const h8*)wf;
+        wl[n] = *(const h8*)(wf + 8 * 64 * 8);
+        ws[n] = *(const f32x4*)(W + C0_S + ch0);
+        wt[n] = *(const f32x4*)(W + C0_T + ch0);
+    }
+    for (int g = 0; g < ng; g++) {
+        const SibUnit& u = U[g];
+        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+        const Rows r0w = make_rows(cr, cc, 1);
+        const uint32_t* cb = u.board;
+        const bool rowok = li < r0w.n;
+        const int pr = rowok ? r0w.r0 + li / r0w.wr : 0, pc = rowok ? r0w.c0 + li % r0w.wr : 0;
+        h8 a;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = 8 * q + j;
+            float v = 0.f;
+            if (rowok && k < 27) {
+                const int tap = k / 3, cin = k % 3;
+                const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
+                if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
+                    const int bit = bit_of_board(rr, c2);
+                    const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+                    v = (float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
+                }
+            }
+            a[j] = (_Float16)v;
+        }
+        _Float16* xw = (_Float16*)lds + g * WIN;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int nt = 2 * np + n;
+            const int ch0 = nt * 16 + 4 * q;
+            const f32x4 s = ws[n], t = wt[n];
+            f32x4 acc = zero4();
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a, acc, 0, 0, 0);
+            if (rowok) {
+                h4 hi, lo;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float y = __builtin_fmaf(acc[r], s[r], t[r]);
+                    y = y > 0.f ? y : 0.f;
+                    const _Float16 h = (_Float16)y;
+                    hi[r] = h;
+                    lo[r] = (_Float16)(y - (float)h);
+                }
+                const int off = Win<3>::off(ch0, (pr - cr + 3) * 7 + (pc - cc + 3));
+                *(h4*)(xw + off) = hi;
+                *(h4*)(xw + Win<3>::plane() + off) = lo;
+                _Float16* d = u.own + PATCH_OFF[0] + ((ch0 >> 3) * 9 + (pr - cr + 1) * 3 + (pc - cc + 1)) * 8 + (ch0 & 7);
+                *(h4*)d = hi;
+                *(h4*)(d + 16 * 9 * 8) = lo;
+            }
+        }
+    }
+}
+
+// The rows of a pass: units u0 .. u0+ng-1 in order, each its recomputed square of
+// radius ro (clipped, row-major), packed back to back; lane li of tile m takes row
+// 16m + li (rows past the end repeat the pass's first row, outputs discarded).
+template <int NMAX>
+struct SibPos {
+    int pr[NMAX], pc[NMAX], g[NMAX], row[NMAX];
+    bool valid[NMAX];
+};
+
+template <int NMAX, int G>
+__device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, int lane, SibPos<NMAX>& tp) {
+    int start[G + 1], r0[G], c0[G], wr[G];
+    start[0] = 0;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        Rows q = make_rows(0, 0, 0);
+        if (g < ng) q = make_rows(U[g].cell / BN, U[g].cell % BN, ro);
+        r0[g] = q.r0;
+        c0[g] = q.c0;
+        wr[g] = q.wr;
+        start[g + 1] = start[g] + (g < ng ? q.n : 0);
+    }
+    const int total = start[G];
+    const int li = lane & 15;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        int i = m * 16 + li;
+        tp.valid[m] = i < total;
+        if (i >= total) i = 0;
+        int g = 0;
+#pragma unroll
+        for (int h = 1; h < G; h++) g += i >= start[h] ? 1 : 0;
+        int j = 0, rr = 0, R0 = 0, C0 = 0, WR = 1;
+#pragma unroll
+        for (int h = 0; h < G; h++)
+            if (h == g) {
+                j = i - start[h];
+                R0 = r0[h];
+                C0 = c0[h];
+                WR = wr[h];
+            }
+        rr = (int)(((float)j + 0.5f) / (float)WR);  // exact: j < 121, WR <= 11
+        tp.g[m] = g;
+        tp.row[m] = j;
+        tp.pr[m] = R0 + rr;
+        tp.pc[m] = C0 + (j - rr * WR);
+    }
+    return total;
+}
+
+// One map layer (LAYER 0 = y1: X0 r3 windows -> y1 r2; 1 = x1: Y1 r4 -> x1 r3, + x0;
+// 2 = y2: X1 r5 -> y2 r4) over units [u0, u0 + ng): the k-loop, then the epilogue into
+// each node's own square (global)
+template <int LAYER, int NMAX, int G, bool GC>
+__device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
+                                              int lane, SibStamp& st, int si) {
+    constexpr int R = LAYER + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = R - 1;
+    constexpr int MAPOUT = LAYER + 1, S = 2 * ro + 1, SS = S * S;
+    constexpr bool SKIP = LAYER == 1;
+    SibPos<NMAX> tp;
+    const int total = sib_positions<NMAX, G>(U, ng, ro, lane, tp);
+    const int nt = (total + 15) >> 4;
+    int ctr[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const int cell = U[tp.g[m]].cell, cr = cell / BN, cc = cell - (cell / BN) * BN;
+        ctr[m] = tp.g[m] * 2 * 16 * P + (tp.pr[m] - cr + R) * Wd + (tp.pc[m] - cc + R);
+    }
+    f32x4 acc[2][NMAX];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
+    st(si);
+    const float* Rw = W + RES0 + LAYER * RES_STRIDE;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(Rw + RES_S + ch0), t = *(const f32x4*)(Rw + RES_T + ch0);
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            if (m >= nt || !tp.valid[m]) continue;
+            const SibUnit& u = U[tp.g[m]];
+            const int pr = tp.pr[m], pc = tp.pc[m];
+            const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+            f32x4 sk = zero4();
+            if (SKIP) {
+                const _Float16 *xh_p, *xl_p;
+                map_src<0, GC>(u, pr, pc, ch0, xh_p, xl_p);
+                const h4 xh = *(const h4*)xh_p, xl = *(const h4*)xl_p;
+#pragma unroll
+                for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
+            }
+            h4 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
+                if (SKIP) y += sk[r];
+                y = y > 0.f ? y : 0.f;
+                const _Float16 h = (_Float16)y;
+                hi[r] = h;
+                lo[r] = (_Float16)(y - (float)h);
+            }
+            _Float16* d = u.own + PATCH_OFF[MAPOUT] + ((ch0 >> 3) * SS + (pr - cr + ro) * S + (pc - cc + ro)) * 8 + (ch0 & 7);
+            *(h4*)d = hi;
+            *(h4*)(d + 16 * SS * 8) = lo;
+        }
+    }
+}
+
+// x2 + the 1x1 head convs for one unit (Y2 r6 window at LDS 0): wave np = n-tile pair
+// over all the unit's M tiles; the head partial sums in tree_node's per-lane chain
+// (n-tile 2np then 2np+1, channels in order) and cross-lane order, to hpart
+template <bool GC>
+__device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, const float* __restrict__ W, int np,
+                                               int lane, float* __restrict__ hpart, SibStamp& st, int si) {
+    constexpr int layer = 3, NMAX = 8;
+    const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+    const Rows rows = make_rows(cr, cc, 5);
+    const int nt = (rows.n + 15) >> 4;
+    TilePos<NMAX> tp;
+    tile_positions<NMAX, 6>(rows, 0, lane, tp);
+    int ctr[NMAX];
+    tile_centres<NMAX, Win<6>>(tp, cr, cc, ctr);
+    f32x4 acc[2][NMAX];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
+    st(si);
+    const float* R = W + RES0 + layer * RES_STRIDE;
+    float s0[NMAX], s1[NMAX], sv[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
+        const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
+        const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            if (m >= nt) continue;
+            const _Float16 *xh_p, *xl_p;
+            map_src<2, GC>(u, tp.pr[m], tp.pc[m], ch0, xh_p, xl_p);
+            const h4 xh = *(const h4*)xh_p, xl = *(const h4*)xl_p;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
+                y = y > 0.f ? y : 0.f;
+                s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
+                s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
+                sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        if (m >= nt) continue;
+        float a = s0[m], c = s1[m], v = sv[m];
+        a += __shfl_xor(a, 16);
+        c += __shfl_xor(c, 16);
+        v += __shfl_xor(v, 16);
+        a += __shfl_xor(a, 32);
+        c += __shfl_xor(c, 32);
+        v += __shfl_xor(v, 32);
+        const int i = tp.row[m];
+        if (lane < 16 && tp.valid[m]) {
+            hpart[(np * 3 + 0) * HP_ROWS + i] = a;
+            hpart[(np * 3 + 1) * HP_ROWS + i] = c;
+            hpart[(np * 3 + 2) * HP_ROWS + i] = v;
+        }
+    }
+}
+
+// node b's head-conv record: its recomputed radius-5 square from hpart (bias, then the
+// 4 pairs' partials in order), the rest copied from its base's record
+__device__ __forceinline__ void sib_record(const SibUnit& u, const float* __restrict__ W, float* __restrict__ hbuf,
+                                           const float* __restrict__ hpart, int tid) {
+    const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+    const Rows r4 = make_rows(cr, cc, 5);
+    const float* hr = hbuf + (size_t)u.base * HSTRIDE;
+    float* h = hbuf + (size_t)u.leaf * HSTRIDE;
+    for (int j = tid; j < HSTRIDE; j += NTS) {
+        float v = hr[j];
+        int pos = -1, which = 0;
+        if (j < POS) {
+            pos = j;
+        } else if (j < 2 * POS) {
+            pos = j - POS;
+            which = 1;
+        } else if (j >= HV_OFF && j < HV_OFF + POS) {
+            pos = j - HV_OFF;
+            which = 2;
+        }
+        if (pos >= 0) {
+            const int pr = pos / BN, pc = pos % BN;
+            if (pr >= r4.r0 && pr < r4.r0 + r4.n / r4.wr && pc >= r4.c0 && pc < r4.c0 + r4.wr) {
+                const int i = (pr - r4.r0) * r4.wr + (pc - r4.c0);
+                float acc = which == 0 ? W[P_B] : (which == 1 ? W[P_B + 1] : W[V_B]);
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc += hpart[(q * 3 + which) * HP_ROWS + i];
+                v = acc;
+            }
+        }
+        h[j] = v;
+    }
+}
+
+// GC = false: the root children among leaves [0, count) (cinfo >= 0, bit 30 clear);
+// GC = true: the grandchild list.  Workgroup w of XCD x takes a contiguous range of
+// x's contiguous eighth, so a chunk's nodes are siblings and a root's maps stay in one
+// L2.  scratch: SIB_G patch-sized areas per workgroup.
+template <bool GC>
+__global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __restrict__ scratch, int n,
+                                                       const int32_t* __restrict__ d_count,
+                                                       const int32_t* __restrict__ list,
+                                                       const int32_t* __restrict__ list_count) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_S];
+    SibUnit* U = (SibUnit*)(lds + SIB_U);
+    float* hpart = (float*)(lds + SIB_HP);
+    __shared__ int s_ng, s_next;
+    const int count = GC ? *list_count : (d_count ? (*d_count < n ? *d_count : n) : n);
+    const int nx = gridDim.x >= 8 ? 8 : 1;
+    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
+    if (k >= per) return;
+    const int xchunk = (count + nx - 1) / nx;
+    const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+    const int sub = (xe - xb + per - 1) / per;
+    const int beg = xb + k * sub, end = beg + sub < xe ? beg + sub : xe;
+    _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int np = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const float* W = A.W;
+    int pos = beg;
+    SibStamp st;
+    while (pos < end) {
+        __syncthreads();  // the previous chunk's readers of U are done
+        // the next up to SIB_G nodes of the range (wave 0: ballots over 64 leaves at a time)
+        if (np == 0) {
+            int cnt = 0, p = pos;
+            while (cnt < SIB_G && p < end) {
+                const int i = p + lane;
+                bool take = false;
+                if (i < end) {
+                    if (GC) {
+                        take = true;
+                    } else {
+                        const int ci = A.cinfo[i];
+                        take = ci >= 0 && !(ci & (1 << 30));
+                    }
+                }
+                const uint64_t m = __ballot(take);
+                const int rank = cnt + __popcll(m & ((1ull << lane) - 1));
+                if (take && rank < SIB_G) {
+                    const int b = GC ? list[i] : i;
+                    SibUnit u;
+                    const int ci = A.cinfo[b];
+                    const int o = (ci >> 8) & 0x3fffff;
+                    u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
+                    u.leaf = b;
+                    u.cell = ci & 0xff;
+                    u.base = A.meta[b];
+                    u.own = myscr + (size_t)rank * PATCH_HALVES;
+                    u.par = nullptr;
+                    u.pcell = 0;
+#pragma unroll
+                    for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
+                    if (GC) {  // the parent (a root child with a patch slot)
+                        const int pa = u.base;
+                        u.pcell = A.cinfo[pa] & 0xff;
+                        u.par = A.patches + (size_t)A.pslot[pa] * PATCH_HALVES;
+                    } else {
+                        const int ps = A.pslot[b];
+                        if (ps >= 0) u.own = A.patches + (size_t)ps * PATCH_HALVES;  // it has grandchildren: its patch
+                    }
+                    U[rank] = u;
+                }
+                const int found = __popcll(m);
+                if (cnt + found > SIB_G) {  // resume after the SIB_G-th node taken
+                    const uint64_t m6 = __ballot(take && rank == SIB_G - 1);
+                    p += __ffsll((unsigned long long)m6);
+                    cnt = SIB_G;
+                } else {
+                    cnt += found;
+                    p += 64;
+                }
+            }
+            if (lane == 0) {
+                s_ng = cnt;
+                s_next = p;
+            }
+        }
+        __syncthreads();
+        const int ng = s_ng;
+        pos = s_next;
+        if (ng == 0) continue;
+        st(0);
+#ifdef GZ_PVINC_STAMPS
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, (unsigned long long)ng);
+#endif
+        // y1 over all nodes.  The per-pass asm barriers keep the compiler from hoisting
+        // every pass's per-lane weight and window addresses out of the loops (they would
+        // all stay live, and spill).
+        const float* Wp = W;
+        int t = tid;
+        asm volatile("" : "+s"(Wp), "+v"(t));
+        sib_fill<0, GC>(lds, U, 0, ng, t);
+        __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
+        st(1);
+        sib_conv0<SIB_G>(lds, U, ng, Wp, np, t & 63);
+        __syncthreads();
+        st(2);
+        sib_map_layer<0, 10, SIB_G, GC>(lds, U, ng, Wp, np, t & 63, st, 3);
+        __syncthreads();
+        st(4);
+        // x1 in passes of 3
+        for (int u0 = 0; u0 < ng; u0 += 3) {
+            const int g = ng - u0 < 3 ? ng - u0 : 3;
+            Wp = W;
+            t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+            sib_fill<1, GC>(lds, U, u0, g, t);
+            __syncthreads();
+            st(5);
+            sib_map_layer<1, 10, 3, GC>(lds, U + u0, g, Wp, np, t & 63, st, 6);
+            __syncthreads();
+            st(7);
+        }
+        // y2 in passes of 2
+        for (int u0 = 0; u0 < ng; u0 += 2) {
+            const int g = ng - u0 < 2 ? ng - u0 : 2;
+            Wp = W;
+            t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+            sib_fill<2, GC>(lds, U, u0, g, t);
+            __syncthreads();
+            st(8);
+            sib_map_layer<2, 11, 2, GC>(lds, U + u0, g, Wp, np, t & 63, st, 9);
+            __syncthreads();
+            st(10);
+        }
+        // x2 + heads, one node per pass
+        for (int u0 = 0; u0 < ng; u0++) {
+            Wp = W;
+            t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+            sib_fill<3, GC>(lds, U, u0, 1, t);
+            __syncthreads();
+            st(11);
+            sib_head_layer<GC>(lds, U[u0], Wp, np, t & 63, hpart, st, 12);
+            __syncthreads();
+            st(13);
+            sib_record(U[u0], Wp, A.hbuf, hpart, t);
+            st(14);
+        }
+    }
+}
+
 // one thread per leaf: roots (meta -1) take the next map slot (ord), others -1;
 // no patch slot yet
 __global__ void tree_roots_kernel(const int32_t* __restrict__ meta, int n, const int32_t* __restrict__ d_count,
@@ -1000,10 +1711,21 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, int grid, void* stream) {
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int grid, void* stream) {
     TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
-    pv_child_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, n, d_count);
-    pv_grandchild_kernel<<<grid, NTC, 0, (hipStream_t)stream>>>(A, d_grand, d_ngrand);
+    // GZ_PVINC_SIB=1: the sibling-batched kernel (pv_sib_kernel; in development, off by default)
+    static const int sib = [] {
+        const char* e = getenv("GZ_PVINC_SIB");
+        return e ? atoi(e) : 0;
+    }();
+    hipStream_t s = (hipStream_t)stream;
+    if (sib) {
+        pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, nullptr, nullptr);
+        pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
+    } else {
+        pv_child_kernel<<<grid, NTC, 0, s>>>(A, n, d_count);
+        pv_grandchild_kernel<<<grid, NTC, 0, s>>>(A, d_grand, d_ngrand);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("pv_child_kernel: ") + hipGetErrorString(e)).c_str());

@@ -946,17 +946,19 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, int grid, void* stream);
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int grid, void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr int PV_PATCH_HALVES = 164 * 256;  // a root child's recomputed squares (gz_pvinc.hip)
+constexpr size_t SIB_SCRATCH_HALVES = 6 * (size_t)PV_PATCH_HALVES;  // per workgroup of pv_sib_kernel
 inline int32_t patch_cap_of(int32_t root_cap) { return 16 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;
     int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *cinfo, *ghead, *ctr;
     _Float16* maps;
     _Float16* patches;
+    _Float16* scratch;  // pv_sib_kernel: 6 patch-sized areas per workgroup
 };
 TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
@@ -976,6 +978,8 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     t.maps = (_Float16*)p;
     p += (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16);
     t.patches = (_Float16*)p;
+    p += (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16);
+    t.scratch = (_Float16*)p;
     return t;
 }
 }  // namespace
@@ -984,7 +988,8 @@ extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
     return al256(m * HSTRIDE * sizeof(float)) + 7 * al256(m * 4) + 256 + al256((size_t)patch_cap_of(root_cap) * 4) +
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
-           (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16);
+           (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16) +
+           (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
 }
 
 extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
@@ -1013,7 +1018,7 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
-                                   t.grand, t.ctr + 4, t.cinfo, grid, stream);
+                                   t.grand, t.ctr + 4, t.cinfo, t.scratch, grid, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
