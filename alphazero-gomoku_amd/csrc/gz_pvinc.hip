@@ -896,33 +896,40 @@ static_assert(sizeof(SibUnit) == 128, "unit size");
 
 __device__ inline int iabs(int x) { return x < 0 ? -x : x; }
 
-// The value of map MAP (0..3 = x0, y1, x1, y2) at on-board position (pr, pc) for unit
-// u, channels ch0..ch0+3: the node's own recomputed square (radius MAP+1 around its
-// stone), a grandchild's parent's square, else the root's map.  hi and lo pointers.
+// Where map MAP (0..3 = x0, y1, x1, y2) holds on-board position (pr, pc) for unit u:
+// the node's own recomputed square (radius MAP+1 around its stone), a grandchild's
+// parent's square, else the root's map.  Channel c's hi value is at
+// base + (c >> 3) * cs + (c & 7), its lo value lo halves further.
+struct MapLoc {
+    const _Float16* base;
+    int cs, lo;
+};
 template <int MAP, bool GC>
-__device__ __forceinline__ void map_src(const SibUnit& u, int pr, int pc, int ch0, const _Float16*& hi,
-                                        const _Float16*& lo) {
+__device__ __forceinline__ MapLoc map_loc(const SibUnit& u, int pr, int pc) {
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
-    if (iabs(pr - cr) <= rc && iabs(pc - cc) <= rc) {
-        hi = u.own + PATCH_OFF[MAP] + ((ch0 >> 3) * SS + (pr - cr + rc) * S + (pc - cc + rc)) * 8 + (ch0 & 7);
-        lo = hi + 16 * SS * 8;
-        return;
-    }
+    MapLoc L;
+    L.base = u.gm + MAP * PV_MAP_HALVES + (pr * BN + pc) * 8;
+    L.cs = 256 * 8;
+    L.lo = PV_MAP_PLANE;
     if (GC) {
         const int r1 = u.pcell / BN, c1 = u.pcell - (u.pcell / BN) * BN;
         if (iabs(pr - r1) <= rc && iabs(pc - c1) <= rc) {
-            hi = u.par + PATCH_OFF[MAP] + ((ch0 >> 3) * SS + (pr - r1 + rc) * S + (pc - c1 + rc)) * 8 + (ch0 & 7);
-            lo = hi + 16 * SS * 8;
-            return;
+            L.base = u.par + PATCH_OFF[MAP] + ((pr - r1 + rc) * S + (pc - c1 + rc)) * 8;
+            L.cs = SS * 8;
+            L.lo = 16 * SS * 8;
         }
     }
-    hi = u.gm + MAP * PV_MAP_HALVES + ((ch0 >> 3) * 256 + pr * BN + pc) * 8 + (ch0 & 7);
-    lo = hi + PV_MAP_PLANE;
+    if (iabs(pr - cr) <= rc && iabs(pc - cc) <= rc) {
+        L.base = u.own + PATCH_OFF[MAP] + ((pr - cr + rc) * S + (pc - cc + rc)) * 8;
+        L.cs = SS * 8;
+        L.lo = 16 * SS * 8;
+    }
+    return L;
 }
 
 // Windows (radius R = MAP + 3) of map MAP for units [u0, u0 + ng) at LDS offset 0, one
-// after another in the [plane][16 cg][P][8] layout: each position from map_src, zeros
+// after another in the [plane][16 cg][P][8] layout: each position as map_loc places it, zeros
 // (a zero source) off the board.  LDS-DMA (global_load_lds_dwordx4: item i of a unit's
 // window lands at byte 16 i, wave-uniform base + 16 lane), so a fill holds no
 // registers and all its loads are in flight at once; the caller's __syncthreads drains
@@ -1107,12 +1114,34 @@ __device__ __forceinline__ void sib_conv(const _Float16* act, const int (&ctr)[N
     }
 }
 
-// conv0 + BN + ReLU at the <= 9 positions around each unit's stone (the im2col of the
-// node's board built per lane: row li, k = 8q..8q+7, exactly the columns tree_node
-// stages in LDS), wave np: n-tiles 2np, 2np+1; into the unit's X0 window and its x0 square
+// conv0's im2col for every unit (16 rows x 32 k fp16 each, the columns tree_node
+// stages), all units in parallel, into col (the head-partials area, dead during y1)
+__device__ __forceinline__ void sib_col(_Float16* col, const SibUnit* U, int ng, int tid) {
+    for (int e = tid; e < ng * 512; e += NTS) {
+        const int g = e >> 9, row = (e >> 5) & 15, k = e & 31;
+        const SibUnit& u = U[g];
+        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+        const Rows r0w = make_rows(cr, cc, 1);
+        _Float16 v = (_Float16)0.f;
+        if (row < r0w.n && k < 27) {
+            const int pr = r0w.r0 + row / r0w.wr, pc = r0w.c0 + row % r0w.wr;
+            const int tap = k / 3, cin = k % 3;
+            const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
+            if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
+                const int bit = bit_of_board(rr, c2);
+                const uint32_t bl = (u.board[bit >> 5] >> (bit & 31)) & 1u, wh = (u.board[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+                v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
+            }
+        }
+        col[e] = v;
+    }
+}
+
+// conv0 + BN + ReLU at the <= 9 positions around each unit's stone, wave np: n-tiles
+// 2np, 2np+1; into the unit's X0 window and its x0 square
 template <int G>
-__device__ __forceinline__ void sib_conv0(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
-                                          int lane) {
+__device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const SibUnit* U, int ng,
+                                          const float* __restrict__ W, int np, int lane) {
     const int li = lane & 15, q = lane >> 4;
     constexpr int WIN = wbytes(P_X0) / 2;  // halves per X0 window
     h8 wh[2], wl[2];
@@ -1126,29 +1155,17 @@ __device__ __forceinline__ void sib_conv0(char* lds, const SibUnit* U, int ng, c
         ws[n] = *(const f32x4*)(W + C0_S + ch0);
         wt[n] = *(const f32x4*)(W + C0_T + ch0);
     }
-    for (int g = 0; g < ng; g++) {
+    h8 a[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) a[g] = *(const h8*)(col + g * 512 + li * 32 + 8 * q);
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        if (g >= ng) break;
         const SibUnit& u = U[g];
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         const Rows r0w = make_rows(cr, cc, 1);
-        const uint32_t* cb = u.board;
         const bool rowok = li < r0w.n;
         const int pr = rowok ? r0w.r0 + li / r0w.wr : 0, pc = rowok ? r0w.c0 + li % r0w.wr : 0;
-        h8 a;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int k = 8 * q + j;
-            float v = 0.f;
-            if (rowok && k < 27) {
-                const int tap = k / 3, cin = k % 3;
-                const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
-                if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
-                    const int bit = bit_of_board(rr, c2);
-                    const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
-                    v = (float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
-                }
-            }
-            a[j] = (_Float16)v;
-        }
         _Float16* xw = (_Float16*)lds + g * WIN;
 #pragma unroll
         for (int n = 0; n < 2; n++) {
@@ -1156,8 +1173,8 @@ __device__ __forceinline__ void sib_conv0(char* lds, const SibUnit* U, int ng, c
             const int ch0 = nt * 16 + 4 * q;
             const f32x4 s = ws[n], t = wt[n];
             f32x4 acc = zero4();
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a[g], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a[g], acc, 0, 0, 0);
             if (rowok) {
                 h4 hi, lo;
 #pragma unroll
@@ -1255,6 +1272,22 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
     if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* Rw = W + RES0 + LAYER * RES_STRIDE;
+    // x1's skip input (x0) first: every load of the epilogue in flight at once (rows
+    // past the pass's end read a valid position and are dropped)
+    h4 skh[2][NMAX], skl[2][NMAX];
+    if (SKIP) {
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            const MapLoc L = map_loc<0, GC>(U[tp.g[m]], tp.pr[m], tp.pc[m]);
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+                const _Float16* p = L.base + (ch0 >> 3) * L.cs + (ch0 & 7);
+                skh[n][m] = *(const h4*)p;
+                skl[n][m] = *(const h4*)(p + L.lo);
+            }
+        }
+    }
 #pragma unroll
     for (int n = 0; n < 2; n++) {
         const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
@@ -1265,19 +1298,11 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
             const SibUnit& u = U[tp.g[m]];
             const int pr = tp.pr[m], pc = tp.pc[m];
             const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
-            f32x4 sk = zero4();
-            if (SKIP) {
-                const _Float16 *xh_p, *xl_p;
-                map_src<0, GC>(u, pr, pc, ch0, xh_p, xl_p);
-                const h4 xh = *(const h4*)xh_p, xl = *(const h4*)xl_p;
-#pragma unroll
-                for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
-            }
             h4 hi, lo;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
-                if (SKIP) y += sk[r];
+                if (SKIP) y += (float)skh[n][m][r] + (float)skl[n][m][r];
                 y = y > 0.f ? y : 0.f;
                 const _Float16 h = (_Float16)y;
                 hi[r] = h;
@@ -1312,6 +1337,19 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* R = W + RES0 + layer * RES_STRIDE;
+    // the skip input (x1) first: every load in flight at once
+    h4 skh[2][NMAX], skl[2][NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const MapLoc L = map_loc<2, GC>(u, tp.pr[m], tp.pc[m]);
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+            const _Float16* p = L.base + (ch0 >> 3) * L.cs + (ch0 & 7);
+            skh[n][m] = *(const h4*)p;
+            skl[n][m] = *(const h4*)(p + L.lo);
+        }
+    }
     float s0[NMAX], s1[NMAX], sv[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
@@ -1324,9 +1362,7 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
             if (m >= nt) continue;
-            const _Float16 *xh_p, *xl_p;
-            map_src<2, GC>(u, tp.pr[m], tp.pc[m], ch0, xh_p, xl_p);
-            const h4 xh = *(const h4*)xh_p, xl = *(const h4*)xl_p;
+            const h4 xh = skh[n][m], xl = skl[n][m];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
@@ -1359,13 +1395,16 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
 // node b's head-conv record: its recomputed radius-5 square from hpart (bias, then the
 // 4 pairs' partials in order), the rest copied from its base's record
 __device__ __forceinline__ void sib_record(const SibUnit& u, const float* __restrict__ W, float* __restrict__ hbuf,
-                                           const float* __restrict__ hpart, int tid) {
+                                           const float* __restrict__ hpart, const float (&rec)[3], int tid) {
+    static_assert(HSTRIDE <= 3 * NTS, "record entries per thread");
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
     const Rows r4 = make_rows(cr, cc, 5);
-    const float* hr = hbuf + (size_t)u.base * HSTRIDE;
     float* h = hbuf + (size_t)u.leaf * HSTRIDE;
-    for (int j = tid; j < HSTRIDE; j += NTS) {
-        float v = hr[j];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int j = tid + k * NTS;
+        if (j >= HSTRIDE) break;
+        float v = rec[k];
         int pos = -1, which = 0;
         if (j < POS) {
             pos = j;
@@ -1489,9 +1528,10 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
         int t = tid;
         asm volatile("" : "+s"(Wp), "+v"(t));
         sib_fill<0, GC>(lds, U, 0, ng, t);
+        sib_col((_Float16*)hpart, U, ng, t);
         __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
         st(1);
-        sib_conv0<SIB_G>(lds, U, ng, Wp, np, t & 63);
+        sib_conv0<SIB_G>(lds, (const _Float16*)hpart, U, ng, Wp, np, t & 63);
         __syncthreads();
         st(2);
         sib_map_layer<0, 10, SIB_G, GC>(lds, U, ng, Wp, np, t & 63, st, 3);
@@ -1531,10 +1571,16 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
             sib_fill<3, GC>(lds, U, u0, 1, t);
             __syncthreads();
             st(11);
+            float rec[3];  // the base's record entries of this thread, loaded before the x2 k-loop
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int j = t + k * NTS;
+                rec[k] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
+            }
             sib_head_layer<GC>(lds, U[u0], Wp, np, t & 63, hpart, st, 12);
             __syncthreads();
             st(13);
-            sib_record(U[u0], Wp, A.hbuf, hpart, t);
+            sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
             st(14);
         }
     }
@@ -1713,10 +1759,10 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int grid, void* stream) {
     TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
-    // GZ_PVINC_SIB=1: the sibling-batched kernel (pv_sib_kernel; in development, off by default)
+    // GZ_PVINC_SIB=0: the one-node-per-workgroup kernels (A/B reference for tools/ab.sh)
     static const int sib = [] {
         const char* e = getenv("GZ_PVINC_SIB");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     hipStream_t s = (hipStream_t)stream;
     if (sib) {

@@ -31,7 +31,8 @@ Also reported: the roofline of the PV forward (executed MFMA FLOP / kernel time,
 and the full-forward-equivalent rate), config 4 (planner plies) and the exact-fp32
 run as labelled secondaries, the prior-elided MCTS-only rate (moves identical
 without the priors), and the CPU baseline: the C oracle + torch-fp32 forwards
-("port") in 16 single-thread processes on the host cores.
+("port") on the host cores -- P processes x 1 thread, 1 process x P threads, and
+config 1.
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torchrun.
 """
 import argparse
@@ -47,6 +48,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from gzero import _lib  # noqa: E402
 from gzero import dist as gdist  # noqa: E402
 from gzero import weights  # noqa: E402
 from gzero.device import PVWeights, ptr, stream  # noqa: E402
@@ -90,12 +92,14 @@ def load_clock(kernel):
 
 def _cpu_worker(task):
     """One host process of the CPU baseline: the C oracle's search (1 thread) of
-    `plies` MCTS plies from a timed-window start position, then the torch-fp32 CPU
-    forwards (1 thread) of every node those searches created -- the reference's
-    per-ply work (ai_agent.py:168-204 + GomokuModel.predict per node)."""
-    black, white, n_moves, player, gid, sims, seed, budget = task
+    MCTS plies from a start position, then the torch-fp32 CPU forwards (`threads`
+    intra-op threads) of every node those searches created -- the reference's
+    per-ply work (ai_agent.py:168-204 + GomokuModel.predict per node).  With
+    planner_steps > 0 every rollout starts with BG-planner plies whose GraphNet +
+    OpponentDQN forwards also run on torch CPU (bg_planner.py:243-250)."""
+    black, white, n_moves, player, gid, sims, seed, budget, threads, beta, planner_steps = task
     import torch as T
-    T.set_num_threads(1)
+    T.set_num_threads(threads)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from gzero.boards import words_to_cells, planes_from_cells
@@ -108,7 +112,20 @@ def _cpu_worker(task):
     net = weights.PolicyValueNet()
     net.load_state_dict(weights.init_state_dict(0))
     net.eval()
-    p = O.make_params("medium", sims=sims, beta=0.0, seed=seed)
+    pq = None
+    if planner_steps:
+        from gzero import planner_nets
+        gn, dq = planner_nets.GraphNet(), planner_nets.OpponentDQN()
+        gn.load_state_dict(planner_nets.init_graphnet_state(0))
+        dq.load_state_dict(planner_nets.init_dqn_state(1))
+        gn.eval()
+        dq.eval()
+
+        def pq(board, game_id, sim, step):
+            x = T.from_numpy(planes_from_cells(np.frombuffer(bytes(board.cell), dtype=np.int8)[None]))
+            with T.no_grad():
+                return T.softmax(gn(x), dim=1)[0].numpy(), dq(x)[0].numpy()
+    p = O.make_params("medium", sims=sims, beta=beta, seed=seed, planner_steps=planner_steps, pq=pq)
     t0 = time.perf_counter()
     plies = predicts = 0
     while not b.over and time.perf_counter() - t0 < budget:
@@ -117,6 +134,10 @@ def _cpu_worker(task):
         # the forwards of this ply's nodes: every node's board (root + path stones);
         # terminal nodes are not forwarded (predicts counts the non-terminal ones)
         par, mvs = tree["parent"], tree["move"]
+        if not par:  # an opening ply (_opening_move, ai_agent.py:138-166): no search, no forwards
+            plies += 1
+            O.lib().or_make_move(b, mv // 15, mv % 15)
+            continue
         nb = np.zeros((len(par), 225), np.int8)
         col = np.zeros(len(par), np.int8)
         nb[0], col[0] = root, 3 - b.player
@@ -135,6 +156,15 @@ def _cpu_worker(task):
     return plies, predicts, time.perf_counter() - t0
 
 
+def _cpu_warm(_):
+    """Pool start-up: import torch and the oracle in each worker before any timing."""
+    import torch as T
+    T.set_num_threads(1)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # noqa: F401
+    return 0
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -146,27 +176,62 @@ def cpu_model():
     return "unknown"
 
 
+def host_cores():
+    """(CPUs this process may run on, the CPU share the worker pool is sized to).  On
+    the GPU box the affinity mask shows the whole machine; the job's share is the
+    OMP_NUM_THREADS the box sets (16 per GPU)."""
+    aff = len(os.sched_getaffinity(0))
+    share = aff
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and 0 < int(env) < aff:
+        share = int(env)
+    return aff, share
+
+
 def cpu_baseline(pool, procs, positions, sims, seed, budget_s):
-    """The reference's CPU self-play work on the GPU box's host cores: `procs`
-    single-thread processes (P processes x 1 thread), each
-    searching from one of the GPU run's timed-window start positions with the C
-    oracle and running the torch-fp32 CPU forwards of the nodes it created, for
-    budget_s seconds; value = all processes' plies / wall time."""
-    tasks = [positions[i % len(positions)] + (sims, seed, budget_s) for i in range(procs)]
+    """The reference's CPU self-play work on the GPU box's host cores,
+    three bounded runs:
+      1. config 2 work, `procs` processes x 1 thread, each from one of the GPU run's
+         timed-window start positions (the headline value: the best aggregate);
+      2. config 2 work, 1 process x `procs` torch threads;
+      3. config 1 (1 game from the empty board, 50 sims, beta 0.2, planner_steps 5,
+         medium), 1 process x `procs` torch threads.
+    value = plies / wall time of each run."""
+    aff, _ = host_cores()
+    cpu = cpu_model()
+    runs = []
+    tasks = [positions[i % len(positions)] + (sims, seed, budget_s, 1, 0.0, 0) for i in range(procs)]
     t0 = time.perf_counter()
     res = pool.map(_cpu_worker, tasks)
     wall = time.perf_counter() - t0
-    plies = sum(r[0] for r in res)
-    predicts = sum(r[1] for r in res)
+    plies, predicts = sum(r[0] for r in res), sum(r[1] for r in res)
+    runs.append({"run": f"config 2 work: {procs} processes x 1 thread", "value": plies / wall, "unit": "moves/s",
+                 "per_core": plies / wall / procs, "plies": plies, "forwards": predicts, "wall_s": round(wall, 2),
+                 "cores": procs})
+    one = pool.apply(_cpu_worker, (positions[0] + (sims, seed, budget_s, procs, 0.0, 0),))
+    runs.append({"run": f"config 2 work: 1 process x {procs} threads", "value": one[0] / one[2], "unit": "moves/s",
+                 "per_core": one[0] / one[2] / procs, "plies": one[0], "forwards": one[1],
+                 "wall_s": round(one[2], 2), "cores": procs})
+    empty = (np.zeros(8, np.uint32), np.zeros(8, np.uint32), 0, 1, 0)
+    c1 = pool.apply(_cpu_worker, (empty + (50, seed, budget_s, procs, 0.2, 5),))
+    runs.append({"run": f"config 1: 1 game, 50 sims, beta 0.2, planner_steps 5; 1 process x {procs} threads",
+                 "value": c1[0] / c1[2], "unit": "moves/s", "per_core": c1[0] / c1[2] / procs, "plies": c1[0],
+                 "forwards": c1[1], "wall_s": round(c1[2], 2), "cores": procs})
+    for r in runs:
+        r["value"] = round(r["value"], 3)
+        r["per_core"] = round(r["per_core"], 4)
     return {
-        "value": plies / wall if wall > 0 else None,
+        "value": runs[0]["value"],
         "unit": "moves/s",
         "cores": int(procs),
         "kind": "port",
-        "cpu": cpu_model(),
-        "sample": (f"{procs} processes x 1 thread for {budget_s:.0f} s each ({wall:.1f} s wall): {plies} MCTS plies "
-                   f"at {sims} sims from the GPU run's timed-window start positions (C oracle search) + the "
-                   f"{predicts} policy-value forwards of the nodes they created (torch fp32 CPU, 1 thread)"),
+        "cpu": cpu,
+        "host_cpus_in_affinity": aff,
+        "sample": (f"run 1 of `runs`: {procs} processes x 1 thread for {budget_s:.0f} s each ({wall:.1f} s wall): "
+                   f"{plies} MCTS plies at {sims} sims from the GPU run's timed-window start positions (C oracle "
+                   f"search) + the {predicts} policy-value forwards of the nodes they created (torch fp32 CPU); "
+                   f"{procs} = the job's CPU share of the {aff} CPUs in the affinity mask"),
+        "runs": runs,
     }
 
 
@@ -189,7 +254,8 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         tst = None
         if eng.tree:  # list sizes of the incremental forward (device copy, no sync)
             tst = torch.zeros(6, dtype=torch.int32, device="cuda")
-            eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream())
+            _lib.check(eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream()),
+                       "gz_pv_tree_stats")
         if ex is not None:
             ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
             ex.exchange()
@@ -333,9 +399,9 @@ def main():
         # host worker processes come from a forkserver started before this process
         # touches the GPU (no process that initialised HIP forks or execs)
         import multiprocessing as mp
-        procs = min(16, os.cpu_count() or 1)
+        procs = host_cores()[1]
         pool = mp.get_context("forkserver").Pool(procs)
-        pool.map(abs, range(procs))  # start the workers now
+        pool.map(_cpu_warm, range(procs))  # start the workers (torch imported) now
     torch.cuda.set_device(gdist.local_device())
     if ws != args.gpus and rank == 0:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")

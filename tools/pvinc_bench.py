@@ -75,7 +75,7 @@ def main():
         lib.gz_pvinc_stamps_read(st.ctypes.data, 0)
         names = ["meta+stone", "fill X0/Y1/X1 + im2col", "conv0", "y1 (L1)", "x1 (L2)", "fill Y2", "y2 (L3)",
                  "x2 + heads (L4)", "record"]
-        if os.environ.get("GZ_PVINC_SIB", "0") != "0":  # pv_sib_kernel phases (children + grandchildren kernels)
+        if os.environ.get("GZ_PVINC_SIB", "1") != "0":  # pv_sib_kernel phases (children + grandchildren kernels)
             names = ["select nodes", "fill X0 (y1)", "conv0", "y1 k-loop", "y1 epilogue", "fill Y1 (x1)", "x1 k-loop",
                      "x1 epilogue", "fill X1 (y2)", "y2 k-loop", "y2 epilogue", "fill Y2 (x2)", "x2 k-loop",
                      "x2 epilogue + heads", "record"]
