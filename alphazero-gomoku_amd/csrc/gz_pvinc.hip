@@ -599,6 +599,7 @@ struct TreeArgs {
     const _Float16* maps;
     _Float16* patches;
     float* hbuf;
+    int32_t* tiles;  // pv_sib_kernel: 16-row MFMA tiles executed per residual conv [children, grandchildren]
 };
 
 // The incremental forward of node b relative to node base (its parent): the root
@@ -859,7 +860,13 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
 // Every output element takes the full kernel's products in the full kernel's order
 // (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
 // those of the full forward.
-constexpr int NTS = 256;
+#ifndef SIB_WAVES
+#define SIB_WAVES 8
+#endif
+// SIB_WAVES 8: two waves per SIMD; waves np and np + 4 own the same n-tile pair and
+// split a pass's M tiles (SIB_MH halves).  4: one wave per SIMD over all M tiles.
+constexpr int NTS = 64 * SIB_WAVES, SIB_MH = SIB_WAVES / 4;
+constexpr int sib_tiles(int t) { return (t + SIB_MH - 1) / SIB_MH; }
 constexpr int SIB_G = 6;
 constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
 static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
@@ -1141,7 +1148,7 @@ __device__ __forceinline__ void sib_col(_Float16* col, const SibUnit* U, int ng,
 // 2np, 2np+1; into the unit's X0 window and its x0 square
 template <int G>
 __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const SibUnit* U, int ng,
-                                          const float* __restrict__ W, int np, int lane) {
+                                          const float* __restrict__ W, int np, int mh, int lane) {
     const int li = lane & 15, q = lane >> 4;
     constexpr int WIN = wbytes(P_X0) / 2;  // halves per X0 window
     h8 wh[2], wl[2];
@@ -1161,6 +1168,7 @@ __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const 
 #pragma unroll
     for (int g = 0; g < G; g++) {
         if (g >= ng) break;
+        if (g % SIB_MH != mh) continue;  // the M halves take alternate nodes
         const SibUnit& u = U[g];
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         const Rows r0w = make_rows(cr, cc, 1);
@@ -1205,8 +1213,9 @@ struct SibPos {
     bool valid[NMAX];
 };
 
+// (this wave's M half mh of the pass's tiles; returns the wave's tile count)
 template <int NMAX, int G>
-__device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, int lane, SibPos<NMAX>& tp) {
+__device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, int lane, int mh, SibPos<NMAX>& tp) {
     int start[G + 1], r0[G], c0[G], wr[G];
     start[0] = 0;
 #pragma unroll
@@ -1219,10 +1228,12 @@ __device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, i
         start[g + 1] = start[g] + (g < ng ? q.n : 0);
     }
     const int total = start[G];
+    const int T = (total + 15) >> 4, T0 = (T + SIB_MH - 1) / SIB_MH, t0 = mh * T0;
+    const int ntw = T - t0 < T0 ? (T - t0 > 0 ? T - t0 : 0) : T0;
     const int li = lane & 15;
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
-        int i = m * 16 + li;
+        int i = (t0 + m) * 16 + li;
         tp.valid[m] = i < total;
         if (i >= total) i = 0;
         int g = 0;
@@ -1243,21 +1254,21 @@ __device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, i
         tp.pr[m] = R0 + rr;
         tp.pc[m] = C0 + (j - rr * WR);
     }
-    return total;
+    return ntw;
 }
 
 // One map layer (LAYER 0 = y1: X0 r3 windows -> y1 r2; 1 = x1: Y1 r4 -> x1 r3, + x0;
 // 2 = y2: X1 r5 -> y2 r4) over units [u0, u0 + ng): the k-loop, then the epilogue into
 // each node's own square (global)
-template <int LAYER, int NMAX, int G, bool GC>
+template <int LAYER, int NMAX, int G, bool GC, class Mid>
 __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
-                                              int lane, SibStamp& st, int si) {
+                                              int mh, int lane, int32_t* tiles, SibStamp& st, int si, Mid&& mid) {
     constexpr int R = LAYER + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = R - 1;
     constexpr int MAPOUT = LAYER + 1, S = 2 * ro + 1, SS = S * S;
     constexpr bool SKIP = LAYER == 1;
     SibPos<NMAX> tp;
-    const int total = sib_positions<NMAX, G>(U, ng, ro, lane, tp);
-    const int nt = (total + 15) >> 4;
+    const int nt = sib_positions<NMAX, G>(U, ng, ro, lane, mh, tp);
+    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);  // the executed tiles, one count per M half
     int ctr[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
@@ -1288,16 +1299,35 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
             }
         }
     }
+    // each row's destination in its node's square, read from the unit table before
+    // any store (the stores go through generic pointers the compiler cannot separate
+    // from the table)
+    _Float16* dst[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const SibUnit& u = U[tp.g[m]];
+        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+        dst[m] = u.own + PATCH_OFF[MAPOUT] + ((tp.pr[m] - cr + ro) * S + (tp.pc[m] - cc + ro)) * 8;
+    }
+    f32x4 es[2], et[2];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
         const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-        const f32x4 s = *(const f32x4*)(Rw + RES_S + ch0), t = *(const f32x4*)(Rw + RES_T + ch0);
+        es[n] = *(const f32x4*)(Rw + RES_S + ch0);
+        et[n] = *(const f32x4*)(Rw + RES_T + ch0);
+    }
+    // every global load of the epilogue is issued; the caller's barrier (which waits
+    // for them) and the next pass's window fill go here, so the fill's latency hides
+    // behind the epilogue
+    mid();
+    st(si + 1);
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        const f32x4 s = es[n], t = et[n];
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
             if (m >= nt || !tp.valid[m]) continue;
-            const SibUnit& u = U[tp.g[m]];
-            const int pr = tp.pr[m], pc = tp.pc[m];
-            const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
             h4 hi, lo;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
@@ -1308,7 +1338,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
                 hi[r] = h;
                 lo[r] = (_Float16)(y - (float)h);
             }
-            _Float16* d = u.own + PATCH_OFF[MAPOUT] + ((ch0 >> 3) * SS + (pr - cr + ro) * S + (pc - cc + ro)) * 8 + (ch0 & 7);
+            _Float16* d = dst[m] + (ch0 >> 3) * SS * 8 + (ch0 & 7);
             *(h4*)d = hi;
             *(h4*)(d + 16 * SS * 8) = lo;
         }
@@ -1318,15 +1348,18 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
 // x2 + the 1x1 head convs for one unit (Y2 r6 window at LDS 0): wave np = n-tile pair
 // over all the unit's M tiles; the head partial sums in tree_node's per-lane chain
 // (n-tile 2np then 2np+1, channels in order) and cross-lane order, to hpart
-template <bool GC>
+template <bool GC, class Mid>
 __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, const float* __restrict__ W, int np,
-                                               int lane, float* __restrict__ hpart, SibStamp& st, int si) {
-    constexpr int layer = 3, NMAX = 8;
+                                               int mh, int lane, float* __restrict__ hpart, int32_t* tiles,
+                                               SibStamp& st, int si, Mid&& mid) {
+    constexpr int layer = 3, NMAX = sib_tiles(8);
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
     const Rows rows = make_rows(cr, cc, 5);
-    const int nt = (rows.n + 15) >> 4;
+    const int T = (rows.n + 15) >> 4, T0 = (T + SIB_MH - 1) / SIB_MH, t0 = mh * T0;
+    const int nt = T - t0 < T0 ? (T - t0 > 0 ? T - t0 : 0) : T0;
     TilePos<NMAX> tp;
-    tile_positions<NMAX, 6>(rows, 0, lane, tp);
+    tile_positions<NMAX, 6>(rows, t0, lane, tp);
+    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);
     int ctr[NMAX];
     tile_centres<NMAX, Win<6>>(tp, cr, cc, ctr);
     f32x4 acc[2][NMAX];
@@ -1334,7 +1367,7 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
+    if (nt > 0) sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* R = W + RES0 + layer * RES_STRIDE;
     // the skip input (x1) first: every load in flight at once
@@ -1350,15 +1383,24 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
             skl[n][m] = *(const h4*)(p + L.lo);
         }
     }
+    f32x4 es[2], et[2], e0[2], e1[2], ev[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+        es[n] = *(const f32x4*)(R + RES_S + ch0);
+        et[n] = *(const f32x4*)(R + RES_T + ch0);
+        e0[n] = *(const f32x4*)(W + P_W + ch0);
+        e1[n] = *(const f32x4*)(W + P_W + CH + ch0);
+        ev[n] = *(const f32x4*)(W + V_W + ch0);
+    }
+    mid();  // the caller's barrier + the next pass's fill (see sib_map_layer)
+    st(si + 1);
     float s0[NMAX], s1[NMAX], sv[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
 #pragma unroll
     for (int n = 0; n < 2; n++) {
-        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
-        const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
-        const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+        const f32x4 s = es[n], t = et[n], w0 = e0[n], w1 = e1[n], wv = ev[n];
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
             if (m >= nt) continue;
@@ -1392,16 +1434,17 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     }
 }
 
+constexpr int SIB_REC = (HSTRIDE + NTS - 1) / NTS;  // record entries per thread
+
 // node b's head-conv record: its recomputed radius-5 square from hpart (bias, then the
 // 4 pairs' partials in order), the rest copied from its base's record
 __device__ __forceinline__ void sib_record(const SibUnit& u, const float* __restrict__ W, float* __restrict__ hbuf,
-                                           const float* __restrict__ hpart, const float (&rec)[3], int tid) {
-    static_assert(HSTRIDE <= 3 * NTS, "record entries per thread");
+                                           const float* __restrict__ hpart, const float (&rec)[SIB_REC], int tid) {
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
     const Rows r4 = make_rows(cr, cc, 5);
     float* h = hbuf + (size_t)u.leaf * HSTRIDE;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < SIB_REC; k++) {
         const int j = tid + k * NTS;
         if (j >= HSTRIDE) break;
         float v = rec[k];
@@ -1452,14 +1495,15 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     const int beg = xb + k * sub, end = beg + sub < xe ? beg + sub : xe;
     _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int np = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
     const float* W = A.W;
+    int32_t* tiles = A.tiles ? A.tiles + (GC ? 1 : 0) : nullptr;
     int pos = beg;
     SibStamp st;
     while (pos < end) {
         __syncthreads();  // the previous chunk's readers of U are done
         // the next up to SIB_G nodes of the range (wave 0: ballots over 64 leaves at a time)
-        if (np == 0) {
+        if (wave == 0) {
             int cnt = 0, p = pos;
             while (cnt < SIB_G && p < end) {
                 const int i = p + lane;
@@ -1521,67 +1565,90 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
 #ifdef GZ_PVINC_STAMPS
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, (unsigned long long)ng);
 #endif
-        // y1 over all nodes.  The per-pass asm barriers keep the compiler from hoisting
-        // every pass's per-lane weight and window addresses out of the loops (they would
-        // all stay live, and spill).
-        const float* Wp = W;
-        int t = tid;
-        asm volatile("" : "+s"(Wp), "+v"(t));
-        sib_fill<0, GC>(lds, U, 0, ng, t);
-        sib_col((_Float16*)hpart, U, ng, t);
-        __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
-        st(1);
-        sib_conv0<SIB_G>(lds, (const _Float16*)hpart, U, ng, Wp, np, t & 63);
-        __syncthreads();
-        st(2);
-        sib_map_layer<0, 10, SIB_G, GC>(lds, U, ng, Wp, np, t & 63, st, 3);
-        __syncthreads();
-        st(4);
-        // x1 in passes of 3
-        for (int u0 = 0; u0 < ng; u0 += 3) {
-            const int g = ng - u0 < 3 ? ng - u0 : 3;
-            Wp = W;
-            t = tid;
-            asm volatile("" : "+s"(Wp), "+v"(t));
-            sib_fill<1, GC>(lds, U, u0, g, t);
-            __syncthreads();
-            st(5);
-            sib_map_layer<1, 10, 3, GC>(lds, U + u0, g, Wp, np, t & 63, st, 6);
-            __syncthreads();
-            st(7);
-        }
-        // y2 in passes of 2
-        for (int u0 = 0; u0 < ng; u0 += 2) {
-            const int g = ng - u0 < 2 ? ng - u0 : 2;
-            Wp = W;
-            t = tid;
-            asm volatile("" : "+s"(Wp), "+v"(t));
-            sib_fill<2, GC>(lds, U, u0, g, t);
-            __syncthreads();
-            st(8);
-            sib_map_layer<2, 11, 2, GC>(lds, U + u0, g, Wp, np, t & 63, st, 9);
-            __syncthreads();
-            st(10);
-        }
-        // x2 + heads, one node per pass
-        for (int u0 = 0; u0 < ng; u0++) {
-            Wp = W;
-            t = tid;
-            asm volatile("" : "+s"(Wp), "+v"(t));
-            sib_fill<3, GC>(lds, U, u0, 1, t);
-            __syncthreads();
-            st(11);
-            float rec[3];  // the base's record entries of this thread, loaded before the x2 k-loop
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const int j = t + k * NTS;
-                rec[k] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
+        // The chunk's passes: y1 over all nodes, x1 in passes of 3, y2 in passes of 2,
+        // x2 + heads one node at a time.  After each pass's k-loop, a barrier and then
+        // the NEXT pass's window fill (LDS-DMA) run before this pass's epilogue, so the
+        // fill's latency hides behind the epilogue's VALU work -- unless the next pass
+        // reads squares this pass writes (y1 -> x1; x1 -> y2 / y2 -> x2 over the same
+        // nodes in small chunks): that fill waits for the epilogue.  The per-pass asm barriers keep the
+        // compiler from hoisting every pass's per-lane addresses out of the loop (they
+        // would all stay live, and spill).
+        const int nx1 = (ng + 2) / 3, ny2 = (ng + 1) / 2, npass = 1 + nx1 + ny2 + ng;
+        auto pass_of = [&](int p, int& L, int& u0, int& g) {
+            if (p == 0) {
+                L = 0, u0 = 0, g = ng;
+            } else if (p <= nx1) {
+                L = 1, u0 = 3 * (p - 1), g = ng - u0 < 3 ? ng - u0 : 3;
+            } else if (p <= nx1 + ny2) {
+                L = 2, u0 = 2 * (p - 1 - nx1), g = ng - u0 < 2 ? ng - u0 : 2;
+            } else {
+                L = 3, u0 = p - 1 - nx1 - ny2, g = 1;
             }
-            sib_head_layer<GC>(lds, U[u0], Wp, np, t & 63, hpart, st, 12);
+        };
+        auto fill = [&](int L, int u0, int g, int t) {
+            if (L == 1) sib_fill<1, GC>(lds, U, u0, g, t);
+            else if (L == 2) sib_fill<2, GC>(lds, U, u0, g, t);
+            else if (L == 3) sib_fill<3, GC>(lds, U, u0, g, t);
+        };
+        {
+            int t = tid;
+            asm volatile("" : "+v"(t));
+            sib_fill<0, GC>(lds, U, 0, ng, t);
+            sib_col((_Float16*)hpart, U, ng, t);
+            __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
+            st(1);
+            const float* Wp = W;
+            asm volatile("" : "+s"(Wp));
+            sib_conv0<SIB_G>(lds, (const _Float16*)hpart, U, ng, Wp, np, mh, t & 63);
             __syncthreads();
-            st(13);
-            sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
-            st(14);
+            st(2);
+        }
+        bool filled = true;  // this pass's windows are in LDS (y1: above)
+        for (int p = 0; p < npass; p++) {
+            int L, u0, g, L2 = 0, v0 = 0, g2 = 0;
+            pass_of(p, L, u0, g);
+            // prefetch the next pass's windows unless they hold squares this pass writes
+            // (the next layer over some of the same nodes)
+            bool pre = p + 1 < npass;
+            if (pre) {
+                pass_of(p + 1, L2, v0, g2);
+                pre = !(L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2);
+            }
+            const float* Wp = W;
+            int t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+            if (!filled) {
+                fill(L, u0, g, t);
+                __syncthreads();
+                st(1);
+            }
+            filled = pre;
+            auto mid = [&]() {
+                __syncthreads();  // every wave is past this pass's k-loop: the windows are free
+                if (pre) fill(L2, v0, g2, t);
+            };
+            if (L == 0) {
+                sib_map_layer<0, sib_tiles(10), SIB_G, GC>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
+            } else if (L == 1) {
+                sib_map_layer<1, sib_tiles(10), 3, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 6, mid);
+            } else if (L == 2) {
+                sib_map_layer<2, sib_tiles(11), 2, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 9, mid);
+            } else {
+                float rec[SIB_REC];  // the base's record entries of this thread, loaded before the x2 k-loop
+#pragma unroll
+                for (int k = 0; k < SIB_REC; k++) {
+                    const int j = t + k * NTS;
+                    rec[k] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
+                }
+                sib_head_layer<GC>(lds, U[u0], Wp, np, mh, t & 63, hpart, tiles, st, 12, mid);
+                __syncthreads();  // hpart complete; the next pass's windows have landed
+                st(14);
+                sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
+                st(15);
+                continue;
+            }
+            __syncthreads();  // the squares are stored; the next pass's windows have landed
+            st(3 * L + 5);
         }
     }
 }
@@ -1757,8 +1824,9 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, _Float16* d_scratch, int grid, void* stream) {
-    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf};
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles, int grid,
+                                         void* stream) {
+    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
     // GZ_PVINC_SIB=0: the one-node-per-workgroup kernels (A/B reference for tools/ab.sh)
     static const int sib = [] {
         const char* e = getenv("GZ_PVINC_SIB");

@@ -946,7 +946,8 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, _Float16* d_scratch, int grid, void* stream);
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles, int grid,
+                                         void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1018,13 +1019,24 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
-                                   t.grand, t.ctr + 4, t.cinfo, t.scratch, grid, stream);
+                                   t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, grid, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("gz_pv_forward_tree: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+
+// the 16-row MFMA tiles of the residual convs the last tree forward's incremental
+// kernels executed: [root children, grandchildren] (0 with GZ_PVINC_SIB=0)
+extern "C" int gz_pv_tree_exec_tiles(const void* d_workspace, int32_t n, int32_t* d_out2, void* stream) {
+    TreeWs t = tree_carve((void*)d_workspace, n, 0);
+    if (hipMemcpyAsync(d_out2, t.ctr + 8, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) {
+        gz_internal_set_error("gz_pv_tree_exec_tiles: copy");
         return GZ_ERR_HIP;
     }
     return GZ_OK;

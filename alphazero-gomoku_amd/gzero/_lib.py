@@ -100,6 +100,7 @@ SIGNATURES = {
     "gz_pv_tree_workspace_bytes": (_SZ, [_I32, _I32]),
     "gz_pv_forward_tree": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "gz_pv_tree_stats": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "gz_pv_tree_exec_tiles": (ctypes.c_int, [_P, _I32, _P, _P]),
     "gz_gn_weight_floats": (_SZ, []),
     "gz_gn_workspace_bytes": (_SZ, [_I32]),
     "gz_gn_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),

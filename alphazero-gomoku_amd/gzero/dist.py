@@ -95,18 +95,23 @@ class RecordExchange:
     the ring full (0 unless the consumer falls behind by a whole ring).
     """
 
-    def __init__(self, record_cap, chunk, device, capacity=None, group=None):
+    def __init__(self, record_cap, chunk, device, capacity=None, group=None, max_push=None):
         self.item = RECORD_DTYPE.itemsize
         self.record_cap, self.chunk = int(record_cap), int(chunk)
-        self.R = int(capacity) if capacity else self.record_cap + 4 * self.chunk
+        # rows a push copies (a fixed shape): every row of the engine's buffer by
+        # default (lossless); a bound below that counts the excess as overflow
+        self.max_push = min(self.record_cap, int(max_push)) if max_push else self.record_cap
+        self.R = int(capacity) if capacity else self.max_push + 4 * self.chunk
         self.group = group
         self.rank, self.ws = world()
         dev = torch.device(device)
-        self.box = torch.zeros((self.R + 1, self.item), dtype=torch.uint8, device=dev)  # row R = dummy
+        # rows R .. R + max_push - 1: scratch for the copied rows past the count (one
+        # row each, so the fixed-shape copy never piles writes onto one row)
+        self.box = torch.zeros((self.R + self.max_push, self.item), dtype=torch.uint8, device=dev)
         self.head = torch.zeros(1, dtype=torch.int64, device=dev)
         self.tail = torch.zeros(1, dtype=torch.int64, device=dev)
         self.overflow = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ar_cap = torch.arange(self.record_cap, dtype=torch.int64, device=dev)
+        self.ar_cap = torch.arange(self.max_push, dtype=torch.int64, device=dev)
         self.ar_chunk = torch.arange(self.chunk, dtype=torch.int64, device=dev)
         self.recv = torch.zeros((self.ws, self.chunk, self.item), dtype=torch.uint8, device=dev)
         self.recv_counts = torch.zeros(self.ws, dtype=torch.int64, device=dev)
@@ -116,18 +121,20 @@ class RecordExchange:
         rows in rec_bytes (uint8, record_cap x 80 bytes or more) to the outbox."""
         n = d_count.reshape(1).to(torch.int64).clamp(0, self.record_cap)
         free = self.R - (self.tail - self.head)
-        k = torch.minimum(n, free)
+        k = torch.minimum(torch.minimum(n, free), torch.full_like(n, self.max_push))
         self.overflow += n - k
-        pos = torch.where(self.ar_cap < k, (self.tail + self.ar_cap) % self.R, self.R)
-        src = rec_bytes[: self.record_cap * self.item].view(self.record_cap, self.item)
+        pos = torch.where(self.ar_cap < k, (self.tail + self.ar_cap) % self.R, self.R + self.ar_cap)
+        src = rec_bytes[: self.max_push * self.item].view(self.max_push, self.item)
         self.box.index_copy_(0, pos, src)
         self.tail += k
 
     def exchange(self):
         """All-gather one chunk per rank -> (recv uint8 [ws, chunk, 80], counts int64 [ws]),
-        both on the device; rank r's valid rows are recv[r, :counts[r]]."""
+        both on the device; rank r's valid rows are recv[r, :counts[r]].  The two tensors
+        are this object's own buffers, overwritten by the next exchange(): consume them
+        (ReplayCollector.absorb, chunks_to_records) or clone them before then."""
         cnt = torch.minimum(self.tail - self.head, torch.full_like(self.head, self.chunk))
-        pos = torch.where(self.ar_chunk < cnt, (self.head + self.ar_chunk) % self.R, self.R)
+        pos = torch.where(self.ar_chunk < cnt, (self.head + self.ar_chunk) % self.R, self.R + self.ar_chunk % self.max_push)
         # zero padding rows (the dummy row is scratch); a multiply, not a masked
         # assignment, which would synchronise on the mask's nonzero count
         send = self.box.index_select(0, pos) * (self.ar_chunk < cnt).to(torch.uint8)[:, None]
@@ -143,6 +150,54 @@ class RecordExchange:
     def pending(self):
         """Records pushed but not yet exchanged (device tensor)."""
         return self.tail - self.head
+
+
+class ReplayCollector:
+    """Every rank's copy of one self-play iteration's replay, built on the device from
+    the per-step RecordExchange chunks (no host synchronisation per chunk).
+
+    ``absorb`` appends the rows of all ranks whose game id lies in [id_lo, id_hi) --
+    the iteration's games; the engines' continuous refill plays on past them and
+    those rows are dropped -- to a device buffer and counts the finished games (one
+    ply-0 row per game).  Every rank absorbs the same chunks, so every rank's buffer,
+    count and finish decision agree without another collective.  ``records`` sorts
+    the rows by (game id, ply): the union of the ranks' games in id order, which is
+    the order the reference's replay has (training.py:377-395: games in play order,
+    each game's plies in order)."""
+
+    def __init__(self, capacity, id_lo, id_hi, device):
+        self.item = RECORD_DTYPE.itemsize
+        self.cap = int(capacity)
+        self.id_lo, self.id_hi = int(id_lo), int(id_hi)
+        dev = torch.device(device)
+        self.buf = torch.zeros((self.cap + 1, self.item), dtype=torch.uint8, device=dev)  # row cap = dummy
+        self.n = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.games = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.dropped = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def absorb(self, recv, counts):
+        ws, chunk, item = recv.shape
+        rows = recv.reshape(ws * chunk, item)
+        gid = rows[:, 64:72].contiguous().view(torch.int64).reshape(-1)
+        ply = rows[:, 72:74].contiguous().view(torch.int16).reshape(-1)
+        valid = (torch.arange(chunk, device=recv.device)[None, :] < counts[:, None]).reshape(-1)
+        keep = valid & (gid >= self.id_lo) & (gid < self.id_hi)
+        k = keep.to(torch.int64)
+        pos = self.n + torch.cumsum(k, 0) - 1
+        ok = keep & (pos < self.cap)
+        self.dropped += (keep & ~ok).to(torch.int64).sum()
+        self.buf.index_copy_(0, torch.where(ok, pos, torch.full_like(pos, self.cap)), rows)
+        self.n += ok.to(torch.int64).sum()
+        self.games += (ok & (ply == 0)).to(torch.int64).sum()
+
+    def records(self):
+        """Device uint8 rows [n, 80] sorted by (game id, ply), and n (synchronises)."""
+        n = int(self.n.item())
+        rows = self.buf[:n]
+        gid = rows[:, 64:72].contiguous().view(torch.int64).reshape(-1)
+        ply = rows[:, 72:74].contiguous().view(torch.int16).reshape(-1).to(torch.int64)
+        order = torch.argsort(gid * 1024 + ply, stable=True)
+        return rows.index_select(0, order), n
 
 
 def chunks_to_records(recv, counts):

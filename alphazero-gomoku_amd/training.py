@@ -211,6 +211,58 @@ def selfplay(n_games: int, num_simulations: int = 200, difficulty: str = "medium
                     "game_slices": slices}
 
 
+def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int = 200, difficulty: str = "medium",
+                    beta: float = 0.2, seed: int = 0, n_slots: int = 4096, game_id_base: int = 0, model=None,
+                    plies_per_step: int = 16, planner_steps: int = 0, planner=None, pv_mode: str = "tree"):
+    """training.run_iteration's self-play on every rank: this rank plays game ids
+    [game_id_base, game_id_base + n_games) as ``selfplay`` does, and each step's
+    finished games go through the sync-free RecordExchange (one all-gather per step,
+    RCCL) into a ReplayCollector, so every rank ends with the rows of ALL ranks'
+    games in [id_lo, id_hi), sorted by (game id, ply), on the device.  The loop ends
+    when every one of those games has arrived (the count every rank computes from
+    the same chunks, so the ranks stop together).
+    Returns (device uint8 rows [n, 80], n, stats)."""
+    from gzero import dist as gdist
+    from gzero.selfplay import SelfPlayEngine
+    rank, ws = gdist.world()
+    c_puct, expl = {"easy": (1.4, 0.2), "medium": (1.6, 0.05), "hard": (1.8, 0.01)}[difficulty]
+    slots = min(n_slots, n_games)
+    gnw = None
+    if planner_steps:
+        if planner is None:
+            from bg_planner import BGPlannerAI
+            planner = BGPlannerAI(1, difficulty)
+        gnw = planner.device_weights()
+    pvw = model.device_weights() if model is not None else None
+    tree = pv_mode == "tree" and pvw is not None and pvw.precision == "f16x3"
+    eng = SelfPlayEngine(n_slots=slots, num_simulations=num_simulations, c_puct=c_puct, exploration=expl,
+                         beta=beta, seed=seed, pv_weights=pvw,
+                         plies_per_step=min(plies_per_step, 4) if tree else plies_per_step,
+                         game_id_base=game_id_base, planner_steps=planner_steps,
+                         planner_difficulty=difficulty, gn_weights=gnw, pv_mode="tree" if tree else "full")
+    ex = gdist.RecordExchange(eng.record_cap, 2 * eng.n_slots * eng.plies_per_step, "cuda")
+    want = id_hi - id_lo
+    col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda")
+    moves = steps = 0
+    t0 = time.time()
+    while True:
+        eng.step()
+        ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
+        col.absorb(*ex.exchange())
+        moves += int(eng.counters()["moves"])
+        steps += 1
+        if int(col.games.item()) >= want:
+            break
+    rows, n = col.records()
+    if int(ex.overflow.item()) or int(col.dropped.item()):
+        raise RuntimeError(f"selfplay_device: {int(ex.overflow.item())} records overflowed the exchange, "
+                           f"{int(col.dropped.item())} the collector")
+    return rows, n, {"games": want, "moves_played": moves, "steps": steps, "seconds": time.time() - t0}
+
+
+_MAX_GAME_RECORDS = 225  # a game has at most 225 plies (one record each)
+
+
 # ---------------------------------------------------------------- arena (training.py:221-270)
 
 
@@ -360,20 +412,24 @@ def run_iteration(model, trainer, it: int, games_per_iteration: int = 10, num_si
     35 % 8-fold augmentation, a 90/10 split drawn from ``random``, ``epochs``
     epochs of the data-parallel SGD step and the StepLR step."""
     from gzero import dist as gdist
-    from gzero.train import DeviceDataset, records_to_device
+    from gzero.train import DeviceDataset
     rank, ws = gdist.world()
     t0 = time.time()
-    replay_base = (it * ws + rank) * games_per_iteration
-    rep, st = selfplay(games_per_iteration, num_simulations=num_simulations, difficulty=difficulty, beta=beta,
-                       seed=seed, game_id_base=replay_base, model=model, planner_steps=planner_steps,
-                       planner=planner)
-    recs = _replay_records(rep)
-    d = records_to_device(recs) if len(recs) else torch.zeros(0, dtype=torch.uint8, device="cuda")
+    id_lo = it * ws * games_per_iteration
+    replay_base = id_lo + rank * games_per_iteration
+    # every rank's records reach every rank step by step (RecordExchange), sorted by
+    # game id at the end: the same replay on every rank, in the reference's game order
+    d, n_rec, st = selfplay_device(games_per_iteration, id_lo, id_lo + ws * games_per_iteration,
+                                   num_simulations=num_simulations, difficulty=difficulty, beta=beta, seed=seed,
+                                   game_id_base=replay_base, model=model, planner_steps=planner_steps,
+                                   planner=planner)
+    d = d.reshape(-1)
+    moves = torch.tensor([float(st["moves_played"])], dtype=torch.float64, device="cuda")
     if ws > 1:
-        d = gdist.all_gather_records(d, len(recs))
-    n_rec = d.numel() // 80
+        import torch.distributed as tdist
+        tdist.all_reduce(moves)
     t1 = time.time()
-    out = {"iteration": it, "records": n_rec, "selfplay_s": t1 - t0, "moves_played": st["moves_played"] * ws}
+    out = {"iteration": it, "records": n_rec, "selfplay_s": t1 - t0, "moves_played": int(moves.item())}
     if n_rec == 0:
         return dict(out, skipped=True)
     ds = DeviceDataset(d, use_augmentation=True, augment_ratio=augment_ratio, n_records=n_rec)
@@ -396,21 +452,6 @@ def run_iteration(model, trainer, it: int, games_per_iteration: int = 10, num_si
     model.eval_mode()
     t2 = time.time()
     return dict(out, samples=n, train_loss=float(np.mean(tl)), val_loss=float(np.mean(vl)), sgd_s=t2 - t1)
-
-
-def _replay_records(rep: "SimpleReplay"):
-    """SimpleReplay -> device record layout (gzero.boards.RECORD_DTYPE)."""
-    from gzero import boards
-    n = len(rep)
-    rec = np.zeros(n, boards.RECORD_DTYPE)
-    if n:
-        planes = np.stack(rep.states)
-        cells = (planes[:, 0] > 0.5).astype(np.int8) + 2 * (planes[:, 1] > 0.5).astype(np.int8)
-        rec["black"], rec["white"] = boards.cells_to_words(cells.reshape(n, 225))
-        rec["move"] = rep.move_indices
-        rec["player"] = rep.players
-        rec["z"] = rep.outcomes
-    return rec
 
 
 def _rng_isolated(fn, *a, **k):

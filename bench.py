@@ -58,6 +58,10 @@ METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2 dense peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (spec)
 PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
+TILE_FLOP = 2 * 16 * 128 * 1152  # one 16-row tile of a residual 3x3 conv (fp32-equivalent)
+# per incremental node besides its residual tiles: conv0 (one 16-row tile, K 27), the
+# 1x1 head convs on the radius-5 square (121 rows unclipped) and the FC heads
+INC_EXTRA_FLOP = 2 * (16 * 128 * 27 + 121 * 128 * 3 + 450 * 225 + 225 * 64 + 64)
 
 
 
@@ -253,9 +257,12 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
         ctr = eng.d_counters.clone()  # per-step counters, stays on the device
         tst = None
         if eng.tree:  # list sizes of the incremental forward (device copy, no sync)
-            tst = torch.zeros(6, dtype=torch.int32, device="cuda")
+            tst = torch.zeros(8, dtype=torch.int32, device="cuda")
             _lib.check(eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream()),
                        "gz_pv_tree_stats")
+            # [6:8] = the residual-conv MFMA tiles the incremental kernels executed
+            _lib.check(eng.lib.gz_pv_tree_exec_tiles(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst[6:]), stream()),
+                       "gz_pv_tree_exec_tiles")
         if ex is not None:
             ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
             ex.exchange()
@@ -306,8 +313,16 @@ def roofline_of(m, precision):
     if m.get("tree"):
         # roots seen, roots w/ maps, children, full, grandchildren, patch slots
         t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)
-        # executed MFMA FLOP per board, from the last step's leaves (tree_exec_flops)
-        executed = m["exec_per_board"] * mean_leaves
+        # executed MFMA FLOP (fp32-equivalent): full-forward nodes x 267.38 MFLOP + the
+        # residual-conv tiles the incremental kernels counted x 16 rows x 128 x 1152 x 2
+        # + per incremental node its conv0 tile, 1x1 heads (radius-5 square, unclipped:
+        # an upper bound) and FC heads; if the kernels counted no tiles (GZ_PVINC_SIB=0),
+        # the model of tree_exec_flops
+        tiles = float(t[6] + t[7])
+        if tiles > 0:
+            executed = (t[1] + t[3]) * PV_FLOP + tiles * TILE_FLOP + (t[2] + t[4]) * INC_EXTRA_FLOP
+        else:
+            executed = m["exec_per_board"] * mean_leaves
         achieved = executed / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
         tree = {"roots": round(float(t[1]), 1), "children_incremental": round(float(t[2]), 1),
                 "grandchildren_incremental": round(float(t[4]), 1), "patches": round(float(t[5]), 1),
@@ -315,12 +330,14 @@ def roofline_of(m, precision):
                 "child_share": round(float((t[2] + t[4]) / max(1.0, mean_leaves)), 4),
                 "executed_flop_per_launch": round(float(executed), 0),
                 "algorithmic_tflops_full_forward_equivalent": round(algorithmic, 3),
-                "executed_mflop_per_child": round((m["exec_per_board"] * mean_leaves - (t[1] + t[3]) * PV_FLOP)
+                "executed_tiles_per_launch": round(tiles, 1),
+                "executed_mflop_per_child": round((executed - (t[1] + t[3]) * PV_FLOP)
                                                   / max(1.0, t[2] + t[4]) / 1e6, 2),
-                "note": ("achieved = MFMA work executed (roots and deeper nodes: the full 267.38 MFLOP; a root child "
-                         "or grandchild: "
-                         "the 16-row tiles of its radius-2..5 windows, clipped at the board edge) / kernel time; "
-                         "every node's logits, value, softmax and prior are bit-identical to the full forward's")}
+                "note": ("achieved = MFMA work executed / kernel time: roots and untagged nodes the full 267.38 "
+                         "MFLOP; root children and grandchildren the 16-row MFMA tiles their kernel counted "
+                         "(pv_sib_kernel packs several nodes' recomputed squares into each layer pass) plus conv0 "
+                         "and the heads; every node's logits, value, softmax and prior are bit-identical to the "
+                         "full forward's")}
     traffic, _ = load_traffic(mean_leaves, "tree" if m.get("tree") else "full") if precision == "f16x3" \
         else (None, None)
     if precision == "fp32":
@@ -425,7 +442,10 @@ def main():
     eng = engine(args.beta, args.planner_steps, w, args.pv_mode if args.pv_precision == "f16x3" else "full")
     # N > 1: the per-step RCCL all-gather of finished games' (s, pi, z) records,
     # fixed-size and sync-free (gzero.dist.RecordExchange: counts stay on the device)
-    ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda") if ws > 1 else None
+    # each push copies at most 2 chunks of rows (steady state: about one record per slot
+    # and ply); a burst past that is counted in record_exchange.overflow
+    ex = gdist.RecordExchange(eng.record_cap, 2 * args.slots * P, "cuda", max_push=4 * args.slots * P) \
+        if ws > 1 else None
     burn_in = args.burn_in
     m = measure(eng, args.steps, args.warmup, burn_in, ws, ex)
     T = m["T"]

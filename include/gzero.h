@@ -202,6 +202,10 @@ int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const i
  * with stored maps, incremental children, full-forward boards, incremental
  * grandchildren, parents that claimed a patch slot. */
 int gz_pv_tree_stats(const void* d_workspace, int32_t n, int32_t* d_out6, void* stream);
+/* d_out2 (device int32[2]) = the 16-row x 128-channel x 1152-deep MFMA tiles of the
+ * residual convs the last tree forward's incremental kernels executed, for root
+ * children and for grandchildren (measurement: bench.py's executed-FLOP roofline). */
+int gz_pv_tree_exec_tiles(const void* d_workspace, int32_t n, int32_t* d_out2, void* stream);
 
 /* ---- K7: BG planner nets (bg_planner.py:22-78, BGPlannerAI.get_move :243-250) ----
  * d_weights: packed blob of gz_gn_weight_floats() floats (csrc/gz_gnet.h,

@@ -9,7 +9,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from gzero import boards
-from gzero.dist import RecordExchange, all_gather_records, chunks_to_records, shard_ids, to_records
+from gzero.dist import RecordExchange, ReplayCollector, all_gather_records, chunks_to_records, shard_ids, to_records
 
 
 def _free_port():
@@ -124,6 +124,78 @@ def test_record_exchange_overflow_counts():
     assert int(ex.pending().item()) == 6 and int(ex.overflow.item()) == 6
     ex.exchange()
     assert int(ex.pending().item()) == 4
+
+
+# training.run_iteration's collector (training.selfplay_device) under world size 2:
+# each rank's "engine" finishes games in bursts, plies of a game arriving together,
+# game ids past the iteration's range keep coming (continuous refill) and must be
+# dropped; every rank must end with the union of both ranks' games, sorted by
+# (game id, ply), and stop after the same number of exchanges.
+G_PER_RANK = 5
+
+
+def _games_of(rank):
+    """(game id, plies) this rank's engine finishes, in finishing order: its 5 games
+    of the iteration (ids 10 + 5 rank + i, iteration base 10) and refill games past 20."""
+    rng = np.random.default_rng(rank)
+    ids = list(10 + G_PER_RANK * rank + rng.permutation(G_PER_RANK)) + [20 + 2 * k + rank for k in range(6)]
+    return [(int(g), int(rng.integers(1, 30))) for g in ids]
+
+
+def _collector_worker(rank, ws, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    games = _games_of(rank)
+    cap = 64
+    ex = RecordExchange(cap, 16, "cpu")
+    col = ReplayCollector(ws * G_PER_RANK * 225, 10, 10 + ws * G_PER_RANK, "cpu")
+    k = steps = 0
+    while True:
+        rows = []
+        for _ in range(1 + (steps + rank) % 2):  # 1 or 2 games finish per step
+            if k < len(games):
+                gid, plies = games[k]
+                k += 1
+                r = np.zeros(plies, boards.RECORD_DTYPE)
+                r["game_id"], r["ply"] = gid, np.arange(plies)[::-1]  # plies in any order
+                r["move"] = (gid * 7 + np.arange(plies)[::-1]) % 225
+                rows.append(r)
+        rec = np.concatenate(rows) if rows else np.zeros(0, boards.RECORD_DTYPE)
+        buf = np.zeros(cap, boards.RECORD_DTYPE)
+        buf[: len(rec)] = rec
+        ex.push(torch.from_numpy(buf.view(np.uint8).copy()), torch.tensor([len(rec)], dtype=torch.int32))
+        col.absorb(*ex.exchange())
+        steps += 1
+        if int(col.games.item()) >= ws * G_PER_RANK:
+            break
+    rows_t, n = col.records()
+    q.put((rank, rows_t.numpy().tobytes(), steps, int(ex.overflow.item()), int(col.dropped.item())))
+    dist.destroy_process_group()
+
+
+def test_replay_collector_world2_is_the_union_of_the_ranks_games():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_collector_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (b, st, ov, dr) for r, b, st, ov, dr in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][1] == res[1][1]  # the same number of exchanges
+    assert all(v[2] == 0 and v[3] == 0 for v in res.values())
+    got = {r: np.frombuffer(v[0], boards.RECORD_DTYPE) for r, v in res.items()}
+    assert got[0].tobytes() == got[1].tobytes()
+    want = []
+    for r in range(2):
+        for gid, plies in _games_of(r):
+            if 10 <= gid < 20:
+                want += [(gid, p, (gid * 7 + p) % 225) for p in range(plies)]
+    want.sort()
+    g = got[0]
+    assert [(int(a), int(b), int(c)) for a, b, c in zip(g["game_id"], g["ply"], g["move"])] == want
 
 
 # training.main under world size 2: rank 0 alone runs the arena (which draws from

@@ -76,8 +76,9 @@ def main():
         names = ["meta+stone", "fill X0/Y1/X1 + im2col", "conv0", "y1 (L1)", "x1 (L2)", "fill Y2", "y2 (L3)",
                  "x2 + heads (L4)", "record"]
         if os.environ.get("GZ_PVINC_SIB", "1") != "0":  # pv_sib_kernel phases (children + grandchildren kernels)
-            names = ["select nodes", "fill X0 (y1)", "conv0", "y1 k-loop", "y1 epilogue", "fill Y1 (x1)", "x1 k-loop",
-                     "x1 epilogue", "fill X1 (y2)", "y2 k-loop", "y2 epilogue", "fill Y2 (x2)", "x2 k-loop",
+            names = ["select nodes", "window fills (not overlapped)", "conv0", "y1 k-loop", "y1 barrier + next fill",
+                     "y1 epilogue", "x1 k-loop", "x1 barrier + next fill", "x1 epilogue", "y2 k-loop",
+                     "y2 barrier + next fill", "y2 epilogue", "x2 k-loop", "x2 barrier + next fill",
                      "x2 epilogue + heads", "record"]
         kids = max(1, int(st[16]))
         tot = sum(int(x) for x in st[:len(names)])
