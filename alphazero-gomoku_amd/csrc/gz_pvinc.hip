@@ -861,7 +861,7 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
 // (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
 // those of the full forward.
 #ifndef SIB_WAVES
-#define SIB_WAVES 8
+#define SIB_WAVES 4
 #endif
 // SIB_WAVES 8: two waves per SIMD; waves np and np + 4 own the same n-tile pair and
 // split a pass's M tiles (SIB_MH halves).  4: one wave per SIMD over all M tiles.
