@@ -861,7 +861,7 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
 // (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
 // those of the full forward.
 #ifndef SIB_WAVES
-#define SIB_WAVES 4
+#define SIB_WAVES 8
 #endif
 // SIB_WAVES 8: two waves per SIMD; waves np and np + 4 own the same n-tile pair and
 // split a pass's M tiles (SIB_MH halves).  4: one wave per SIMD over all M tiles.
@@ -1020,8 +1020,17 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
+    // SIB_PROBE (timing probes, wrong results): 1 = every activation read is the
+    // conflict-free pattern of consecutive rows, 2 = every weight load reads k-step 0
+    // (L1-resident: no weight stream)
+#ifndef SIB_PROBE
+#define SIB_PROBE 0
+#endif
+#if SIB_PROBE
+#warning "SIB_PROBE is a timing probe: the tree forward's results are wrong in this build"
+#endif
     auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (SIB_PROBE == 2 ? 0 : ks * KS_BYTES) + n * 1024 + lo * LO_BYTES, 0));
     };
     h8 b[RING][2][2];
 #pragma unroll
@@ -1040,9 +1049,12 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
         for (int m = 0; m < NT; m++) c[n][m] = acc[n][m];
     int nb[NT];
     h8 ah[NT], al[NT];
+    int ctr_[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) ctr_[m] = SIB_PROBE == 1 ? m * 16 + (lane & 15) + Wd + 1 : ctr[m];
 #pragma unroll
     for (int m = 0; m < NT; m++) {
-        nb[m] = (ctr[m] - Wd - 1 + q * P) * 8;  // tap 0 = (-1, -1)
+        nb[m] = (ctr_[m] - Wd - 1 + q * P) * 8;  // tap 0 = (-1, -1)
         ah[m] = *(const h8*)(act + nb[m]);
         al[m] = *(const h8*)(act + PLANE + nb[m]);
     }
@@ -1077,7 +1089,7 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
                 if (cq < CQ - 1) {
                     o = nb[m] + (cq + 1) * 4 * P * 8;
                 } else {
-                    nb[m] = (ctr[m] + toff + q * P) * 8;
+                    nb[m] = (ctr_[m] + (SIB_PROBE == 1 ? 0 : toff) + q * P) * 8;
                     o = nb[m];
                 }
                 ah[m] = *(const h8*)(act + o);
@@ -1204,6 +1216,15 @@ __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const 
     }
 }
 
+// SIB_LAG (8 waves): the second M half's waves start their k-loop SIB_LAG x 64
+// cycles late, so their weight loads follow their partners' and can hit the CU's L1
+#ifndef SIB_LAG
+#define SIB_LAG 0
+#endif
+__device__ __forceinline__ void sib_lag(int mh) {
+    if (SIB_LAG > 0 && mh) __builtin_amdgcn_s_sleep(SIB_LAG);
+}
+
 // The rows of a pass: units u0 .. u0+ng-1 in order, each its recomputed square of
 // radius ro (clipped, row-major), packed back to back; lane li of tile m takes row
 // 16m + li (rows past the end repeat the pass's first row, outputs discarded).
@@ -1280,6 +1301,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    sib_lag(mh);
     if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* Rw = W + RES0 + LAYER * RES_STRIDE;
@@ -1367,6 +1389,7 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    sib_lag(mh);
     if (nt > 0) sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* R = W + RES0 + layer * RES_STRIDE;

@@ -240,7 +240,9 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
                          plies_per_step=min(plies_per_step, 4) if tree else plies_per_step,
                          game_id_base=game_id_base, planner_steps=planner_steps,
                          planner_difficulty=difficulty, gn_weights=gnw, pv_mode="tree" if tree else "full")
-    ex = gdist.RecordExchange(eng.record_cap, 2 * eng.n_slots * eng.plies_per_step, "cuda")
+    # a chunk of a quarter of the engine's record buffer: a game's records leave the
+    # outbox in one or a few steps even when many games end together
+    ex = gdist.RecordExchange(eng.record_cap, max(2 * eng.n_slots * eng.plies_per_step, eng.record_cap // 4), "cuda")
     want = id_hi - id_lo
     col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda")
     moves = steps = 0
@@ -251,7 +253,15 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
         col.absorb(*ex.exchange())
         moves += int(eng.counters()["moves"])
         steps += 1
-        if int(col.games.item()) >= want:
+        if int(col.games.item()) >= want:  # every game's first record is in
+            break
+    # drain: the outboxes may still hold later plies of those games; an exchange in
+    # which every rank sent nothing means every outbox is empty (all ranks see the
+    # same counts, so they stop together)
+    while True:
+        recv, cnt = ex.exchange()
+        col.absorb(recv, cnt)
+        if int(cnt.sum().item()) == 0:
             break
     rows, n = col.records()
     if int(ex.overflow.item()) or int(col.dropped.item()):

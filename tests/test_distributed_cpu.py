@@ -148,7 +148,7 @@ def _collector_worker(rank, ws, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     games = _games_of(rank)
     cap = 64
-    ex = RecordExchange(cap, 16, "cpu")
+    ex = RecordExchange(cap, 8, "cpu", capacity=4096)  # chunk < a game: its plies span exchanges
     col = ReplayCollector(ws * G_PER_RANK * 225, 10, 10 + ws * G_PER_RANK, "cpu")
     k = steps = 0
     while True:
@@ -168,6 +168,11 @@ def _collector_worker(rank, ws, port, q):
         col.absorb(*ex.exchange())
         steps += 1
         if int(col.games.item()) >= ws * G_PER_RANK:
+            break
+    while True:  # drain the outboxes as training.selfplay_device does
+        recv, cnt = ex.exchange()
+        col.absorb(recv, cnt)
+        if int(cnt.sum().item()) == 0:
             break
     rows_t, n = col.records()
     q.put((rank, rows_t.numpy().tobytes(), steps, int(ex.overflow.item()), int(col.dropped.item())))
