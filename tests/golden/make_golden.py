@@ -629,6 +629,71 @@ def part_prior():
                    "prior_f64_b64": base64.b64encode(np.concatenate(priors).tobytes()).decode()})
 
 
+def part_pvnet2():
+    """G4c: the reference GomokuModel at a second weight seed (29) on 288 boards that
+    form 16 search-like families -- a root, 12 of its children (one stone of the
+    side to move more) and 5 children of its first child (two stones more) -- the
+    boards the incremental tree forward sees.  Per board: the move list, its parent
+    in the fixture (-1 for a root), the reference's logits, value, softmax
+    (GomokuModel.predict, neural_network.py:238-247) and masked prior
+    (MCTSNode._get_prior_probability, ai_agent.py:564-582)."""
+    import base64
+    import random as pyrandom
+    import numpy as np
+    import torch
+    from gzero import weights
+    h = ref()
+    sd = weights.init_state_dict(seed=29)
+    path = os.path.join(os.getcwd(), "pv_golden2.pth")
+    torch.save({"model_state_dict": sd, "model_type": "alphazero_gomoku", "board_size": 15, "device": "cpu"}, path)
+    model = h.nn.GomokuModel(model_path=path, board_size=15, device="cpu")
+    rng = pyrandom.Random(31)
+    cases = []
+
+    def nonterminal_children(moves, k):
+        b = replay(h, moves)
+        empty = [i for i in range(N * N) if b.board[i // N, i % N] == 0]
+        rng.shuffle(empty)
+        out = []
+        for c in empty:
+            t = replay(h, moves)
+            t.make_move(c // N, c % N)
+            if not t.game_over:
+                out.append(moves + [c])
+            if len(out) == k:
+                break
+        return out
+
+    for f in range(16):
+        L = [0, 1, 2, 5, 9, 14, 20, 28, 36, 46, 58, 70, 84, 100, 118, 140][f]
+        root = gen_moves(rng, L, avoid_five=True, near=rng.random() < 0.5) if L else []
+        r = len(cases)
+        cases.append({"moves": root, "parent": -1})
+        kids = nonterminal_children(root, 12)
+        first = len(cases)
+        cases += [{"moves": m, "parent": r} for m in kids]
+        cases += [{"moves": m, "parent": first} for m in nonterminal_children(kids[0], 5)]
+    logits_all, value_all, probs_all, counts, priors = [], [], [], [], []
+    for c in cases:
+        b = replay(h, c["moves"])
+        probs, value = model.predict(b.get_board_state())
+        x = torch.from_numpy(b.get_board_tensor()).unsqueeze(0)
+        with torch.no_grad():
+            lg, _ = model.model(x)
+        node = h.ai.MCTSNode(b, None, None, model, {})
+        pr = np.asarray(node.prior_prob, np.float64)
+        logits_all.append(lg.numpy().reshape(-1))
+        value_all.append(float(value))
+        probs_all.append(np.asarray(probs, np.float32))
+        counts.append(len(pr))
+        priors.append(pr)
+    enc = lambda a: base64.b64encode(np.ascontiguousarray(a, np.float32).tobytes()).decode()
+    dump("pvnet2", {"weights_seed": 29, "cases": cases, "logits_f32_b64": enc(np.stack(logits_all)),
+                    "value_f32_b64": enc(np.asarray(value_all)), "probs_f32_b64": enc(np.stack(probs_all)),
+                    "prior_counts": counts,
+                    "prior_f64_b64": base64.b64encode(np.concatenate(priors).tobytes()).decode()})
+
+
 def part_augment():
     """G8: training.augment_sample -- label index and where the plane's stone lands."""
     import numpy as np
@@ -1050,7 +1115,7 @@ def part_arena():
 
 
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
-         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "augment": part_augment,
+         "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "pvnet2": part_pvnet2, "augment": part_augment,
          "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
          "sgd": part_sgd, "arena": part_arena}
 

@@ -181,3 +181,40 @@ def test_prior_random_boards_exact_vs_oracle(oracle):
         empty = cells[i] == 0
         assert prior[i][empty].tobytes() == oracle.prior(pr[i], cells[i]).tobytes(), i
         assert np.all(prior[i][~empty] == 0.0)
+
+
+def test_pvnet2_second_seed_full_and_tree_forward_vs_reference(oracle):
+    """G4c: weight seed 29 on 288 boards in 16 families (root, 12 children, 5
+    grandchildren through the first child) against the reference's own logits,
+    value, softmax and prior (tests/golden/make_golden.py part_pvnet2):
+    * the full f16x3 forward within 1e-4 (softmax, prior within 1e-4 as well);
+    * the incremental tree forward -- roots full, children and grandchildren through
+      pv_sib_kernel -- within the same 1e-4 of the REFERENCE (not only of the full
+      forward), and bit-identical to the full forward."""
+    g = golden("pvnet2")
+    sd = weights.init_state_dict(seed=g["weights_seed"])
+    w = device.PVWeights(weights.pack_pv_weights(sd), precision="f16x3")
+    rows, cells = _fixture_rows(oracle, g)
+    n = len(cells)
+    meta = np.array([c["parent"] for c in g["cases"]], np.int32)
+    ref_lg = _dec(g["logits_f32_b64"], (n, 225))
+    ref_v = _dec(g["value_f32_b64"], (n,))
+    ref_p = _dec(g["probs_f32_b64"], (n, 225))
+    ref_prior = np.frombuffer(base64.b64decode(g["prior_f64_b64"]), np.float64)
+    full = device.pv_forward(w, rows, want_prior=True)
+    tree = device.pv_forward_tree(w, rows, meta)
+    roots = int((meta == -1).sum())
+    assert tree[4][1] == roots and tree[4][2] == 12 * roots and tree[4][4] == 5 * roots and tree[4][3] == 0, tree[4]
+    for lg, v, pr, prior in (full[:4], tree[:4]):
+        assert np.abs(lg - ref_lg).max() < TOL, np.abs(lg - ref_lg).max()
+        assert np.abs(v - ref_v).max() < TOL
+        assert np.abs(pr - ref_p).max() < TOL
+        off = 0
+        for i, cl in enumerate(cells):
+            k = g["prior_counts"][i]
+            empty = cl == 0
+            assert int(empty.sum()) == k
+            assert np.abs(prior[i][empty] - ref_prior[off:off + k]).max() < TOL, i
+            off += k
+    for a, b in zip(full[:4], tree[:4]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
