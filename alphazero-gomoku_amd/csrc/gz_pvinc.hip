@@ -1495,10 +1495,9 @@ __device__ __forceinline__ void sib_record(const SibUnit& u, const float* __rest
     }
 }
 
-// GC = false: the root children among leaves [0, count) (cinfo >= 0, bit 30 clear);
-// GC = true: the grandchild list.  Workgroup w of XCD x takes a contiguous range of
-// x's contiguous eighth, so a chunk's nodes are siblings and a root's maps stay in one
-// L2.  scratch: SIB_G patch-sized areas per workgroup.
+// list: the root children (GC = false, tree_lists_kernel) or the grandchildren (GC =
+// true, tree_grand_order_kernel), list_count entries.  scratch: SIB_G patch-sized
+// areas per workgroup.
 template <bool GC>
 __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __restrict__ scratch, int n,
                                                        const int32_t* __restrict__ d_count,
@@ -1507,83 +1506,50 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     __shared__ __attribute__((aligned(16))) char lds[LDS_S];
     SibUnit* U = (SibUnit*)(lds + SIB_U);
     float* hpart = (float*)(lds + SIB_HP);
-    __shared__ int s_ng, s_next;
-    const int count = GC ? *list_count : (d_count ? (*d_count < n ? *d_count : n) : n);
+    const int count = *list_count;
+    // XCD-aware interleave: XCD x = blockIdx % 8 takes a contiguous eighth of the list
+    // and its workgroups take its groups of SIB_G nodes in turn, so the CUs of one XCD
+    // work on neighbouring nodes -- a few roots at a time, whose maps then stay in
+    // that XCD's L2
     const int nx = gridDim.x >= 8 ? 8 : 1;
     const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
     const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
-    const int sub = (xe - xb + per - 1) / per;
-    const int beg = xb + k * sub, end = beg + sub < xe ? beg + sub : xe;
     _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
     const float* W = A.W;
     int32_t* tiles = A.tiles ? A.tiles + (GC ? 1 : 0) : nullptr;
-    int pos = beg;
     SibStamp st;
-    while (pos < end) {
+    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
         __syncthreads();  // the previous chunk's readers of U are done
-        // the next up to SIB_G nodes of the range (wave 0: ballots over 64 leaves at a time)
-        if (wave == 0) {
-            int cnt = 0, p = pos;
-            while (cnt < SIB_G && p < end) {
-                const int i = p + lane;
-                bool take = false;
-                if (i < end) {
-                    if (GC) {
-                        take = true;
-                    } else {
-                        const int ci = A.cinfo[i];
-                        take = ci >= 0 && !(ci & (1 << 30));
-                    }
-                }
-                const uint64_t m = __ballot(take);
-                const int rank = cnt + __popcll(m & ((1ull << lane) - 1));
-                if (take && rank < SIB_G) {
-                    const int b = GC ? list[i] : i;
-                    SibUnit u;
-                    const int ci = A.cinfo[b];
-                    const int o = (ci >> 8) & 0x3fffff;
-                    u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
-                    u.leaf = b;
-                    u.cell = ci & 0xff;
-                    u.base = A.meta[b];
-                    u.own = myscr + (size_t)rank * PATCH_HALVES;
-                    u.par = nullptr;
-                    u.pcell = 0;
+        const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
+        if (wave == 0 && lane < ng) {  // the chunk's nodes
+            const int b = list[pos + lane];
+            SibUnit u;
+            const int ci = A.cinfo[b];
+            const int o = (ci >> 8) & 0x3fffff;
+            u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
+            u.leaf = b;
+            u.cell = ci & 0xff;
+            u.base = A.meta[b];
+            u.own = myscr + (size_t)lane * PATCH_HALVES;
+            u.par = nullptr;
+            u.pcell = 0;
 #pragma unroll
-                    for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
-                    if (GC) {  // the parent (a root child with a patch slot)
-                        const int pa = u.base;
-                        u.pcell = A.cinfo[pa] & 0xff;
-                        u.par = A.patches + (size_t)A.pslot[pa] * PATCH_HALVES;
-                    } else {
-                        const int ps = A.pslot[b];
-                        if (ps >= 0) u.own = A.patches + (size_t)ps * PATCH_HALVES;  // it has grandchildren: its patch
-                    }
-                    U[rank] = u;
-                }
-                const int found = __popcll(m);
-                if (cnt + found > SIB_G) {  // resume after the SIB_G-th node taken
-                    const uint64_t m6 = __ballot(take && rank == SIB_G - 1);
-                    p += __ffsll((unsigned long long)m6);
-                    cnt = SIB_G;
-                } else {
-                    cnt += found;
-                    p += 64;
-                }
+            for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
+            if (GC) {  // the parent (a root child with a patch slot)
+                const int pa = u.base;
+                u.pcell = A.cinfo[pa] & 0xff;
+                u.par = A.patches + (size_t)A.pslot[pa] * PATCH_HALVES;
+            } else {
+                const int ps = A.pslot[b];
+                if (ps >= 0) u.own = A.patches + (size_t)ps * PATCH_HALVES;  // it has grandchildren: its patch
             }
-            if (lane == 0) {
-                s_ng = cnt;
-                s_next = p;
-            }
+            U[lane] = u;
         }
         __syncthreads();
-        const int ng = s_ng;
-        pos = s_next;
-        if (ng == 0) continue;
         st(0);
 #ifdef GZ_PVINC_STAMPS
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, (unsigned long long)ng);
@@ -1759,7 +1725,8 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
                                   const int32_t* __restrict__ ord, const int32_t* __restrict__ pslot,
                                   const uint32_t* __restrict__ boards, int32_t* __restrict__ ctr,
                                   int32_t* __restrict__ roots, int32_t* __restrict__ full, int32_t* __restrict__ ghead,
-                                  int32_t* __restrict__ gnext, int32_t* __restrict__ cinfo) {
+                                  int32_t* __restrict__ gnext, int32_t* __restrict__ cinfo,
+                                  int32_t* __restrict__ children) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < count;
@@ -1779,8 +1746,9 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
         }
         cinfo[i] = ci;
     }
-    const uint64_t c = __ballot(child);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
+    // the root children in runs of a wave's leaves (a wave's 64 leaves keep their
+    // order; the runs land in any order): pv_sib_kernel's work list
+    wave_append(child, i, ctr + 2, children);
 }
 
 // the grandchild list in PARENT order: one thread per leaf; a parent with a patch
@@ -1822,7 +1790,8 @@ extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
                                          int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
                                          int32_t* d_roots, int32_t* d_full, int32_t* d_grand, int32_t* d_ghead,
-                                         int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo, void* stream) {
+                                         int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo,
+                                         int32_t* d_children, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess ||
         (patch_cap > 0 && hipMemsetAsync(d_ghead, 0xff, (size_t)patch_cap * sizeof(int32_t), s) != hipSuccess)) {
@@ -1833,7 +1802,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
     tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_boards, patch_cap, d_pslot, d_ctr);
     tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_boards, d_ctr, d_roots, d_full, d_ghead,
-                                        d_gnext, d_cinfo);
+                                        d_gnext, d_cinfo, d_children);
     tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1847,7 +1816,8 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles, int grid,
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
+                                         const int32_t* d_children, const int32_t* d_nchildren, int grid,
                                          void* stream) {
     TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
     // GZ_PVINC_SIB=0: the one-node-per-workgroup kernels (A/B reference for tools/ab.sh)
@@ -1857,7 +1827,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
     }();
     hipStream_t s = (hipStream_t)stream;
     if (sib) {
-        pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, nullptr, nullptr);
+        pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_children, d_nchildren);
         pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
     } else {
         pv_child_kernel<<<grid, NTC, 0, s>>>(A, n, d_count);

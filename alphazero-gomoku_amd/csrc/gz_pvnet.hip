@@ -941,12 +941,14 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
 extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const int32_t* d_count, int32_t root_cap,
                                          int32_t patch_cap, int32_t* d_ord, int32_t* d_pslot, int32_t* d_ctr,
                                          int32_t* d_roots, int32_t* d_full, int32_t* d_grand, int32_t* d_ghead,
-                                         int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo, void* stream);
+                                         int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo,
+                                         int32_t* d_children, void* stream);
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
-                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles, int grid,
+                                         const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
+                                         const int32_t* d_children, const int32_t* d_nchildren, int grid,
                                          void* stream);
 
 namespace {
@@ -956,7 +958,7 @@ constexpr size_t SIB_SCRATCH_HALVES = 6 * (size_t)PV_PATCH_HALVES;  // per workg
 inline int32_t patch_cap_of(int32_t root_cap) { return 16 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;
-    int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *cinfo, *ghead, *ctr;
+    int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *cinfo, *children, *ghead, *ctr;
     _Float16* maps;
     _Float16* patches;
     _Float16* scratch;  // pv_sib_kernel: 6 patch-sized areas per workgroup
@@ -967,7 +969,7 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     TreeWs t;
     t.hbuf = (float*)p;
     p += al256(m * HSTRIDE * sizeof(float));
-    int32_t** arrays[7] = {&t.ord, &t.pslot, &t.roots, &t.full, &t.grand, &t.gnext, &t.cinfo};
+    int32_t** arrays[8] = {&t.ord, &t.pslot, &t.roots, &t.full, &t.grand, &t.gnext, &t.cinfo, &t.children};
     for (auto a : arrays) {
         *a = (int32_t*)p;
         p += al256(m * 4);
@@ -987,7 +989,7 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
 
 extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
-    return al256(m * HSTRIDE * sizeof(float)) + 7 * al256(m * 4) + 256 + al256((size_t)patch_cap_of(root_cap) * 4) +
+    return al256(m * HSTRIDE * sizeof(float)) + 8 * al256(m * 4) + 256 + al256((size_t)patch_cap_of(root_cap) * 4) +
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
            (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16) +
            (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
@@ -1008,7 +1010,8 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     hipStream_t s = (hipStream_t)stream;
     TreeWs t = tree_carve(d_workspace, n, root_cap);
     int rc = gz_internal_tree_classify(d_meta, n, d_count, root_cap, patch_cap_of(root_cap), t.ord, t.pslot, t.ctr,
-                                       t.roots, t.full, t.grand, t.ghead, t.gnext, d_boards, t.cinfo, stream);
+                                       t.roots, t.full, t.grand, t.ghead, t.gnext, d_boards, t.cinfo, t.children,
+                                       stream);
     if (rc) return rc;
     const int grid = pv_grid(n);
     // roots (full forward, maps stored), then every board without a stored root or
@@ -1019,7 +1022,8 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
-                                   t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, grid, stream);
+                                   t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, t.children, t.ctr + 2, grid,
+                                   stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
