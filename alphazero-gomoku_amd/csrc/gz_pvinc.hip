@@ -1133,6 +1133,22 @@ __device__ __forceinline__ void sib_conv(const _Float16* act, const int (&ctr)[N
     }
 }
 
+// A node's recomputed squares: plain stores.  SIB_SQ_PLAIN=0 writes them as
+// agent-scope (sc1) stores, which do not keep their lines in the XCD's L2
+// (MI355X_MICROARCH.md, stores), to leave L2 to the roots' maps: HBM-side fetches
+// 220 -> 194 GB per launch but 2.6 % slower (143.1 vs 146.9 ms), so off.
+#ifndef SIB_SQ_PLAIN
+#define SIB_SQ_PLAIN 1
+#endif
+__device__ __forceinline__ void sq_store(_Float16* p, h4 v) {
+    if (SIB_SQ_PLAIN) {
+        *(h4*)p = v;
+    } else {
+        typedef __attribute__((address_space(1))) uint64_t g64;  // a global (not flat) store
+        __hip_atomic_store((g64*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // conv0's im2col for every unit (16 rows x 32 k fp16 each, the columns tree_node
 // stages), all units in parallel, into col (the head-partials area, dead during y1)
 __device__ __forceinline__ void sib_col(_Float16* col, const SibUnit* U, int ng, int tid) {
@@ -1209,8 +1225,8 @@ __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const 
                 *(h4*)(xw + off) = hi;
                 *(h4*)(xw + Win<3>::plane() + off) = lo;
                 _Float16* d = u.own + PATCH_OFF[0] + ((ch0 >> 3) * 9 + (pr - cr + 1) * 3 + (pc - cc + 1)) * 8 + (ch0 & 7);
-                *(h4*)d = hi;
-                *(h4*)(d + 16 * 9 * 8) = lo;
+                sq_store(d, hi);
+                sq_store(d + 16 * 9 * 8, lo);
             }
         }
     }
@@ -1361,8 +1377,8 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
                 lo[r] = (_Float16)(y - (float)h);
             }
             _Float16* d = dst[m] + (ch0 >> 3) * SS * 8 + (ch0 & 7);
-            *(h4*)d = hi;
-            *(h4*)(d + 16 * SS * 8) = lo;
+            sq_store(d, hi);
+            sq_store(d + 16 * SS * 8, lo);
         }
     }
 }
@@ -1726,7 +1742,7 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
                                   const uint32_t* __restrict__ boards, int32_t* __restrict__ ctr,
                                   int32_t* __restrict__ roots, int32_t* __restrict__ full, int32_t* __restrict__ ghead,
                                   int32_t* __restrict__ gnext, int32_t* __restrict__ cinfo,
-                                  int32_t* __restrict__ children) {
+                                  int32_t* __restrict__ wcount) {
     const int count = d_count ? (*d_count < n ? *d_count : n) : n;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < count;
@@ -1746,9 +1762,62 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
         }
         cinfo[i] = ci;
     }
-    // the root children in runs of a wave's leaves (a wave's 64 leaves keep their
-    // order; the runs land in any order): pv_sib_kernel's work list
-    wave_append(child, i, ctr + 2, children);
+    // root children: counted here, listed in leaf order by tree_children_kernel
+    const uint64_t c = __ballot(child);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(ctr + 2, __popcll(c));
+    if ((threadIdx.x & 63) == 0 && i < n) wcount[i >> 6] = __popcll(c);  // lane 0: i = 64 w
+}
+
+// pv_sib_kernel's work list: the root children in LEAF order (a root's children are
+// adjacent leaves, so neighbouring list entries share a root's maps).  wcount[w] =
+// root children among leaves [64 w, 64 w + 64) (tree_lists_kernel); one workgroup
+// of 1024 threads scans the counts in tiles, then each wave writes its leaves' list
+// entries.  cinfo >= 0 with bit 30 clear marks a root child.
+__global__ __launch_bounds__(1024) void tree_children_kernel(int n, const int32_t* __restrict__ d_count,
+                                                            const int32_t* __restrict__ cinfo,
+                                                            int32_t* __restrict__ wcount,
+                                                            int32_t* __restrict__ children) {
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int nw = (count + 63) >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    // exclusive scan of wcount in place, 1024 entries per tile
+    for (int t0 = 0; t0 < nw; t0 += 1024) {
+        const int w = t0 + tid;
+        const int v = w < nw ? wcount[w] : 0;
+        int x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        if (tid < 16) {
+            int y = wsum[tid];
+            for (int d = 1; d < 16; d <<= 1) {
+                const int z = __shfl_up(y, d, 16);
+                if (tid >= d) y += z;
+            }
+            wsum[tid] = y;  // inclusive over waves
+        }
+        __syncthreads();
+        const int base = carry + (wv ? wsum[wv - 1] : 0);
+        if (w < nw) wcount[w] = base + x - v;
+        __syncthreads();
+        if (tid == 0) carry += wsum[15];
+        __syncthreads();
+    }
+    // each wave: its 64-leaf groups, children in lane order at the group's offset
+    for (int w = wv; w < nw; w += 16) {
+        const int i = w * 64 + lane;
+        const int ci = i < count ? cinfo[i] : -1;
+        const bool child = ci >= 0 && !(ci & (1 << 30));
+        const uint64_t m = __ballot(child);
+        if (child) children[wcount[w] + __popcll(m & ((1ull << lane) - 1))] = i;
+    }
 }
 
 // the grandchild list in PARENT order: one thread per leaf; a parent with a patch
@@ -1801,8 +1870,11 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     const int g = (n + 255) / 256;
     tree_roots_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, root_cap, d_ord, d_pslot, d_ctr);
     tree_patch_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_boards, patch_cap, d_pslot, d_ctr);
+    // per-wave child counts: past the list's n entries (d_children has n + n / 64 + 1)
+    int32_t* wcount = d_children + n;
     tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_boards, d_ctr, d_roots, d_full, d_ghead,
-                                        d_gnext, d_cinfo, d_children);
+                                        d_gnext, d_cinfo, wcount);
+    tree_children_kernel<<<1, 1024, 0, s>>>(n, d_count, d_cinfo, wcount, d_children);
     tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -969,11 +969,13 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     TreeWs t;
     t.hbuf = (float*)p;
     p += al256(m * HSTRIDE * sizeof(float));
-    int32_t** arrays[8] = {&t.ord, &t.pslot, &t.roots, &t.full, &t.grand, &t.gnext, &t.cinfo, &t.children};
+    int32_t** arrays[7] = {&t.ord, &t.pslot, &t.roots, &t.full, &t.grand, &t.gnext, &t.cinfo};
     for (auto a : arrays) {
         *a = (int32_t*)p;
         p += al256(m * 4);
     }
+    t.children = (int32_t*)p;  // n entries + the per-wave counts of tree_children_kernel
+    p += al256((m + m / 64 + 1) * 4);
     t.ctr = (int32_t*)p;
     p += 256;
     t.ghead = (int32_t*)p;
@@ -989,7 +991,8 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
 
 extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
-    return al256(m * HSTRIDE * sizeof(float)) + 8 * al256(m * 4) + 256 + al256((size_t)patch_cap_of(root_cap) * 4) +
+    return al256(m * HSTRIDE * sizeof(float)) + 7 * al256(m * 4) + al256((m + m / 64 + 1) * 4) + 256 +
+           al256((size_t)patch_cap_of(root_cap) * 4) +
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
            (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16) +
            (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);

@@ -84,7 +84,7 @@ def load_traffic(boards, mode):
 def load_clock(kernel):
     """Measured shader clock and MFMA-busy share of `kernel` under load (newest
     profiles/rNN/clock.json that has it), or None."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         p = os.path.join(REPO, "profiles", rnd, "clock.json")
         if os.path.exists(p):
             with open(p) as f:
@@ -101,18 +101,25 @@ def _cpu_worker(task):
     per-ply work (ai_agent.py:168-204 + GomokuModel.predict per node).  With
     planner_steps > 0 every rollout starts with BG-planner plies whose GraphNet +
     OpponentDQN forwards also run on torch CPU (bg_planner.py:243-250)."""
-    black, white, n_moves, player, gid, sims, seed, budget, threads, beta, planner_steps = task
+    positions, sims, seed, budget, threads, beta, planner_steps = task
     import torch as T
     T.set_num_threads(threads)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from gzero.boards import words_to_cells, planes_from_cells
-    cells = words_to_cells(black, white)
-    b = O.Board()
-    O.lib().or_board_init(b)
-    for i in range(225):
-        b.cell[i] = int(cells[i])
-    b.n_moves, b.player = int(n_moves), int(player)
+
+    def start(k):  # the k-th start position (cycled); a finished game moves to the next
+        black, white, n_moves, player, gid = positions[k % len(positions)]
+        cells = words_to_cells(black, white)
+        b = O.Board()
+        O.lib().or_board_init(b)
+        for i in range(225):
+            b.cell[i] = int(cells[i])
+        b.n_moves, b.player = int(n_moves), int(player)
+        return b, gid
+
+    k = 0
+    b, gid = start(k)
     net = weights.PolicyValueNet()
     net.load_state_dict(weights.init_state_dict(0))
     net.eval()
@@ -132,7 +139,10 @@ def _cpu_worker(task):
     p = O.make_params("medium", sims=sims, beta=beta, seed=seed, planner_steps=planner_steps, pq=pq)
     t0 = time.perf_counter()
     plies = predicts = 0
-    while not b.over and time.perf_counter() - t0 < budget:
+    while time.perf_counter() - t0 < budget:
+        if b.over:
+            k += 1
+            b, gid = start(k)
         root = np.frombuffer(bytes(b.cell), dtype=np.int8).copy()
         mv, tree = O.get_move(b, b.player, p, gid, cap=4096)
         # the forwards of this ply's nodes: every node's board (root + path stones);
@@ -204,7 +214,8 @@ def cpu_baseline(pool, procs, positions, sims, seed, budget_s):
     aff, _ = host_cores()
     cpu = cpu_model()
     runs = []
-    tasks = [positions[i % len(positions)] + (sims, seed, budget_s, 1, 0.0, 0) for i in range(procs)]
+    # worker i starts at position i and moves on through the list when its game ends
+    tasks = [(positions[i:] + positions[:i], sims, seed, budget_s, 1, 0.0, 0) for i in range(procs)]
     t0 = time.perf_counter()
     res = pool.map(_cpu_worker, tasks)
     wall = time.perf_counter() - t0
@@ -212,13 +223,13 @@ def cpu_baseline(pool, procs, positions, sims, seed, budget_s):
     runs.append({"run": f"config 2 work: {procs} processes x 1 thread", "value": plies / wall, "unit": "moves/s",
                  "per_core": plies / wall / procs, "plies": plies, "forwards": predicts, "wall_s": round(wall, 2),
                  "cores": procs})
-    one = pool.apply(_cpu_worker, (positions[0] + (sims, seed, budget_s, procs, 0.0, 0),))
+    one = pool.apply(_cpu_worker, ((positions, sims, seed, budget_s, procs, 0.0, 0),))
     runs.append({"run": f"config 2 work: 1 process x {procs} threads", "value": one[0] / one[2], "unit": "moves/s",
                  "per_core": one[0] / one[2] / procs, "plies": one[0], "forwards": one[1],
                  "wall_s": round(one[2], 2), "cores": procs})
-    empty = (np.zeros(8, np.uint32), np.zeros(8, np.uint32), 0, 1, 0)
-    c1 = pool.apply(_cpu_worker, (empty + (50, seed, budget_s, procs, 0.2, 5),))
-    runs.append({"run": f"config 1: 1 game, 50 sims, beta 0.2, planner_steps 5; 1 process x {procs} threads",
+    empty = [(np.zeros(8, np.uint32), np.zeros(8, np.uint32), 0, 1, g) for g in range(4)]
+    c1 = pool.apply(_cpu_worker, ((empty, 50, seed, budget_s, procs, 0.2, 5),))
+    runs.append({"run": f"config 1 (50 sims, beta 0.2, planner_steps 5, medium) from the empty board; 1 process x {procs} threads",
                  "value": c1[0] / c1[2], "unit": "moves/s", "per_core": c1[0] / c1[2] / procs, "plies": c1[0],
                  "forwards": c1[1], "wall_s": round(c1[2], 2), "cores": procs})
     for r in runs:
@@ -304,6 +315,43 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
     }
 
 
+def config5(games, sims, seed, iterations=2):
+    """BASELINE config 5 on one GPU: training.main's iteration (training.run_iteration:
+    self-play of `games` games with the reference's default AI -- medium, `sims` sims,
+    beta 0.2, planner_steps 5, PV forward on every node -- through the sync-free record
+    exchange, the 35 % 8-fold augmented dataset, 2 epochs of SGD, the StepLR step),
+    `iterations` times; iterations/h from the last (the first pays MIOpen's kernel
+    selection)."""
+    import random
+    import training
+    from gzero.train import DeviceTrainer
+    from neural_network import GomokuModel
+    random.seed(seed)
+    torch.manual_seed(seed)
+    model = GomokuModel(device="cuda")
+    trainer = DeviceTrainer(model)
+    its = []
+    for it in range(1, iterations + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = training.run_iteration(model, trainer, it, games, num_simulations=sims, planner_steps=5, beta=0.2,
+                                   seed=seed, verbose=False)
+        torch.cuda.synchronize()
+        r["iteration_s"] = time.perf_counter() - t0
+        its.append(r)
+    last = its[-1]
+    return {"value": round(3600.0 / last["iteration_s"], 2), "unit": "iterations/h",
+            "iteration_s": round(last["iteration_s"], 2), "selfplay_s": round(last["selfplay_s"], 2),
+            "sgd_s": round(last.get("sgd_s", 0.0), 2), "records": last["records"],
+            "samples": last.get("samples"), "moves_played": last["moves_played"],
+            "first_iteration_s": round(its[0]["iteration_s"], 2),
+            "workload": (f"BASELINE config 5 on 1 GPU: training.run_iteration with {games} self-play games per "
+                         f"iteration ({sims} sims, medium, beta 0.2, planner_steps 5, tree PV forward on every node, "
+                         "records through gzero.dist.RecordExchange), 35 % augmentation, 2 epochs of SGD "
+                         "(batch 128, Adam 8e-4, clip 0.8, torch/MIOpen fp32), StepLR; value from the last of "
+                         f"{iterations} iterations")}
+
+
 def roofline_of(m, precision):
     mean_leaves = float(np.mean(m["leaves"]))
     mean_pv_s = float(np.mean(m["pv_ms"])) / 1e3
@@ -363,10 +411,11 @@ def roofline_of(m, precision):
         "note": note,
     }
     if tree:
-        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + untagged nodes, pv_child_kernel on "
-                       "root children, pv_grandchild_kernel on their children, pv_heads_kernel, pv_prior_kernel)")
+        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + untagged nodes, pv_sib_kernel on "
+                       "root children and, second launch, on their children; pv_heads_kernel, pv_prior_kernel)")
         r["incremental"] = tree
-    dominant = "pv_child_kernel" if tree else ("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32")
+    dominant = (("pv_sib_kernel" if os.environ.get("GZ_PVINC_SIB", "1") != "0" else "pv_child_kernel") if tree
+                else ("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32"))
     clk = load_clock(dominant)
     if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
         r["clock"] = {"kernel": dominant, "ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
@@ -405,6 +454,9 @@ def main():
     ap.add_argument("--config4-steps", type=int, default=20,
                     help="N = 1 secondary: BASELINE config 4 (beta 0.2, planner_steps 5) timed over this many "
                          "steps after the same burn-in (0 = skip)")
+    ap.add_argument("--config5-games", type=int, default=512,
+                    help="N = 1 secondary: BASELINE config 5 (training iterations/h) with this many self-play games "
+                         "per iteration (0 = skip)")
     ap.add_argument("--fp32-steps", type=int, default=4,
                     help="N = 1 secondary: the exact-fp32 PV forward timed over this many steps (0 = skip)")
     args = ap.parse_args()
@@ -525,6 +577,10 @@ def main():
                        "roofline": roofline_of(m32, "fp32"),
                        "note": "config 2 with the exact-f32 MFMA forward (v_mfma_f32_16x16x4_f32)"}
         del e32, w32
+
+    # ---- N = 1 secondary: config 5 (training iterations per hour)
+    if ws == 1 and args.config5_games and not args.planner_steps:
+        out["config5"] = config5(args.config5_games, args.sims, args.seed)
 
     # ---- prior-elided run (same kernel, no PV gather / forward)
     if not args.no_elided and not args.planner_steps:
