@@ -14,6 +14,7 @@ The dataset / augmentation / SGD helpers follow the reference's definitions
 rotation for k = 1, 3 -- kept by default, ``fix_labels=True`` corrects it).
 """
 import random
+import re
 import time
 from typing import List, Optional, Tuple
 
@@ -116,7 +117,12 @@ def _is_device_failure(e: BaseException) -> bool:
     from gzero._lib import GzeroError, GzeroUnavailable
     if isinstance(e, (GzeroUnavailable, GzeroError)):
         return True
-    return isinstance(e, RuntimeError) and any(s in str(e) for s in ("HIP", "hip", "CUDA", "cuda", "device-side"))
+    # whole words only: "relationship" / "ownership" in an AI-logic error must
+    # still fall back to a random move as the reference does
+    return isinstance(e, RuntimeError) and _DEVICE_ERR.search(str(e)) is not None
+
+
+_DEVICE_ERR = re.compile(r"\b(?:HIP|hip|CUDA|cuda)\b|\b(?:hip|cuda)[A-Z]\w*|device-side")
 
 
 def play_one_game(ai_black, ai_white, step_timeout: float = 10.0,

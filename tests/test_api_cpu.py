@@ -79,6 +79,19 @@ def test_simple_replay_finalize():
     assert r2.outcomes == [0]
 
 
+def test_device_failure_matches_whole_words_only():
+    """play_one_game re-raises device errors but, like the reference
+    (training.py:191-198), plays a random move after any other AI error."""
+    from training import _is_device_failure
+    from gzero._lib import GzeroError
+    assert _is_device_failure(RuntimeError("HIP error: an illegal memory access was encountered"))
+    assert _is_device_failure(RuntimeError("hipErrorOutOfMemory in hipMalloc"))
+    assert _is_device_failure(RuntimeError("CUDA error: device-side assert triggered"))
+    assert _is_device_failure(GzeroError("gz_selfplay_step failed"))
+    assert not _is_device_failure(RuntimeError("bad relationship between ownership and chips"))
+    assert not _is_device_failure(ValueError("HIP error"))
+
+
 def test_device_paths_fail_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
