@@ -63,4 +63,25 @@ constexpr int TOTAL = D2_P + 16 * 15 * 256;
 //   [REC_X, REC_X + 450) the one-hot stone inputs [black 225 | white 225], zero to REC
 constexpr int REC_X = 464;
 constexpr int REC = 928;
+
+// Incremental GraphNet (gn_inc_kernel): a map slot holds one board's 4 conv inputs
+// embed, L1, L3, L5 (each [plane hi/lo][cg 8][225][8] halves) and its policy-conv
+// output (450 floats, channel-major, padded to 512)
+constexpr int SLOT_MAP_HALVES = 2 * 8 * POS * 8;   // 28,800
+constexpr int SLOT_POL = 4 * SLOT_MAP_HALVES / 2;  // floats from the slot start
+constexpr size_t SLOT_BYTES = (size_t)4 * SLOT_MAP_HALVES * 2 + 512 * 4;
+
+// one GN row's incremental tag (written by gz_plan.hip's collect kernel)
+constexpr int TAG_STONES = 6;
+struct GnTag {
+    int32_t mode;  // 0: full forward, maps stored into slot `job`; 1: incremental
+    int32_t base;  // slot of the maps the board adds stones to
+    int32_t job;   // slot this row writes its maps (and policy-conv output) to
+    int32_t cell;  // incremental: the new stone (r*15+c)
+    int32_t nst;   // stones already added to `base` whose squares live in slot `job`
+    uint8_t st[TAG_STONES];
+    uint8_t pad[2];
+    int32_t pad2;
+};
+static_assert(sizeof(GnTag) == 32, "tag size");
 }  // namespace gzgn

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <type_traits>
 
 #include "gz_f16conv.h"
 #include "gz_gnet.h"
@@ -80,8 +81,19 @@ __device__ __forceinline__ void gn_store(ActF16x3& act, const f32x4 (&acc)[2][NM
 
 // embed conv MFMAs (fragments from the im2col in act.hi) and the 8 tower layers
 // for a wave owning NMW M tiles from m0; every barrier of the board's tower is here
+// the map in LDS (all 225 positions) -> map slot map `m` ([plane][cg][225][8] halves)
+__device__ __forceinline__ void gn_store_map(const ActF16x3& act, _Float16* __restrict__ slot, int m) {
+    _Float16* dst = slot + (size_t)m * SLOT_MAP_HALVES;
+    for (int i = threadIdx.x; i < 2 * 8 * POS; i += NT) {
+        const int pcg = i / POS, pos = i - pcg * POS;
+        const _Float16* src = (pcg < 8 ? act.hi : act.lo) + ((pcg & 7) * ROWS16 + pos) * 8;
+        *(uint4*)(dst + (size_t)i * 8) = *(const uint4*)src;
+    }
+}
+
 template <int NMW>
-__device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict__ W, int np, int m0, int lane) {
+__device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict__ W, int np, int m0, int lane,
+                                         _Float16* __restrict__ slot) {
     {
         const _Float16* col = act.hi;
         const int li = lane & 15, q = lane >> 4;
@@ -108,6 +120,7 @@ __device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict_
         gn_store<NMW>(act, acc, W + GE_B, np, m0, lane);
     }
     __syncthreads();
+    if (slot) gn_store_map(act, slot, 0);  // (read only: the next write to act follows a barrier)
     GN_STAMP(2);
 
     // ---- 4 x [conv3x3 + ReLU, conv1x1 + ReLU] (bg_planner.py:50-54)
@@ -127,14 +140,38 @@ __device__ __forceinline__ void gn_tower(ActF16x3& act, const float* __restrict_
         else GN_STAMP(5);
         gn_store<NMW>(act, acc, W + layer_bias(i), np, m0, lane);
         __syncthreads();
+        if (slot && (i & 1) && i < 7) gn_store_map(act, slot, (i + 1) / 2);  // L1, L3, L5: the 3x3 inputs
         if (i % 2 == 0) GN_STAMP(4);
         else GN_STAMP(6);
     }
 }
 
+// the policy conv 1x1 64->2 at one position (bg_planner.py:45): hp / lp = the
+// position's channel group 0 in the hi / lo plane, cgs = the channel-group stride
+__device__ __forceinline__ void gn_pconv(const float* __restrict__ W, const _Float16* hp, const _Float16* lp, int cgs,
+                                         float& o0, float& o1) {
+    float p0 = W[GP_B], p1 = W[GP_B + 1];
+    for (int c0 = 0; c0 < HID; c0 += 8) {
+        const h8 xh = *(const h8*)(hp + (c0 >> 3) * cgs);
+        const h8 xl = *(const h8*)(lp + (c0 >> 3) * cgs);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float a = (float)xh[j] + (float)xl[j];
+            p0 = __builtin_fmaf(W[GP_W + c0 + j], a, p0);
+            p1 = __builtin_fmaf(W[GP_W + HID + c0 + j], a, p1);
+        }
+    }
+    o0 = p0;
+    o1 = p1;
+}
+
+// boards b = list[i] (list: NULL = 0..count-1).  slots (optional): every board's
+// maps and policy-conv output also go to a map slot -- tags[b].job, or slot b
+// when tags is NULL (the search roots)
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void gn_kernel(
     const float* __restrict__ W, const uint32_t* __restrict__ boards, int n, const int32_t* d_count,
-    float* __restrict__ rec) {
+    float* __restrict__ rec, const int32_t* __restrict__ list, char* __restrict__ slots,
+    const GnTag* __restrict__ tags) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     ActF16x3 act;
     act.hi = (_Float16*)lds;
@@ -151,7 +188,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         planes[(i / (PROWS - POS)) * PROWS + POS + i % (PROWS - POS)] = 0.f;
 
     GN_STAMP(30);
-    for (int b = blockIdx.x; b < count; b += gridDim.x) {
+    for (int i = blockIdx.x; i < count; i += gridDim.x) {
+        const int b = list ? list[i] : i;
+        _Float16* slot = nullptr;
+        if (slots) slot = (_Float16*)(slots + (size_t)(tags ? tags[b].job : b) * SLOT_BYTES);
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -202,9 +242,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         }
         // waves 6-7 own M tiles 12-14 only (tile 15 is all zero rows): 15 tiles, not 16
         if ((wave >> 1) == 3)
-            gn_tower<NM - 1>(act, W, np, m0, lane);
+            gn_tower<NM - 1>(act, W, np, m0, lane, slot);
         else
-            gn_tower<NM>(act, W, np, m0, lane);
+            gn_tower<NM>(act, W, np, m0, lane, slot);
 
         // ---- policy head conv1x1 64->2 (one thread per position), flattened
         // channel-major into the record.  The next board's first LDS write that
@@ -212,18 +252,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         int tid_h = threadIdx.x;  // re-read (not kept live across the tower)
         asm volatile("" : "+v"(tid_h));
         if (tid_h < POS) {
-            float p0 = W[GP_B], p1 = W[GP_B + 1];
-            for (int c0 = 0; c0 < HID; c0 += 8) {
-                float a[8];
-                act.get8(c0, tid_h, a);
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    p0 += W[GP_W + c0 + j] * a[j];
-                    p1 += W[GP_W + HID + c0 + j] * a[j];
-                }
-            }
+            float p0, p1;
+            gn_pconv(W, act.hi + tid_h * 8, act.lo + tid_h * 8, ROWS16 * 8, p0, p1);
             rb[tid_h] = p0;
             rb[POS + tid_h] = p1;
+            if (slot) {
+                float* pol = (float*)slot + SLOT_POL;
+                pol[tid_h] = p0;
+                pol[POS + tid_h] = p1;
+            }
         }
         GN_STAMP(7);
     }
@@ -372,6 +409,608 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
     }
 }
 
+
+// ============================================================ incremental GraphNet
+// A planner ply's board is its predecessor plus one stone (bg_planner.py:243-250 on
+// the board _simulate's previous ply left, ai_agent.py:265-271), and a rollout's
+// first board is usually the search root plus the expanded child's stone.  GraphNet
+// (embed 3x3, then 4 x [3x3, 1x1]) has receptive radius 5, so a board that adds
+// stone c to a board whose maps are kept only changes, at each layer's output,
+// the square of radius 1 (embed), 2 (L0, L1), 3 (L2, L3), 4 (L4, L5), 5 (L6, L7)
+// around c.  gn_inc_kernel recomputes just those squares, IG boards per chunk,
+// layer-major: each 3x3 layer reads the windows (square radius + 1) of its input
+// map, assembled in LDS from the layer's own new square and, elsewhere, the stored
+// maps (LDS-DMA); the 1x1 layers read the new square only.  The policy conv then
+// runs on the radius-5 square; the rest of the 450 policy-conv outputs are the
+// predecessor's.  The stored maps are the 3x3 inputs (embed, L1, L3, L5, map
+// slots in gz_gnet.h): a chain of boards keeps its base's maps (the search root's,
+// or a full forward's) plus, in its own slot, the squares of the stones added since
+// (a window position inside one of those squares reads the slot, else the base).
+// Every output element takes gn_kernel's products in gn_kernel's order (the same
+// k-steps, MFMA operand splits and epilogues), so the records -- and p, q from
+// gn_heads_kernel -- are bitwise those of the full forward.
+constexpr int IG = 3;                     // boards per chunk
+constexpr int NTI = 512;                  // 8 waves: n-tile wave & 3, M half wave >> 2
+constexpr int IWIN_MAX = 169 * 256;       // bytes of a radius-6 window (2 planes x 8 cg x 169 x 16 B)
+constexpr int IA = IG * IWIN_MAX;         // windows / square rows
+constexpr int ICOL = IA;                  // embed im2col [IG][4][16][8] halves
+constexpr int IPC = ICOL + IG * 1024;     // policy-conv outputs [IG][2][128] floats
+constexpr int IU = IPC + IG * 2 * 128 * 4;
+constexpr int ITAB = IU + IG * 128;         // row tables of the radius 1..5 passes, then their totals
+__host__ __device__ constexpr int itab_off(int ro) { return ro <= 1 ? 0 : itab_off(ro - 1) + IG * (2 * ro - 1) * (2 * ro - 1); }
+constexpr int ITOT = itab_off(6);            // 855 entries
+constexpr int ILDS = ITAB + (ITOT + 8) * 4;
+constexpr int IROWS = 368;                // >= IG x 121 square rows, x16
+static_assert(ILDS <= 160 * 1024 && 2 * 8 * IROWS * 16 <= IA && IG * 121 <= IROWS, "LDS");
+
+struct GnUnit {
+    const _Float16* base;  // maps the chain adds stones to
+    _Float16* job;         // this row's slot (its new squares; earlier stones' squares)
+    const float* pol_src;  // policy-conv outputs of the predecessor
+    float* pol_job;
+    float* rec;            // the row's record (gn_heads_kernel input)
+    int32_t cell, nst;
+    uint8_t st[8];
+    uint32_t board[16];
+    int32_t pad[2];
+};
+static_assert(sizeof(GnUnit) == 128, "unit");
+
+typedef __attribute__((address_space(3))) void ig_lds_t;
+typedef __attribute__((address_space(1))) void ig_glb_t;
+__device__ uint4 gz_gn_zero16[1];  // zero-initialised (off-board window positions)
+
+__device__ __forceinline__ int iabs_(int x) { return x < 0 ? -x : x; }
+
+struct Sq {  // clipped square around a cell: rows r0.., cols c0.., h x w
+    int r0, c0, h, w;
+};
+__device__ __forceinline__ Sq square(int cell, int rad) {
+    const int cr = cell / 15, cc = cell - (cell / 15) * 15;
+    Sq q;
+    q.r0 = cr - rad > 0 ? cr - rad : 0;
+    q.c0 = cc - rad > 0 ? cc - rad : 0;
+    q.h = (cr + rad < 14 ? cr + rad : 14) - q.r0 + 1;
+    q.w = (cc + rad < 14 ? cc + rad : 14) - q.c0 + 1;
+    return q;
+}
+
+__device__ __forceinline__ const _Float16* ig_rfl(const _Float16* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const _Float16*)(((uint64_t)hi << 32) | lo);
+}
+
+// window of map MAP (radius R = MAP + 3, [plane][8 cg][P][8] halves) for every unit,
+// unit g at halves g * P * 128: LDS-DMA of every on-board position outside the
+// unit's new square (radius MAP + 1, written by the producing epilogue), zeros off
+// the board; drained by the caller's barrier
+template <int MAP>
+__device__ __forceinline__ void ig_fill(char* lds, const GnUnit* U, int ng, int tid) {
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 16 * P, IT = (PER + NTI - 1) / NTI, rc = MAP + 1;
+    const int wb = tid & ~63;
+    for (int g = 0; g < ng; g++) {
+        const _Float16* base = ig_rfl(U[g].base) + MAP * SLOT_MAP_HALVES;
+        const _Float16* job = ig_rfl(U[g].job) + MAP * SLOT_MAP_HALVES;
+        const int cell = __builtin_amdgcn_readfirstlane(U[g].cell), nst = __builtin_amdgcn_readfirstlane(U[g].nst);
+        const int cr = cell / 15, cc = cell - cr * 15;
+        char* dst = lds + (size_t)g * P * 256;
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = tid + k * NTI;
+            if ((k + 1) * NTI > PER && i >= PER) continue;
+            const int pcg = i / P, loc = i - pcg * P;
+            const int dr = loc / Wd - R, dc = loc % Wd - R;
+            const int pr = cr + dr, pc = cc + dc;
+            const bool on = pr >= 0 && pr < 15 && pc >= 0 && pc < 15;
+            if (on && iabs_(dr) <= rc && iabs_(dc) <= rc) continue;  // the new square (its epilogue writes it)
+            const void* src = (const void*)gz_gn_zero16;
+            if (on) {
+                bool mine = false;
+                for (int s = 0; s < nst; s++) {
+                    const int sc = U[g].st[s], sr = sc / 15, scc = sc - sr * 15;
+                    mine |= iabs_(pr - sr) <= rc && iabs_(pc - scc) <= rc;
+                }
+                src = (const void*)((mine ? job : base) + ((size_t)pcg * POS + pr * 15 + pc) * 8);
+            }
+            __builtin_amdgcn_global_load_lds((ig_glb_t*)src, (ig_lds_t*)(dst + (size_t)(wb + k * NTI) * 16), 16, 0, 0);
+        }
+    }
+}
+
+// the rows of a pass: every unit's square of radius ro (clipped, row-major), packed;
+// row i -> unit g, position (pr, pc), index j in its square
+struct IgRow {
+    int g, pr, pc, j;
+};
+__device__ __forceinline__ IgRow ig_row(const char* lds, int ro, int i) {
+    const int v = ((const int*)(lds + ITAB))[itab_off(ro) + i];
+    IgRow r;
+    r.g = v & 3;
+    r.pr = (v >> 2) & 15;
+    r.pc = (v >> 6) & 15;
+    r.j = v >> 10;
+    return r;
+}
+__device__ __forceinline__ int ig_total(const char* lds, int ro) { return ((const int*)(lds + ITAB))[ITOT + ro]; }
+
+// the row tables of a chunk (every radius), built once by the whole workgroup:
+// entry i of radius ro = unit | pr << 2 | pc << 6 | (index in its square) << 10
+__device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng, int tid) {
+    int* tab = (int*)(lds + ITAB);
+    for (int e = tid; e < 5 * IG * 121; e += NTI) {
+        const int ro = 1 + e / (IG * 121), i = e - (ro - 1) * IG * 121;
+        int start = 0;
+        for (int g = 0; g < ng; g++) {
+            const Sq q = square(U[g].cell, ro);
+            const int n = q.h * q.w;
+            if (i >= start && i < start + n) {
+                const int j = i - start, rr = j / q.w;
+                tab[itab_off(ro) + i] = g | (q.r0 + rr) << 2 | (q.c0 + j - rr * q.w) << 6 | j << 10;
+            }
+            start += n;
+        }
+        if (i == 0) tab[ITOT + ro] = start;
+    }
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <class F, int... I>
+__device__ __forceinline__ void ig_sfor(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// 3x3 k-loop for the wave's n-tile over NT M tiles, with gn_kernel's k-steps (tap-major,
+// cq inner) and per-element product order (w_hi*a_hi, w_lo*a_hi, w_hi*a_lo).  act = the
+// windows (radius R, [plane][8 cg][P][8] halves per unit); ctr[m] = the lane's row's
+// window position (unit offset included, in units of 8 halves within a cg plane).
+// Tiles go in groups of 3 (the 3 products interleaved over the group, so no MFMA waits
+// on its predecessor's result); each group's fragments are read while the previous
+// group's MFMAs run (two fragment buffers); weight fragments 3 k-steps ahead.
+template <int NT, int NMAX, int R>
+__device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
+                                            int nt, int lane, f32x4 (&acc)[NMAX]) {
+    constexpr int Wd = 2 * R + 1, P = Wd * Wd, KS = 18, LO = 64 * P, GT = 3, NG = (NT + GT - 1) / GT;
+    const int q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = (nt * 64 + lane) * 16;
+    auto wload = [&](int ks, int lo) -> h8 {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * 4096 + lo * KS * 4096, 0));
+    };
+    h8 b[4][2];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        b[c][0] = wload(c, 0);
+        b[c][1] = wload(c, 1);
+    }
+    f32x4 c[NT];
+#pragma unroll
+    for (int m = 0; m < NT; m++) c[m] = acc[m];
+    int c8[NT];  // the lane's fragment offset (halves) of tile m at tap (0, 0), cq 0
+#pragma unroll
+    for (int m = 0; m < NT; m++) c8[m] = (ctr[m] + q * P) * 8;
+    h8 fa[2][GT][2];
+    auto toff = [&](int t) {
+        t = t < 9 ? t : t - 9;
+        return ((t / 3 - 1) * Wd + (t % 3 - 1)) * 8;
+    };
+    // fragments of tile group G for (tap, CQ) into buffer PB
+    auto load = [&](auto pb_, auto g_, auto cq_, int tap) {
+        constexpr int PB = decltype(pb_)::value, G = decltype(g_)::value, CQ = decltype(cq_)::value;
+#pragma unroll
+        for (int j = 0; j < GT; j++) {
+            const int m = G * GT + j;
+            if (m < NT) {
+                const int o = c8[m] + toff(tap) + CQ * 4 * P * 8;
+                fa[PB][j][0] = *(const h8*)(act + o);
+                fa[PB][j][1] = *(const h8*)(act + LO + o);
+            }
+        }
+    };
+    auto mfmas = [&](auto pb_, auto g_, auto sl_) {
+        constexpr int PB = decltype(pb_)::value, G = decltype(g_)::value, SL = decltype(sl_)::value;
+#pragma unroll
+        for (int j = 0; j < GT; j++)
+            if (G * GT + j < NT) c[G * GT + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[SL][0], fa[PB][j][0], c[G * GT + j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < GT; j++)
+            if (G * GT + j < NT) c[G * GT + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[SL][1], fa[PB][j][0], c[G * GT + j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < GT; j++)
+            if (G * GT + j < NT) c[G * GT + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[SL][0], fa[PB][j][1], c[G * GT + j], 0, 0, 0);
+    };
+    auto tiles_of = [](int g) { return NT - g * GT < GT ? NT - g * GT : GT; };
+    using I0 = std::integral_constant<int, 0>;
+    load(I0{}, I0{}, I0{}, 0);
+    // NK k-steps from slot 0 (ks0 = 4 tp or 16), tap0 = their first tap; items k = (k-step i, group g)
+    auto ksteps = [&](auto nk_, int ks0, int tap0) {
+        constexpr int NK = decltype(nk_)::value;
+        ig_sfor([&](auto k_) {
+            constexpr int k = decltype(k_)::value, i = k / NG, g = k % NG, pb = k & 1;
+            constexpr int kn = k + 1, in = kn / NG, gn = kn % NG;
+            if (g == 0) {  // weights of k-step ks0 + i + 3 into the slot k-step ks0 + i - 1 released
+                const int ksr = ks0 + i + 3, kn2 = ksr < KS ? ksr : ksr - KS;
+                b[(i + 3) & 3][0] = wload(kn2, 0);
+                b[(i + 3) & 3][1] = wload(kn2, 1);
+            }
+            // the next item's fragments (past the last k-step here: the next tap's cq 0)
+            if (kn < NK * NG)
+                load(std::integral_constant<int, 1 - pb>{}, std::integral_constant<int, gn>{},
+                     std::integral_constant<int, in & 1>{}, tap0 + (in >> 1));
+            else
+                load(std::integral_constant<int, 1 - pb>{}, I0{}, I0{}, tap0 + (NK >> 1));
+            mfmas(std::integral_constant<int, pb>{}, std::integral_constant<int, g>{}, std::integral_constant<int, i>{});
+            if (g == 0) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * (kn < NK * NG ? tiles_of(gn) : tiles_of(0)), 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 3 * tiles_of(g), 0);  // MFMA
+        }, std::make_integer_sequence<int, NK * NG>{});
+    };
+#pragma unroll 1
+    for (int tp = 0; tp < 4; tp++) ksteps(std::integral_constant<int, 4>{}, 4 * tp, 2 * tp);  // taps 2tp, 2tp+1
+    ksteps(std::integral_constant<int, 2>{}, 16, 8);                                          // tap 8
+#pragma unroll
+    for (int m = 0; m < NT; m++) acc[m] = c[m];
+}
+
+template <int NMAX, int R>
+__device__ __forceinline__ void ig_conv3(const _Float16* act, const int (&ctr)[NMAX], int nt_tiles,
+                                         const _Float16* __restrict__ Wf, int nt, int lane, f32x4 (&acc)[NMAX]) {
+    static_assert(NMAX >= 1 && NMAX <= 12, "tile counts");
+    switch (nt_tiles) {
+        case 1: ig_conv3_nt<1, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 2: if constexpr (NMAX >= 2) ig_conv3_nt<2, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 3: if constexpr (NMAX >= 3) ig_conv3_nt<3, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 4: if constexpr (NMAX >= 4) ig_conv3_nt<4, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 5: if constexpr (NMAX >= 5) ig_conv3_nt<5, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 6: if constexpr (NMAX >= 6) ig_conv3_nt<6, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 7: if constexpr (NMAX >= 7) ig_conv3_nt<7, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 8: if constexpr (NMAX >= 8) ig_conv3_nt<8, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 9: if constexpr (NMAX >= 9) ig_conv3_nt<9, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 10: if constexpr (NMAX >= 10) ig_conv3_nt<10, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 11: if constexpr (NMAX >= 11) ig_conv3_nt<11, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        case 12: if constexpr (NMAX >= 12) ig_conv3_nt<12, NMAX, R>(act, ctr, Wf, nt, lane, acc); break;
+        default: break;
+    }
+}
+
+// The wave's rows of a pass over radius-ro squares: its M half of the tiles
+// (the lane's packed row index of tile m is i0 + 16 m; rows >= total are padding)
+struct IgTiles {
+    int i0, total, nt;
+};
+__device__ __forceinline__ IgTiles ig_tiles(const char* lds, int ro, int mh, int lane) {
+    IgTiles t;
+    t.total = ig_total(lds, ro);
+    const int T = (t.total + 15) >> 4, T0 = (T + 1) >> 1, t0 = mh * T0;
+    t.nt = T - t0 < T0 ? (T - t0 > 0 ? T - t0 : 0) : T0;
+    t.i0 = t0 * 16 + (lane & 15);
+    return t;
+}
+
+constexpr int ig_nmax(int ro) { return ((IG * (2 * ro + 1) * (2 * ro + 1) + 15) / 16 + 1) / 2; }
+
+// 3x3 layer (L0, L2, L4, L6: input map MAP window, output square radius MAP + 2) ->
+// relu(acc + bias) as hi / lo into the square rows [plane][cg][IROWS][8] at LDS 0
+template <int MAP, int NMAX>
+__device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, const float* __restrict__ W, int layer,
+                                          int nt, int mh, int lane) {
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 2;
+    static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
+    const IgTiles t = ig_tiles(lds, ro, mh, lane);
+    int ctr[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const int i = t.i0 + 16 * m;
+        const IgRow r = ig_row(lds, ro, i < t.total ? i : 0);
+        const int cell = U[r.g].cell, cr = cell / 15, cc = cell - (cell / 15) * 15;
+        ctr[m] = r.g * 16 * P + (r.pr - cr + R) * Wd + (r.pc - cc + R);
+    }
+    f32x4 acc[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) acc[m] = zero4();
+    const _Float16* wf = (const _Float16*)(W + h_layer_off(layer));
+    if constexpr (NMAX <= 6) {
+        if (t.nt > 0) ig_conv3<NMAX, R>((const _Float16*)lds, ctr, t.nt, wf, nt, lane, acc);
+    } else {
+        // more than 6 tiles: two k-loops over tiles [0, 6) and [6, nt) (the second
+        // streams the weights again), so that one k-loop's registers stay small
+        constexpr int NB = NMAX - 6;
+        int c0[6], c1[NB];
+        f32x4 a0[6], a1[NB];
+#pragma unroll
+        for (int m = 0; m < 6; m++) {
+            c0[m] = ctr[m];
+            a0[m] = zero4();
+        }
+#pragma unroll
+        for (int m = 0; m < NB; m++) {
+            c1[m] = ctr[6 + m];
+            a1[m] = zero4();
+        }
+        if (t.nt > 0) ig_conv3<6, R>((const _Float16*)lds, c0, t.nt < 6 ? t.nt : 6, wf, nt, lane, a0);
+        if (t.nt > 6) ig_conv3<NB, R>((const _Float16*)lds, c1, t.nt - 6, wf, nt, lane, a1);
+#pragma unroll
+        for (int m = 0; m < 6; m++) acc[m] = a0[m];
+#pragma unroll
+        for (int m = 0; m < NB; m++) acc[6 + m] = a1[m];
+    }
+    const int ch0 = nt * 16 + 4 * (lane >> 4);
+    const f32x4 bias = *(const f32x4*)(W + layer_bias(layer) + ch0);
+    __syncthreads();  // every wave is past the k-loop: the windows are dead
+    _Float16* sq = (_Float16*)lds;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const int i = t.i0 + 16 * m;
+        if (m >= t.nt || i >= t.total) continue;
+        h4 hi, lo;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float y = acc[m][r] + bias[r];
+            y = y > 0.f ? y : 0.f;
+            const _Float16 h = (_Float16)y;
+            hi[r] = h;
+            lo[r] = (_Float16)(y - (float)h);
+        }
+        const int o = ((ch0 >> 3) * IROWS + i) * 8 + (ch0 & 7);
+        *(h4*)(sq + o) = hi;
+        *(h4*)(sq + 8 * IROWS * 8 + o) = lo;
+    }
+    __syncthreads();
+}
+
+// 1x1 layer (L1, L3, L5, L7) over the square rows at LDS 0 (radius ro): acc only
+template <int NMAX>
+__device__ __forceinline__ void ig_conv1(const char* lds, const IgTiles& t, const float* __restrict__ W,
+                                         int layer, int nt, int lane, f32x4 (&acc)[NMAX]) {
+    const _Float16* sq = (const _Float16*)lds;
+    const _Float16* wf = (const _Float16*)(W + h_layer_off(layer)) + ((size_t)nt * 64 + lane) * 8;
+    const h8 w0h = *(const h8*)wf, w1h = *(const h8*)(wf + 4 * 64 * 8);
+    const h8 w0l = *(const h8*)(wf + 2 * 4 * 64 * 8), w1l = *(const h8*)(wf + 3 * 4 * 64 * 8);
+    const int q = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) acc[m] = zero4();
+    // groups of 3 tiles; per element gn_kernel's order: k-step 0 (hi*hi, w_lo*hi, hi*a_lo), k-step 1
+#pragma unroll
+    for (int g0 = 0; g0 < NMAX; g0 += 3) {
+        if (g0 >= t.nt) break;
+        h8 a[3][4];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int o = (q * IROWS + t.i0 + 16 * (g0 + j < NMAX ? g0 + j : g0)) * 8;
+            a[j][0] = *(const h8*)(sq + o);
+            a[j][1] = *(const h8*)(sq + 8 * IROWS * 8 + o);
+            a[j][2] = *(const h8*)(sq + 4 * IROWS * 8 + o);
+            a[j][3] = *(const h8*)(sq + 8 * IROWS * 8 + 4 * IROWS * 8 + o);
+        }
+#define IG_P(W_, A_)                                                                                \
+    _Pragma("unroll") for (int j = 0; j < 3; j++) if (g0 + j < NMAX)                                \
+        acc[g0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(W_, a[j][A_], acc[g0 + j], 0, 0, 0);
+        IG_P(w0h, 0)
+        IG_P(w0l, 0)
+        IG_P(w0h, 1)
+        IG_P(w1h, 2)
+        IG_P(w1l, 2)
+        IG_P(w1h, 3)
+#undef IG_P
+    }
+}
+
+// relu(acc + bias) split hi / lo
+__device__ __forceinline__ void ig_split(const f32x4& acc, const f32x4& bias, h4& hi, h4& lo) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        float y = acc[r] + bias[r];
+        y = y > 0.f ? y : 0.f;
+        const _Float16 h = (_Float16)y;
+        hi[r] = h;
+        lo[r] = (_Float16)(y - (float)h);
+    }
+}
+
+// 1x1 layer producing stored map MAP (L1 -> 1, L3 -> 2, L5 -> 3; square radius
+// MAP + 1): k-loop over the square rows, barrier, the next window's fill, then the
+// outputs into that window's new square and the row's map slot
+template <int MAP, int NMAX>
+__device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng, const float* __restrict__ W,
+                                              int layer, int nt, int mh, int lane, int tid) {
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 1;
+    static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
+    const IgTiles t = ig_tiles(lds, ro, mh, lane);
+    f32x4 acc[NMAX];
+    ig_conv1<NMAX>(lds, t, W, layer, nt, lane, acc);
+    const int ch0 = nt * 16 + 4 * (lane >> 4);
+    const f32x4 bias = *(const f32x4*)(W + layer_bias(layer) + ch0);
+    __syncthreads();  // the square rows are dead
+    ig_fill<MAP>(lds, U, ng, tid);
+    _Float16* win = (_Float16*)lds;
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const int i = t.i0 + 16 * m;
+        if (m >= t.nt || i >= t.total) continue;
+        h4 hi, lo;
+        ig_split(acc[m], bias, hi, lo);
+        const IgRow r = ig_row(lds, ro, i);
+        const int cell = U[r.g].cell, cr = cell / 15, cc = cell - (cell / 15) * 15;
+        const int w = (r.pr - cr + R) * Wd + (r.pc - cc + R);
+        const int o = r.g * 16 * P * 8 + ((ch0 >> 3) * P + w) * 8 + (ch0 & 7);
+        *(h4*)(win + o) = hi;
+        *(h4*)(win + 8 * P * 8 + o) = lo;
+        _Float16* g = U[r.g].job + MAP * SLOT_MAP_HALVES + ((ch0 >> 3) * POS + r.pr * 15 + r.pc) * 8 + (ch0 & 7);
+        *(h4*)g = hi;
+        *(h4*)(g + 8 * POS * 8) = lo;
+    }
+    __syncthreads();  // the window is complete (the barrier drains the fill)
+}
+
+__global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards,
+                                                        const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ list_count,
+                                                        const GnTag* __restrict__ tags, char* __restrict__ slots,
+                                                        float* __restrict__ rec) {
+    __shared__ __attribute__((aligned(16))) char lds[ILDS];
+    GnUnit* U = (GnUnit*)(lds + IU);
+    _Float16* col = (_Float16*)(lds + ICOL);
+    float* pcv = (float*)(lds + IPC);
+    const int count = *list_count;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nt = wave & 3, mh = wave >> 2;
+    for (int pos0 = blockIdx.x * IG; pos0 < count; pos0 += gridDim.x * IG) {
+        __syncthreads();  // the previous chunk is done with U
+        const int ng = count - pos0 < IG ? count - pos0 : IG;
+        if (tid < ng) {
+            const int b = list[pos0 + tid];
+            const GnTag tg = tags[b];
+            GnUnit u;
+            char* bs = slots + (size_t)tg.base * SLOT_BYTES;
+            char* js = slots + (size_t)tg.job * SLOT_BYTES;
+            u.base = (const _Float16*)bs;
+            u.job = (_Float16*)js;
+            u.pol_src = (const float*)(tg.nst > 0 || tg.base == tg.job ? js : bs) + SLOT_POL;
+            u.pol_job = (float*)js + SLOT_POL;
+            u.rec = rec + (size_t)b * REC;
+            u.cell = tg.cell;
+            u.nst = tg.nst;
+#pragma unroll
+            for (int s = 0; s < 8; s++) u.st[s] = s < TAG_STONES ? tg.st[s] : 0;
+#pragma unroll
+            for (int w = 0; w < 16; w++) u.board[w] = boards[(size_t)b * 16 + w];
+            u.pad[0] = u.pad[1] = 0;
+            U[tid] = u;
+        }
+        __syncthreads();
+        ig_build_rows(lds, U, ng, tid);  // (read after the embed's barriers)
+        // (the asm barriers keep the compiler from hoisting every section's per-lane
+        // addresses out of the chunk loop, where they would all stay live, and spill)
+        auto fresh = [&](const float*& Wp, int& t) {
+            Wp = W;
+            t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+        };
+        const float* Wp;
+        int t_;
+        fresh(Wp, t_);
+        // ---- embed: window of map 0 (fill) + im2col of the radius-1 squares
+        ig_fill<0>(lds, U, ng, t_);
+        for (int e = tid; e < IG * 512; e += NTI) {
+            const int g = e >> 9, row = (e >> 5) & 15, k = e & 31;
+            _Float16 v = (_Float16)0.f;
+            if (g < ng) {
+                const Sq q = square(U[g].cell, 1);
+                if (row < q.h * q.w && k < 27) {
+                    const int pr = q.r0 + row / q.w, pc = q.c0 + row % q.w;
+                    const int tap = k / 3, cin = k % 3;
+                    const int rr = pr + tap / 3 - 1, cc = pc + tap % 3 - 1;
+                    if (rr >= 0 && rr < 15 && cc >= 0 && cc < 15) {
+                        const int bit = rr * 16 + cc;
+                        const uint32_t bl = (U[g].board[bit >> 5] >> (bit & 31)) & 1u;
+                        const uint32_t wh = (U[g].board[8 + (bit >> 5)] >> (bit & 31)) & 1u;
+                        v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
+                    }
+                }
+            }
+            col[((g * 4 + (k >> 3)) * 16 + row) * 8 + (k & 7)] = v;
+        }
+        __syncthreads();  // the fill has landed; the im2col is complete
+        fresh(Wp, t_);
+        {
+            const int ln = t_ & 63, li = ln & 15, q = ln >> 4, ch0 = nt * 16 + 4 * q;
+            const _Float16* wf = (const _Float16*)(Wp + GH_E) + ((size_t)nt * 64 + ln) * 8;
+            const h8 wh = *(const h8*)wf, wl = *(const h8*)(wf + 4 * 64 * 8);
+            const f32x4 bias = *(const f32x4*)(Wp + GE_B + ch0);
+            constexpr int P0 = 49;
+            for (int g = mh; g < ng; g += 2) {
+                const h8 a = *(const h8*)(col + ((g * 4 + q) * 16 + li) * 8);
+                f32x4 acc = zero4();
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, a, acc, 0, 0, 0);
+                const Sq sq = square(U[g].cell, 1);
+                if (li < sq.h * sq.w) {
+                    h4 hi, lo;
+                    ig_split(acc, bias, hi, lo);
+                    const int pr = sq.r0 + li / sq.w, pc = sq.c0 + li % sq.w;
+                    const int cell = U[g].cell, cr = cell / 15, cc = cell - cr * 15;
+                    const int w = (pr - cr + 3) * 7 + (pc - cc + 3);
+                    _Float16* win = (_Float16*)lds + g * 16 * P0 * 8 + ((ch0 >> 3) * P0 + w) * 8 + (ch0 & 7);
+                    *(h4*)win = hi;
+                    *(h4*)(win + 8 * P0 * 8) = lo;
+                    _Float16* gp = U[g].job + ((ch0 >> 3) * POS + pr * 15 + pc) * 8 + (ch0 & 7);
+                    *(h4*)gp = hi;
+                    *(h4*)(gp + 8 * POS * 8) = lo;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- the tower: 3x3 over a window -> square rows; 1x1 -> the next map
+        fresh(Wp, t_);
+        // NMAX = the tiles of a wave's M half: ceil(ceil(IG (2 ro + 1)^2 / 16) / 2)
+        ig_layer3<0, 3>(lds, U, ng, Wp, 0, nt, mh, t_ & 63);        // L0: <= 75 rows
+        fresh(Wp, t_);
+        ig_layer1_map<1, 3>(lds, U, ng, Wp, 1, nt, mh, t_ & 63, t_);
+        fresh(Wp, t_);
+        ig_layer3<1, 5>(lds, U, ng, Wp, 2, nt, mh, t_ & 63);        // L2: <= 147 rows
+        fresh(Wp, t_);
+        ig_layer1_map<2, 5>(lds, U, ng, Wp, 3, nt, mh, t_ & 63, t_);
+        fresh(Wp, t_);
+        ig_layer3<2, 8>(lds, U, ng, Wp, 4, nt, mh, t_ & 63);        // L4: <= 243 rows
+        fresh(Wp, t_);
+        ig_layer1_map<3, 8>(lds, U, ng, Wp, 5, nt, mh, t_ & 63, t_);
+        fresh(Wp, t_);
+        ig_layer3<3, 12>(lds, U, ng, Wp, 6, nt, mh, t_ & 63);       // L6: <= 363 rows
+        fresh(Wp, t_);
+        {   // L7 (1x1) in place over the square rows, then the policy conv per row
+            const int ln = t_ & 63;
+            static_assert(ig_nmax(5) <= 12, "tiles per M half");
+            const IgTiles t = ig_tiles(lds, 5, mh, ln);
+            f32x4 acc[12];
+            ig_conv1<12>(lds, t, Wp, 7, nt, ln, acc);
+            const int ch0 = nt * 16 + 4 * (ln >> 4);
+            const f32x4 bias = *(const f32x4*)(Wp + layer_bias(7) + ch0);
+            __syncthreads();
+            _Float16* sq = (_Float16*)lds;
+#pragma unroll
+            for (int m = 0; m < 12; m++) {
+                const int i = t.i0 + 16 * m;
+                if (m >= t.nt || i >= t.total) continue;
+                h4 hi, lo;
+                ig_split(acc[m], bias, hi, lo);
+                const int o = ((ch0 >> 3) * IROWS + i) * 8 + (ch0 & 7);
+                *(h4*)(sq + o) = hi;
+                *(h4*)(sq + 8 * IROWS * 8 + o) = lo;
+            }
+            __syncthreads();
+            fresh(Wp, t_);
+            const int total = ig_total(lds, 5);
+            if (t_ < total) {
+                const IgRow r = ig_row(lds, 5, t_);
+                float p0, p1;
+                gn_pconv(Wp, sq + t_ * 8, sq + 8 * IROWS * 8 + t_ * 8, IROWS * 8, p0, p1);
+                pcv[(r.g * 2 + 0) * 128 + r.j] = p0;
+                pcv[(r.g * 2 + 1) * 128 + r.j] = p1;
+            }
+            __syncthreads();
+        }
+        // ---- records: policy-conv outputs (new square, else the predecessor's), stones
+        for (int e = tid; e < ng * REC; e += NTI) {
+            const int g = e / REC, i = e - g * REC;
+            const GnUnit& u = U[g];
+            float v = 0.f;
+            if (i < 2 * POS) {
+                const int ch = i >= POS ? 1 : 0, p = i - ch * POS, pr = p / 15, pc = p - (p / 15) * 15;
+                const Sq q = square(u.cell, 5);
+                if (pr >= q.r0 && pr < q.r0 + q.h && pc >= q.c0 && pc < q.c0 + q.w)
+                    v = pcv[(g * 2 + ch) * 128 + (pr - q.r0) * q.w + (pc - q.c0)];
+                else
+                    v = u.pol_src[i];
+                u.pol_job[i] = v;
+            } else if (i >= REC_X && i < REC_X + 2 * POS) {
+                const int ch = i >= REC_X + POS ? 1 : 0, p = i - REC_X - ch * POS;
+                const int bit = (p / 15) * 16 + (p % 15);
+                v = (float)((u.board[ch * 8 + (bit >> 5)] >> (bit & 31)) & 1u);
+            }
+            u.rec[i] = v;
+        }
+    }
+}
 }  // namespace
 
 #ifdef GZ_GN_STAMPS
@@ -391,6 +1030,91 @@ extern "C" size_t gz_gn_weight_floats(void) { return (size_t)TOTAL; }
 
 extern "C" size_t gz_gn_workspace_bytes(int32_t n) { return (size_t)(n < 1 ? 1 : n) * REC * sizeof(float); }
 
+static int gn_cus() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return cus;
+}
+
+static int gn_launch_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string(what) + ": " + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}
+
+// the search roots' full forward: maps and policy-conv outputs into slots 0..n-1
+// (gz_plan.hip; d_rec: n record rows of scratch)
+extern "C" int gz_internal_gn_roots(const float* d_weights, const uint32_t* d_rows, int32_t n, void* d_slots,
+                                    float* d_rec, void* stream) {
+    if (n <= 0) return GZ_OK;
+    const int cus = gn_cus();
+    gn_kernel<<<n < 2 * cus ? n : 2 * cus, NT, 0, (hipStream_t)stream>>>(d_weights, d_rows, n, nullptr, d_rec, nullptr,
+                                                                       (char*)d_slots, nullptr);
+    return gn_launch_check("gn_kernel (roots)");
+}
+
+// the planner nets over tagged rows (gz_plan.hip's collect kernel): full-forward
+// rows (keeping their maps in their slots) and incremental rows, then the batched
+// heads over all rows
+extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint32_t* d_rows, int32_t max_rows,
+                                             const int32_t* d_count, const int32_t* d_full_list,
+                                             const int32_t* d_full_count, const int32_t* d_inc_list,
+                                             const int32_t* d_inc_count, const void* d_tags, void* d_slots,
+                                             float* d_p, float* d_q, float* d_rec, void* stream) {
+    if (max_rows <= 0) return GZ_OK;
+    const int cus = gn_cus();
+    hipStream_t s = (hipStream_t)stream;
+    gn_kernel<<<max_rows < 2 * cus ? max_rows : 2 * cus, NT, 0, s>>>(d_weights, d_rows, max_rows, d_full_count, d_rec,
+                                                                     d_full_list, (char*)d_slots, (const GnTag*)d_tags);
+    const int chunks = (max_rows + IG - 1) / IG;
+    gn_inc_kernel<<<chunks < cus ? chunks : cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
+                                                              (const GnTag*)d_tags, (char*)d_slots, d_rec);
+    gn_heads_kernel<<<(max_rows + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr);
+    return gn_launch_check("gn_inc_kernel");
+}
+
+// rows by kind for gz_gn_forward_chain
+__global__ void gn_split_kernel(const GnTag* __restrict__ tags, int n, int32_t* __restrict__ lists,
+                                int32_t* __restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int k = tags[i].mode == 1 ? 1 : 0;
+    lists[(size_t)k * n + atomicAdd(&counts[k], 1)] = i;
+}
+
+extern "C" size_t gz_gn_slot_bytes(void) { return SLOT_BYTES; }
+
+extern "C" size_t gz_gn_chain_workspace_bytes(int32_t n) {
+    const size_t m = (size_t)(n < 1 ? 1 : n);
+    return m * REC * 4 + 2 * m * 4 + 256;
+}
+
+extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boards, int32_t n, const void* d_tags,
+                                   void* d_slots, float* d_p, float* d_q, void* d_workspace, void* stream) {
+    if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_tags || !d_slots || !d_p || !d_q || !d_workspace))) {
+        gz_internal_set_error("gz_gn_forward_chain: bad arguments");
+        return GZ_ERR_ARG;
+    }
+    if (n == 0) return GZ_OK;
+    hipStream_t s = (hipStream_t)stream;
+    float* rec = (float*)d_workspace;
+    int32_t* lists = (int32_t*)(rec + (size_t)n * REC);
+    int32_t* counts = lists + 2 * (size_t)n;
+    if (hipMemsetAsync(counts, 0, 8, s) != hipSuccess) {
+        gz_internal_set_error("gz_gn_forward_chain: memset");
+        return GZ_ERR_HIP;
+    }
+    gn_split_kernel<<<(n + 255) / 256, 256, 0, s>>>((const GnTag*)d_tags, n, lists, counts);
+    int rc = gn_launch_check("gn_split_kernel");
+    if (rc) return rc;
+    return gz_internal_gn_forward_tagged(d_weights, d_boards, n, nullptr, lists, counts, lists + n, counts + 1,
+                                         d_tags, d_slots, d_p, d_q, rec, stream);
+}
+
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
                              float* d_p, float* d_q, float* d_logits, void* d_workspace, void* stream) {
     if (n < 0 || (n > 0 && (!d_weights || !d_boards || !d_p || !d_q || !d_workspace))) {
@@ -403,7 +1127,7 @@ extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, i
         cus = 256;
     int grid = n < 2 * cus ? n : 2 * cus;
     hipStream_t s = (hipStream_t)stream;
-    gn_kernel<<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace);
+    gn_kernel<<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace, nullptr, nullptr, nullptr);
     gn_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count, d_p, d_q,
                                                         d_logits);
     hipError_t e = hipGetLastError();

@@ -23,12 +23,15 @@
 // and trees are identical to the C oracle's (tests/test_gpu_plan.py).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
+#include "gz_gnet.h"
 #include "gz_search.h"
 
 using namespace gz;
+using gzgn::GnTag;
 
 namespace {
 
@@ -61,14 +64,26 @@ struct PlanJob {  // 128 bytes
     int8_t state;     // 0 none, 1 planner plies, 2 rollout, 3 done
     int8_t steps;
     int8_t pad[2];
-    int32_t pad2[6];
+    // incremental GraphNet chain (gn_inc_kernel): the stones added since the base
+    // maps whose squares are in the job's map slot, whether the base is that slot
+    // (after a full forward) rather than the search root's, and the planner move
+    // the next planner ply's board adds
+    uint8_t st[gzgn::TAG_STONES];
+    uint8_t nst, bj, pend, pad3;
+    int32_t pad2[3];
 };
 static_assert(sizeof(PlanJob) == 128, "job");
 
 struct Counters {
     int32_t rows;     // GN rows collected this round
     int32_t pending;  // games with a job after resume
-    int32_t pad[62];
+    int32_t nfull, ninc;  // this planner step's full-forward / incremental rows
+    int32_t pad[60];
+};
+// never cleared by a search: gz_plan_gn_stats reads (and resets) them
+struct GnStats {
+    int64_t full, inc, mismatch, checked;
+    int64_t pad[4];
 };
 
 __host__ __device__ inline size_t ctx_stride(int S) { return sizeof(PlanCtx) + tree_bytes_for(S); }
@@ -78,44 +93,73 @@ constexpr size_t GN_REC_BYTES = 928 * 4;  // = gz_gn_workspace_bytes(1) (gz_gnet
 struct Workspace {
     char* ctx;
     PlanJob* jobs;
-    uint32_t* gn_in;   // [n*S][16]
-    float* gn_p;       // [n*S][225]
+    uint32_t* gn_in;   // [C][16] (C = chunk_rows: the GN rows of one planner step)
+    float* gn_p;       // [C][225]
     float* gn_q;
-    float* gn_rec;     // gz_gn_forward's workspace for n*S rows
+    float* gn_rec;     // gz_gn_forward's workspace for C rows
     int32_t* rows;     // row -> job
     Counters* ctr;
+    GnStats* stats;
+    GnTag* tags;       // [C] incremental tags of the rows
+    int32_t* full_list, *inc_list;  // [C] rows by kind
+    float *chk_p, *chk_q, *chk_rec;  // GZ_FLAG_GN_CHECK: the full forward of the same rows
+    char* slots;       // map slots: [n] search roots, then [C] jobs (gzgn::SLOT_BYTES each)
+    size_t end;
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Round 0 (the parallel phase: up to n * S rollouts at once) runs its jobs in chunks
+// of C: a chunk's planner plies, then the next chunk's; jobs are independent, so
+// this only bounds the row buffers and the map slots (one per job of a chunk)
+constexpr size_t PLAN_CHUNK = 65536;
+__host__ __device__ inline size_t chunk_rows(int n, int S) {
+    const size_t nj = (size_t)n * (S > 0 ? S : 1);
+    const size_t c = (size_t)n > PLAN_CHUNK ? (size_t)n : PLAN_CHUNK;
+    return nj < c ? nj : c;
+}
+
 __host__ __device__ inline Workspace carve(void* base, int n, int S) {
     char* p = (char*)base;
-    const size_t nj = (size_t)n * (S > 0 ? S : 1);
+    const size_t nj = (size_t)n * (S > 0 ? S : 1), C = chunk_rows(n, S);
     Workspace w;
     w.ctr = (Counters*)p;
     p += align256(sizeof(Counters));
+    w.stats = (GnStats*)p;
+    p += align256(sizeof(GnStats));
     w.ctx = p;
     p += align256(ctx_stride(S) * (size_t)n);
     w.jobs = (PlanJob*)p;
     p += align256(sizeof(PlanJob) * nj);
     w.gn_in = (uint32_t*)p;
-    p += align256(nj * 16 * 4);
+    p += align256(C * 16 * 4);
     w.gn_p = (float*)p;
-    p += align256(nj * 225 * 4);
+    p += align256(C * 225 * 4);
     w.gn_q = (float*)p;
-    p += align256(nj * 225 * 4);
+    p += align256(C * 225 * 4);
     w.gn_rec = (float*)p;
-    p += align256(nj * GN_REC_BYTES);
+    p += align256(C * GN_REC_BYTES);
     w.rows = (int32_t*)p;
-    p += align256(nj * 4);
+    p += align256(C * 4);
+    w.tags = (GnTag*)p;
+    p += align256(C * sizeof(GnTag));
+    w.full_list = (int32_t*)p;
+    p += align256(C * 4);
+    w.inc_list = (int32_t*)p;
+    p += align256(C * 4);
+    w.chk_p = (float*)p;
+    p += align256(C * 225 * 4);
+    w.chk_q = (float*)p;
+    p += align256(C * 225 * 4);
+    w.chk_rec = (float*)p;
+    p += align256(C * GN_REC_BYTES);
+    w.slots = p;
+    p += align256(((size_t)n + C) * gzgn::SLOT_BYTES);
+    w.end = (size_t)(p - (char*)base);
     return w;
 }
 
-__host__ inline size_t workspace_bytes(int n, int S) {
-    Workspace w = carve(nullptr, n, S);
-    const size_t nj = (size_t)n * (S > 0 ? S : 1);
-    return (size_t)((char*)w.rows - (char*)nullptr) + align256(nj * 4);
-}
+__host__ inline size_t workspace_bytes(int n, int S) { return carve(nullptr, n, S).end; }
 
 __device__ inline PlanCtx* ctx_at(const Workspace& w, int g, int S) {
     return (PlanCtx*)(w.ctx + (size_t)g * ctx_stride(S));
@@ -481,10 +525,17 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
     }
 }
 
-// jobs in their planner plies -> GN rows; jobs past them -> rollout
-__global__ void plan_collect_kernel(Workspace w, int n_jobs, int planner_steps, int final_round) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_jobs) return;
+// jobs [j0, j1) in their planner plies -> GN rows; jobs past them -> rollout.
+// inc: also tag each row for the incremental GraphNet (gn_inc_kernel): a rollout's
+// first board that is the search root plus one stone, and every later planner ply's
+// board (its predecessor plus the planner's move), add one stone to maps that are
+// kept; any other board runs the full forward and keeps its maps in the job's slot.
+// Job slot: n + (job - j0) in round 0's chunks (slot_game 0), n + game afterwards
+// (one job per game).
+__global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int j1, int planner_steps, int final_round,
+                                    int inc, int slot_game) {
+    const int i = j0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= j1) return;
     PlanJob& j = w.jobs[i];
     if (j.state != 1) return;
     BB black, white;
@@ -500,9 +551,83 @@ __global__ void plan_collect_kernel(Workspace w, int n_jobs, int planner_steps, 
         dst[1] = make_uint4(black.w[4], black.w[5], black.w[6], black.w[7]);
         dst[2] = make_uint4(white.w[0], white.w[1], white.w[2], white.w[3]);
         dst[3] = make_uint4(white.w[4], white.w[5], white.w[6], white.w[7]);
+        if (inc) {
+            GnTag t;
+            t.job = n + (slot_game ? j.game : i - j0);
+            t.mode = 1;
+            t.nst = 0;
+            t.cell = -1;
+            if (j.steps == 0) {  // one stone from the root?
+                const PlanCtx* cx = ctx_at(w, j.game, S);
+                BB rb, rw;
+                load_bb(rb, cx->black);
+                load_bb(rw, cx->white);
+                int nd = 0, bit = -1;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t db = black.w[k] ^ rb.w[k], dw = white.w[k] ^ rw.w[k];
+                    nd += __popc(db) + __popc(dw);
+                    const uint32_t add = (db & black.w[k]) | (dw & white.w[k]);
+                    if (add) bit = k * 32 + __ffs(add) - 1;
+                }
+                if (nd == 1 && bit >= 0) {
+                    t.cell = bit_to_cell(bit);
+                    t.base = j.game;
+                    j.bj = 0;
+                    j.nst = 0;
+                } else {
+                    t.mode = 0;
+                }
+            } else if (j.bj) {  // the job's own full maps
+                t.cell = j.pend;
+                t.base = t.job;
+            } else if (j.nst < gzgn::TAG_STONES) {  // the root's maps + the job's squares
+                t.cell = j.pend;
+                t.base = j.game;
+                t.nst = j.nst;
+#pragma unroll
+                for (int k = 0; k < gzgn::TAG_STONES; k++) t.st[k] = j.st[k];
+            } else {
+                t.mode = 0;
+            }
+            if (t.mode == 0) {
+                t.base = t.job;
+                j.bj = 1;
+                j.nst = 0;
+                w.full_list[atomicAdd(&w.ctr->nfull, 1)] = row;
+            } else {
+                if (!j.bj) j.st[j.nst++] = (uint8_t)t.cell;
+                w.inc_list[atomicAdd(&w.ctr->ninc, 1)] = row;
+            }
+            w.tags[row] = t;
+        }
     } else {
         j.state = 2;
     }
+}
+
+// GZ_FLAG_GN_CHECK: rows whose incremental record (policy-conv outputs), p or q
+// differ in any bit from the full forward's
+__global__ void plan_gn_check_kernel(Workspace w) {
+    const int row = blockIdx.x;
+    if (row >= w.ctr->rows) return;
+    bool bad = false;
+    for (int e = threadIdx.x; e < 450; e += blockDim.x)
+        bad |= __float_as_uint(w.gn_rec[(size_t)row * 928 + e]) != __float_as_uint(w.chk_rec[(size_t)row * 928 + e]);
+    for (int e = threadIdx.x; e < 225; e += blockDim.x) {
+        bad |= __float_as_uint(w.gn_p[(size_t)row * 225 + e]) != __float_as_uint(w.chk_p[(size_t)row * 225 + e]);
+        bad |= __float_as_uint(w.gn_q[(size_t)row * 225 + e]) != __float_as_uint(w.chk_q[(size_t)row * 225 + e]);
+    }
+    bad = __syncthreads_or(bad);
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&w.stats->checked, 1ull);
+        if (bad) atomicAdd((unsigned long long*)&w.stats->mismatch, 1ull);
+    }
+}
+
+__global__ void plan_gn_count_kernel(Workspace w) {
+    atomicAdd((unsigned long long*)&w.stats->full, (unsigned long long)w.ctr->nfull);
+    atomicAdd((unsigned long long*)&w.stats->inc, (unsigned long long)w.ctr->ninc);
 }
 
 // one planner ply (BGPlannerAI.get_move + make_move) per collected row
@@ -532,6 +657,7 @@ __global__ __launch_bounds__(WAVE) void plan_step_kernel(Workspace w, gz_planner
         j.mover = (int8_t)(3 - mover);
         j.cnt = cnt;
         j.steps = (int8_t)(j.steps + 1);
+        j.pend = (uint8_t)mv;
         if (win || ne == 1 || n_moves + 1 >= 200) {  // game over: straight to the value
             j.state = 3;
             j.value = win ? (mover == P ? 1.0 : -1.0) : 0.1;
@@ -831,6 +957,13 @@ extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
                              float* d_p, float* d_q, float* d_logits, void* d_workspace, void* stream);
 extern "C" size_t gz_gn_workspace_bytes(int32_t n);
+extern "C" int gz_internal_gn_roots(const float* d_weights, const uint32_t* d_rows, int32_t n, void* d_slots,
+                                    float* d_rec, void* stream);
+extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint32_t* d_rows, int32_t max_rows,
+                                             const int32_t* d_count, const int32_t* d_full_list,
+                                             const int32_t* d_full_count, const int32_t* d_inc_list,
+                                             const int32_t* d_inc_count, const void* d_tags, void* d_slots,
+                                             float* d_p, float* d_q, float* d_rec, void* stream);
 
 static int plan_fail(int code, const char* msg) {
     gz_internal_set_error(msg);
@@ -871,7 +1004,13 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
     Workspace w = carve(d_workspace, n, S);
     LeafSink sink{d_leaves, leaf_cap, d_leaf_count, gather ? d_leaf_meta : nullptr};
     const int n_jobs = n * S;
+    const int C = (int)chunk_rows(n, S);
     const int jb = (n_jobs + 255) / 256;
+    // incremental GraphNet (gn_inc_kernel) unless GZ_GN_INC=0; GZ_FLAG_GN_CHECK also
+    // runs the full forward on every row and counts the rows that differ
+    const char* env = getenv("GZ_GN_INC");
+    const bool inc = p->planner_steps > 0 && !(env && env[0] == '0');
+    const bool check = inc && (p->flags & GZ_FLAG_GN_CHECK) != 0;
     int rc;
     if (hipMemsetAsync(w.ctr, 0, sizeof(Counters), s) != hipSuccess)
         return plan_fail(GZ_ERR_HIP, "gz_plan_search: memset");
@@ -879,6 +1018,41 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         return plan_fail(GZ_ERR_HIP, "gz_plan_search: memset");
     plan_begin_kernel<<<n, WAVE, 0, s>>>(d_boards, d_game_ids, n, *p, w, sink, gather ? 1 : 0);
     if ((rc = plan_check("plan_begin_kernel"))) return rc;
+    if (inc) {  // the roots' maps and policy-conv outputs -> root slots 0..n-1
+        boards_to_rows_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_boards, n, w.gn_in);
+        if ((rc = plan_check("boards_to_rows_kernel"))) return rc;
+        if ((rc = gz_internal_gn_roots(d_gn_weights, w.gn_in, n, w.slots, w.gn_rec, stream))) return rc;
+    }
+    // one planner step over jobs [j0, j1): collect -> GraphNet + DQN -> planner move
+    auto planner_step = [&](int j0, int j1, int max_rows, int slot_game) -> int {
+        int r;
+        // rows, pending (recomputed by the next resume), nfull, ninc
+        if (hipMemsetAsync(&w.ctr->rows, 0, 16, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
+        plan_collect_kernel<<<(j1 - j0 + 255) / 256, 256, 0, s>>>(w, S, n, j0, j1, p->planner_steps, 0, inc ? 1 : 0,
+                                                                   slot_game);
+        if ((r = plan_check("plan_collect_kernel"))) return r;
+        if (!inc) {
+            if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
+                                   stream)))
+                return r;
+        } else {
+            if ((r = gz_internal_gn_forward_tagged(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.full_list,
+                                                   &w.ctr->nfull, w.inc_list, &w.ctr->ninc, w.tags, w.slots, w.gn_p,
+                                                   w.gn_q, w.gn_rec, stream)))
+                return r;
+            plan_gn_count_kernel<<<1, 1, 0, s>>>(w);
+            if ((r = plan_check("plan_gn_count_kernel"))) return r;
+            if (check) {
+                if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.chk_p, w.chk_q, nullptr,
+                                       w.chk_rec, stream)))
+                    return r;
+                plan_gn_check_kernel<<<max_rows, 256, 0, s>>>(w);
+                if ((r = plan_check("plan_gn_check_kernel"))) return r;
+            }
+        }
+        plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp);
+        return plan_check("plan_step_kernel");
+    };
     for (int round = 0;; round++) {
         int32_t pending = 0;
         if (hipMemcpyAsync(&pending, &w.ctr->pending, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -886,19 +1060,17 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
             return plan_fail(GZ_ERR_HIP, "gz_plan_search: reading the pending count");
         if (pending == 0) break;
         if (round > S + 1) return plan_fail(GZ_ERR_INTERNAL, "gz_plan_search: search did not terminate");
-        // rows of the biggest round: every job of the parallel phase, else one per game
-        const int max_rows = round == 0 ? n_jobs : n;
-        for (int st = 0; st < p->planner_steps; st++) {
-            if (hipMemsetAsync(&w.ctr->rows, 0, 4, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
-            plan_collect_kernel<<<jb, 256, 0, s>>>(w, n_jobs, p->planner_steps, 0);
-            if ((rc = plan_check("plan_collect_kernel"))) return rc;
-            if ((rc = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
-                                    stream)))
-                return rc;
-            plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp);
-            if ((rc = plan_check("plan_step_kernel"))) return rc;
+        if (round == 0) {  // every job of the parallel phase, C at a time
+            for (int j0 = 0; j0 < n_jobs; j0 += C) {
+                const int j1 = j0 + C < n_jobs ? j0 + C : n_jobs;
+                for (int st = 0; st < p->planner_steps; st++)
+                    if ((rc = planner_step(j0, j1, j1 - j0, 0))) return rc;
+            }
+        } else {  // one job per game
+            for (int st = 0; st < p->planner_steps; st++)
+                if ((rc = planner_step(0, n_jobs, n, 1))) return rc;
         }
-        plan_collect_kernel<<<jb, 256, 0, s>>>(w, n_jobs, p->planner_steps, 1);
+        plan_collect_kernel<<<jb, 256, 0, s>>>(w, S, n, 0, n_jobs, p->planner_steps, 1, 0, 0);
         if ((rc = plan_check("plan_collect_kernel"))) return rc;
         plan_rollout_kernel<<<jb, 256, 0, s>>>(w, n_jobs, p->max_depth);
         if ((rc = plan_check("plan_rollout_kernel"))) return rc;
@@ -908,6 +1080,29 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
     }
     plan_finish_kernel<<<n, WAVE, 0, s>>>(n, S, w, d_moves, d_stats, (char*)d_trees);
     return plan_check("plan_finish_kernel");
+}
+
+// out[4] (host int64) = rows that ran the full forward / the incremental forward /
+// were checked / differed from the full forward (GZ_FLAG_GN_CHECK), summed over the
+// searches since the last reset
+extern "C" int gz_plan_gn_stats(void* d_workspace, int32_t n, int32_t num_simulations, int64_t* out, int32_t reset,
+                                void* stream) {
+    if (!d_workspace || n < 1 || num_simulations < 1) return plan_fail(GZ_ERR_ARG, "gz_plan_gn_stats: bad arguments");
+    Workspace w = carve(d_workspace, n, num_simulations);
+    hipStream_t s = (hipStream_t)stream;
+    GnStats h;
+    if (out) {
+        if (hipMemcpyAsync(&h, w.stats, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return plan_fail(GZ_ERR_HIP, "gz_plan_gn_stats: copy");
+        out[0] = h.full;
+        out[1] = h.inc;
+        out[2] = h.checked;
+        out[3] = h.mismatch;
+    }
+    if (reset && hipMemsetAsync(w.stats, 0, sizeof(GnStats), s) != hipSuccess)
+        return plan_fail(GZ_ERR_HIP, "gz_plan_gn_stats: reset");
+    return GZ_OK;
 }
 
 extern "C" int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,

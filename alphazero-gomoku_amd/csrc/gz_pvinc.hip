@@ -1022,7 +1022,11 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
     const int wo = (nt0 * 64 + lane) * 16;
     // SIB_PROBE (timing probes, wrong results): 1 = every activation read is the
     // conflict-free pattern of consecutive rows, 2 = every weight load reads k-step 0
-    // (L1-resident: no weight stream)
+    // (L1-resident: no weight stream), 3 = only the first SIB_PROBE_TAPS of the 9 taps
+    // (the MFMA work a delta convolution would leave)
+#ifndef SIB_PROBE_TAPS
+#define SIB_PROBE_TAPS 5
+#endif
 #ifndef SIB_PROBE
 #define SIB_PROBE 0
 #endif
@@ -1059,7 +1063,7 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
         al[m] = *(const h8*)(act + PLANE + nb[m]);
     }
 #pragma unroll 1
-    for (int tap = 0; tap < 9; tap++) {
+    for (int tap = 0; tap < (SIB_PROBE == 3 ? SIB_PROBE_TAPS : 9); tap++) {
         const int t2 = tap + 1 < 9 ? tap + 1 : 0;  // past the last tap: tap 0 again (unused)
         const int toff = (t2 / 3 - 1) * Wd + (t2 % 3 - 1);
 #pragma unroll

@@ -982,6 +982,18 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
     return GZ_OK;
 }
 
+int gz_plan_gn_stats(void* d_workspace, int32_t n, int32_t num_simulations, int64_t* out, int32_t reset, void* stream);
+
+int gz_selfplay_plan_gn_stats(void* d_workspace, int32_t n_slots, int32_t num_simulations, int64_t* out,
+                              int32_t reset, void* stream) {
+    if (!d_workspace || n_slots <= 0) return fail(GZ_ERR_ARG, "gz_selfplay_plan_gn_stats: bad arguments");
+    char* ws = (char*)d_workspace;
+    ws += ((size_t)n_slots * sizeof(gz_board_state) + 255) & ~(size_t)255;
+    ws += ((size_t)n_slots * 8 + 255) & ~(size_t)255;
+    ws += ((size_t)n_slots * 4 + 255) & ~(size_t)255;
+    return gz_plan_gn_stats(ws, n_slots, num_simulations, out, reset, stream);
+}
+
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations, gz_board_state* d_out,
                        int64_t* d_game_ids, void* stream) {
     (void)num_simulations;

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("GZ_LIBRARY") or os.path.join(HERE, "libgzero.so")
 
 GZ_OK = 0
 GZ_FLAG_GATHER_LEAVES = 1
+GZ_FLAG_GN_CHECK = 2  # planner searches: check every incremental GraphNet row against the full forward
 GZ_MAX_SIMULATIONS = 4095
 GZ_MAX_GAME_PLIES = 200
 GZ_PV_FP32 = 0
@@ -110,6 +111,11 @@ SIGNATURES = {
     "gz_selfplay_plan_workspace_bytes": (_SZ, [_I32, _I32]),
     "gz_selfplay_plan_run": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I32, _P, _I32, _P, _I32, _P, _P, _P]),
     "gz_planner_move": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
+    "gz_plan_gn_stats": (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P]),
+    "gz_gn_slot_bytes": (_SZ, []),
+    "gz_gn_chain_workspace_bytes": (_SZ, [_I32]),
+    "gz_gn_forward_chain": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),
+    "gz_selfplay_plan_gn_stats": (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P]),
     "gz_knowledge_scores": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
     "gz_dataset_build": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P]),
     "gz_dataset_gather": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _I64, _I32, _P, _P, _P, _P]),

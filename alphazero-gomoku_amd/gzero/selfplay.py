@@ -48,6 +48,7 @@ class SelfPlayEngine:
             self.pparams = _lib.planner_params(planner_difficulty)
             self.d_plan_ws = torch.empty(self.lib.gz_selfplay_plan_workspace_bytes(self.n_slots, num_simulations),
                                          dtype=torch.uint8, device="cuda")
+            self.gn_stats(reset=True)
         self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
             else PVWeights(pv_weights)
         if pv_mode not in ("full", "tree"):
@@ -100,6 +101,19 @@ class SelfPlayEngine:
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
                                             self.leaf_cap, ptr(self.d_meta), ptr(self.d_counters), stream()),
                    "gz_selfplay_run")
+
+    def gn_stats(self, reset=False, check=None):
+        """Planner-net rows since the last reset: {"full", "incremental", "checked",
+        "mismatched"} (gz_selfplay_plan_gn_stats; synchronises).  check=True/False
+        turns GZ_FLAG_GN_CHECK (every incremental row re-run by the full forward and
+        compared bitwise) on/off for the following searches."""
+        if check is not None:
+            f = self.params.flags & ~_lib.GZ_FLAG_GN_CHECK
+            self.params.flags = f | (_lib.GZ_FLAG_GN_CHECK if check else 0)
+        out = (ctypes.c_int64 * 4)()
+        _lib.check(self.lib.gz_selfplay_plan_gn_stats(ptr(self.d_plan_ws), self.n_slots, self.params.num_simulations,
+                                                      out, 1 if reset else 0, stream()), "gz_selfplay_plan_gn_stats")
+        return {"full": out[0], "incremental": out[1], "checked": out[2], "mismatched": out[3]}
 
     def advance(self, n_plies):
         """Play n_plies plies on every slot without gathering leaves for the PV forward

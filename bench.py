@@ -557,11 +557,16 @@ def main():
     if ws == 1 and args.config4_steps and not args.planner_steps:
         e4 = engine(0.2, 5, w, args.pv_mode if args.pv_precision == "f16x3" else "full")
         m4 = measure(e4, args.config4_steps, 2, burn_in, 1)
+        gs = e4.gn_stats()
         out["config4"] = {
             "value": round(m4["moves"] / m4["T"], 3), "unit": "moves/s", "steps": args.config4_steps, "warmup": 2,
             "ms_per_step": round(m4["T"] / args.config4_steps * 1e3, 3),
             "pv_boards_per_step": round(float(np.mean(m4["leaves"])), 1),
             "pv_mode": "tree" if e4.tree else "full",
+            "planner_net_rows": {"full_forward": gs["full"], "incremental": gs["incremental"],
+                                 "note": "GraphNet rows over the warm-up and timed steps: incremental = boards one "
+                                         "stone from kept maps (the search root's, or the rollout's previous "
+                                         "planner ply), bit-identical to the full forward (gn_inc_kernel)"},
             "workload": (f"BASELINE config 4: {args.slots} games, {args.sims} sims/move, beta 0.2, planner_steps 5 "
                          "(every rollout starts with 5 BGPlannerAI plies: GraphNet + OpponentDQN forward, knowledge "
                          f"search, top-k compose), PV forward + prior on every node; burn-in {burn_in} plies "

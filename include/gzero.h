@@ -58,6 +58,8 @@ typedef struct gz_search_params {
 } gz_search_params;
 
 #define GZ_FLAG_GATHER_LEAVES 1 /* append every non-terminal node's board for the PV forward */
+#define GZ_FLAG_GN_CHECK 2      /* planner searches: also run the full GraphNet forward on every
+                                   incremental row and count differing rows (gz_plan_gn_stats) */
 
 /* BGPlannerAI.params (bg_planner.py:215-219): easy {8, 0.5, 0.2}, medium
  * {12, 0.65, 0.1}, hard {16, 0.75, 0.05}. */
@@ -231,6 +233,34 @@ int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, in
                    const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
                    void* d_workspace, void* d_trees, int32_t* d_moves, gz_search_stats* d_stats,
                    uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_count, void* stream);
+
+/* Incremental planner nets inside gz_plan_search / gz_selfplay_plan_run: a planner
+ * ply's board is its predecessor plus the planner's move, and a rollout's first
+ * board usually the search root plus one stone (bg_planner.py:243-250,
+ * ai_agent.py:251-285), so GraphNet recomputes only the radius 1..5 squares around
+ * the new stone from kept maps (the root's, or the rollout's own chain); the outputs
+ * are bit-identical to gz_gn_forward's.  GZ_GN_INC=0 in the environment turns it
+ * off.  out[4] (host) = rows run by the full forward, by the incremental forward,
+ * rows checked against the full forward (GZ_FLAG_GN_CHECK) and rows that differed,
+ * summed since the last reset (reset != 0 zeroes them after reading; the counters
+ * start undefined until the first reset).  gz_selfplay_plan_gn_stats takes
+ * gz_selfplay_plan_run's workspace. */
+/* The incremental GraphNet on explicit chains (tests, tools): row i's 32-byte tag
+ * (csrc/gz_gnet.h GnTag) = {mode, base, job, cell, nst, stones[6], pad}: mode 0 =
+ * full forward, its maps and policy-conv outputs kept in slot `job`; mode 1 = the
+ * board is the board of slot `base` plus the stone `cell`, with the squares of the
+ * earlier stones stones[0..nst) (added since `base`) in slot `job`, where this row's
+ * squares go too.  Slots: gz_gn_slot_bytes() each.  p, q as gz_gn_forward (bit-
+ * identical).  Rows of one call must use distinct `job` slots, and no row's `job`
+ * may be another row's `base`.  d_workspace: gz_gn_chain_workspace_bytes(n). */
+size_t gz_gn_slot_bytes(void);
+size_t gz_gn_chain_workspace_bytes(int32_t n);
+int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boards, int32_t n, const void* d_tags,
+                        void* d_slots, float* d_p, float* d_q, void* d_workspace, void* stream);
+int gz_plan_gn_stats(void* d_workspace, int32_t n, int32_t num_simulations, int64_t* out, int32_t reset,
+                     void* stream);
+int gz_selfplay_plan_gn_stats(void* d_workspace, int32_t n_slots, int32_t num_simulations, int64_t* out,
+                              int32_t reset, void* stream);
 
 /* BGPlannerAI.get_move (bg_planner.py:232-269) for each board: d_ai = the
  * planner's colour P, d_keys = RNG stream; d_moves (-1 = None), d_draws.

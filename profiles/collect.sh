@@ -5,7 +5,7 @@
 # Usage: profiles/collect.sh <round-tag> [bench args...]
 set -u
 tag=${1:-r01}; shift || true
-args=${*:-"--steps 8 --warmup 2 --no-cpu-baseline --config4-steps 0 --fp32-steps 0 --no-elided"}
+args=${*:-"--steps 8 --warmup 2 --no-cpu-baseline --config4-steps 0 --fp32-steps 0 --no-elided --config5-games 0"}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 export TMPDIR=/tmp

@@ -1106,6 +1106,52 @@ def _arena_task(args):
                        for b in h.arena_boards]}
 
 
+def _arena_plans_task(args):
+    """evaluate_model with the planner ON (eval_plans 2, the reference default,
+    training.py:223): as _arena_task, with every AI's planner nets loaded from the
+    fixture seeds and every planner call recorded (board, sim, top-k, p / q at the
+    top-k cells, move), so that the oracle can replay the games exactly on the
+    reference's own net outputs."""
+    base, games, eval_num_sim = args
+    import contextlib
+    import io
+    _arena_task((base, 0, True, eval_num_sim))  # installs the arena hooks
+    h = ref()
+    _install_planner_capture(h)
+    A = h.ai.AlphaZeroGomokuAI
+    if not getattr(h, "arena_plans_installed", False):
+        orig_init = A.__init__
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            if getattr(self, "bg_planner", None) is not None:
+                _load_planner(h, self.bg_planner)
+
+        A.__init__ = init
+        h.arena_plans_installed = True
+    h.arena_gid, h.arena_boards = base, []
+    h.planner_calls = []
+    cur = h.nn.GomokuModel(model_path=None, board_size=15, device="cpu")
+    bl = h.nn.GomokuModel(model_path=None, board_size=15, device="cpu")
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = h.tr.evaluate_model(cur, bl, "cpu", games=games, eval_difficulty="easy", eval_num_sim=eval_num_sim,
+                                  eval_plans=2)
+    calls = h.planner_calls
+    h.planner_calls = None
+    return {"game_id_base": base, "games": games, "baseline": True, "eval_num_sim": eval_num_sim,
+            "easy_sims": ARENA_EASY_SIMS, "eval_plans": 2, "result": res, "seconds": time.time() - t0,
+            "boards": [{"moves": [r * N + c for r, c, _ in b.move_history], "winner": b.winner}
+                       for b in h.arena_boards], "calls": calls}
+
+
+def part_arena_plans():
+    tasks = [(9200 + 10 * i, 2, [3, 4][i % 2]) for i in range(4)]
+    with Pool(4) as pool:
+        out = pool.map(_arena_plans_task, tasks, chunksize=1)
+    dump("arena_plans", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
+
+
 def part_arena():
     tasks = [(9000 + 10 * i, 2, False, [3, 6][i % 2]) for i in range(4)]
     tasks += [(9100 + 10 * i, 2, True, 3) for i in range(4)]
@@ -1117,7 +1163,7 @@ def part_arena():
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
          "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "pvnet2": part_pvnet2, "augment": part_augment,
          "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
-         "sgd": part_sgd, "arena": part_arena}
+         "sgd": part_sgd, "arena": part_arena, "arena_plans": part_arena_plans}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(PARTS)

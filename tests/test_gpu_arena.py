@@ -96,3 +96,64 @@ def test_arena_vs_reference_fixture(monkeypatch):
         for got, ref in zip(res["games"], c["boards"]):
             assert got["moves"] == ref["moves"], c["game_id_base"]
             assert got["winner"] == ref["winner"]
+
+
+def test_arena_with_planner_vs_oracle(monkeypatch, oracle):
+    """evaluate_model with the planner ON (eval_plans 2, the reference default,
+    training.py:223) on the fixture's settings (tests/golden arena_plans.json.gz:
+    planner nets of the fixture seeds, easy simulations lowered, one seed, game ids
+    base + g): every batched GPU game equals the oracle's game driven by the GPU's own
+    planner-net outputs (gz_gn_forward), move for move.  With
+    test_oracle_planner.test_arena_with_planner_exact_on_reference_outputs (the oracle
+    on the reference's recorded outputs = the reference's games) this pins the
+    planner-steered arena to the reference's evaluate_model; the games whose moves
+    differ from the reference's own (a near-tie of the two implementations' fp32 net
+    outputs flips a planner choice) are counted, not failed."""
+    import ai_agent
+    import bg_planner
+    from conftest import golden
+    from gzero import boards, device, planner_nets
+    from neural_network import GomokuModel
+    from training import evaluate_model
+    g = golden("arena_plans")
+    gsd, dsd = planner_nets.init_graphnet_state(g["gn_seed"]), planner_nets.init_dqn_state(g["dqn_seed"])
+    orig_p = bg_planner.BGPlannerAI.__init__
+
+    def pinit(self, *a, **k):
+        orig_p(self, *a, **k)
+        self.graph_net.load_state_dict(gsd)
+        self.opp_dqn.load_state_dict(dsd)
+
+    orig_a = ai_agent.AlphaZeroGomokuAI.__init__
+
+    def ainit(self, *a, **k):
+        orig_a(self, *a, **k)
+        if self.difficulty == "easy":
+            self.params["num_simulations"] = g["cases"][0]["easy_sims"]
+
+    monkeypatch.setattr(bg_planner.BGPlannerAI, "__init__", pinit)
+    monkeypatch.setattr(ai_agent.AlphaZeroGomokuAI, "__init__", ainit)
+    gnw = device.GNWeights(planner_nets.pack_planner_weights(gsd, dsd))
+
+    def pq(board, game_id, sim, step):
+        cells = np.frombuffer(bytes(board.cell), dtype=np.int8).reshape(1, 225)
+        bl, wh = boards.cells_to_words(cells)
+        p, q, _ = device.gn_forward(gnw, boards.leaf_words(bl, wh))
+        return p[0], q[0]
+
+    cur, base = GomokuModel(device="cpu"), GomokuModel(device="cpu")
+    differ = 0
+    for c in g["cases"]:
+        res = evaluate_model(cur, base, games=c["games"], eval_difficulty="easy", eval_num_sim=c["eval_num_sim"],
+                             eval_plans=2, seeds=(g["seed"], g["seed"]), game_id_base=c["game_id_base"],
+                             return_games=True)
+        cp = oracle.make_params("easy", sims=c["easy_sims"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+        bp = oracle.make_params("easy", sims=c["eval_num_sim"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+        for k, got in enumerate(res["games"]):
+            black, white = (cp, bp) if k % 2 == 0 else (bp, cp)
+            ref = oracle.play_game(black, white, c["game_id_base"] + k)
+            assert got["moves"] == ref["moves"], (c["game_id_base"], k)
+            assert got["winner"] == (ref["winner"] or None)
+            differ += got["moves"] != c["boards"][k]["moves"]
+    print(f"planner-on arena: {differ} of {sum(c['games'] for c in g['cases'])} games differ from the "
+          "reference's own (net near-ties)")

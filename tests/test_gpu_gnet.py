@@ -61,3 +61,96 @@ def test_gnet_vs_torch_random(nets):
     np.testing.assert_allclose(lg, lr, rtol=0, atol=1e-4)
     np.testing.assert_allclose(p, pr, rtol=0, atol=1e-6)
     np.testing.assert_allclose(q, qr, rtol=0, atol=1e-4)
+
+
+GN_TAG = np.dtype([("mode", "<i4"), ("base", "<i4"), ("job", "<i4"), ("cell", "<i4"), ("nst", "<i4"),
+                   ("st", "u1", (6,)), ("pad", "u1", (2,)), ("pad2", "<i4")])
+
+
+def _chain_forward(w, cells, tags, d_slots):
+    import torch
+    from gzero import _lib, device
+    lib = _lib.load()
+    n = len(cells)
+    bl, wh = boards.cells_to_words(np.asarray(cells, np.int8))
+    rows = boards.leaf_words(bl, wh)
+    d_b = torch.from_numpy(np.ascontiguousarray(rows, np.uint32).view(np.int32).copy()).cuda()
+    d_t = torch.from_numpy(np.ascontiguousarray(tags).view(np.uint8).copy()).cuda()
+    d_p = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    d_q = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    ws = torch.empty(lib.gz_gn_chain_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.gz_gn_forward_chain(device.ptr(w.tensor), device.ptr(d_b), n, device.ptr(d_t),
+                                       device.ptr(d_slots), device.ptr(d_p), device.ptr(d_q), device.ptr(ws),
+                                       device.stream()), "gz_gn_forward_chain")
+    torch.cuda.synchronize()
+    p, q, _ = device.gn_forward(w, rows)
+    return d_p.cpu().numpy().reshape(n, 225), d_q.cpu().numpy().reshape(n, 225), p, q
+
+
+def test_incremental_graphnet_chains_bitwise(nets):
+    """gn_inc_kernel on explicit chains: bases (full forward, maps kept), then 6 plies
+    adding one stone each -- centre, edges and corners, stones near each other and
+    far apart, a full forward in the middle of some chains -- p and q bit-identical to
+    gz_gn_forward of the same boards at every ply."""
+    import torch
+    from gzero import _lib
+    _, _, _, w = nets
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+    R = 40
+    base = rng.choice(3, size=(R, 225), p=[0.7, 0.15, 0.15]).astype(np.int8)
+    base[0] = 0  # the empty board
+    d_slots = torch.empty(3 * R * lib.gz_gn_slot_bytes(), dtype=torch.uint8, device="cuda")
+    tags = np.zeros(R, GN_TAG)
+    tags["mode"], tags["job"] = 0, np.arange(R)
+    p, q, pf, qf = _chain_forward(w, base, tags, d_slots)
+    assert p.view(np.uint32).tolist() == pf.view(np.uint32).tolist() and (q.view(np.uint32) == qf.view(np.uint32)).all()
+    cur = base.copy()
+    stones = [[] for _ in range(R)]
+    bj = np.zeros(R, bool)
+    corners = [0, 14, 210, 224, 7, 105, 119, 217]
+    for ply in range(6):
+        tags = np.zeros(R, GN_TAG)
+        for r in range(R):
+            empty = np.flatnonzero(cur[r] == 0)
+            pref = [c for c in corners if cur[r][c] == 0]
+            c = int(pref[(r + ply) % len(pref)]) if (r % 3 == 0 and pref) else int(rng.choice(empty))
+            cur[r][c] = 1 + (ply + r) % 2
+            full = r % 5 == 4 and ply == 2  # a full forward inside the chain
+            t = tags[r]
+            t["job"] = R + r
+            if full:
+                t["mode"], t["base"] = 0, R + r
+                bj[r], stones[r] = True, []
+            else:
+                t["mode"], t["cell"] = 1, c
+                t["base"] = R + r if bj[r] else r
+                t["nst"] = 0 if bj[r] else len(stones[r])
+                for k, s in enumerate(stones[r]):
+                    t["st"][k] = s
+                if not bj[r]:
+                    stones[r].append(c)
+        p, q, pf, qf = _chain_forward(w, cur, tags, d_slots)
+        bad = [r for r in range(R) if not ((p[r].view(np.uint32) == pf[r].view(np.uint32)).all()
+                                           and (q[r].view(np.uint32) == qf[r].view(np.uint32)).all())]
+        if bad:  # which stored map first differs from the full forward's (diagnostics)
+            ft = np.zeros(R, GN_TAG)
+            ft["mode"], ft["job"] = 0, 2 * R + np.arange(R)
+            _chain_forward(w, cur, ft, d_slots)
+            sb = lib.gz_gn_slot_bytes()
+            raw = d_slots.cpu().numpy()
+            r = bad[0]
+            job = raw[(R + r) * sb:(R + r + 1) * sb]
+            ref = raw[(2 * R + r) * sb:(2 * R + r + 1) * sb]
+            c = int(tags[r]["cell"]) if tags[r]["mode"] == 1 else 0
+            diag = []
+            for m in range(4):
+                mj = job[m * 57600:(m + 1) * 57600].view(np.float16).reshape(16, 225, 8)
+                mr = ref[m * 57600:(m + 1) * 57600].view(np.float16).reshape(16, 225, 8)
+                sq = [pp for pp in range(225) if abs(pp // 15 - c // 15) <= m + 1 and abs(pp % 15 - c % 15) <= m + 1]
+                nb = sum(not np.array_equal(mj[:, pp].view(np.uint16), mr[:, pp].view(np.uint16)) for pp in sq)
+                diag.append((m, nb, len(sq)))
+            pj = job[230400:230400 + 1800].view(np.float32)
+            pr_ = ref[230400:230400 + 1800].view(np.float32)
+            diag.append(("pol", int((pj.view(np.uint32) != pr_.view(np.uint32)).sum()), float(np.abs(pj - pr_).max())))
+            assert not bad, (ply, bad[:8], float(np.abs(p - pf).max()), float(np.abs(q - qf).max()), c, diag)

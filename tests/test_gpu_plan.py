@@ -193,3 +193,45 @@ def test_config1_game_vs_oracle(oracle, gnw):
     ref = oracle.play_game(prm, prm, 0)
     assert game["moves"] == ref["moves"]
     assert game["players"] == ref["players"] and game["z"] == ref["z"]
+
+
+def test_incremental_graphnet_bitwise_on_planner_plies(gnw):
+    """Config-4 plies (200 sims, beta 0.2, planner_steps 5, medium) from mid-game
+    positions: every planner-net row the incremental GraphNet (gn_inc_kernel) ran
+    -- rollout boards one stone from the root, and each later planner ply's board --
+    has policy-conv outputs, p and q bitwise equal to the full forward's
+    (GZ_FLAG_GN_CHECK re-runs gz_gn_forward on every row of every planner step)."""
+    from gzero.selfplay import SelfPlayEngine
+    eng = SelfPlayEngine(n_slots=96, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED + 7,
+                         plies_per_step=1, planner_steps=5, planner_difficulty="medium", gn_weights=gnw)
+    eng.advance(24)
+    eng.gn_stats(reset=True, check=True)
+    for _ in range(2):
+        eng.step()
+    st = eng.gn_stats()
+    assert st["incremental"] > 0.8 * (st["incremental"] + st["full"]), st
+    assert st["checked"] == st["incremental"] + st["full"], st
+    assert st["mismatched"] == 0, st
+
+
+def test_incremental_graphnet_same_games(gnw, monkeypatch):
+    """The same planner self-play with the incremental GraphNet on and off
+    (GZ_GN_INC=0): identical boards and records after every step."""
+    from gzero.selfplay import SelfPlayEngine
+
+    def run(flag):
+        monkeypatch.setenv("GZ_GN_INC", flag)
+        eng = SelfPlayEngine(n_slots=32, num_simulations=40, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED + 9,
+                             plies_per_step=4, planner_steps=5, planner_difficulty="medium", gn_weights=gnw)
+        eng.advance(8)
+        out = []
+        for _ in range(4):
+            eng.step()
+            b, g = eng.boards()
+            out.append((np.asarray(b).tobytes(), np.asarray(g).tobytes(), eng.records().tobytes()))
+        return out, eng.gn_stats()
+
+    on, st_on = run("1")
+    off, st_off = run("0")
+    assert st_on["incremental"] > 0 and st_off["incremental"] == 0
+    assert on == off

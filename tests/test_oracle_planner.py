@@ -144,3 +144,41 @@ def test_planner_search_vs_reference(idx):
         kids = [[tree["move"][i], tree["visits"][i], tree["value"][i]]
                 for i in range(len(tree["parent"])) if tree["parent"][i] == 0]
         assert kids == c["children"]
+
+
+def _arena_pq(calls):
+    """pq callback from recorded planner calls: a board's p / q at its recorded top-k
+    cells (p / q depend on the board alone, so one board's calls merge)."""
+    tab = {}
+    for call in calls:
+        p, q = tab.setdefault(call["board"], (np.zeros(225, np.float32), np.zeros(225, np.float32)))
+        p[call["top"]] = _hexf(call["p"])
+        q[call["top"]] = _hexf(call["q"])
+
+    def pq(board, game_id, sim, step):
+        return tab[_board_str(board)]
+    return pq
+
+
+def test_arena_with_planner_exact_on_reference_outputs():
+    """evaluate_model with the planner ON (eval_plans 2, the reference default,
+    training.py:223; tests/golden arena_plans.json.gz, make_golden.py
+    part_arena_plans): with every planner call fed the reference's own recorded net
+    outputs, the oracle plays each game (the evaluated AI on black in even games,
+    easy difficulty with the fixture's simulation counts, beta 0.2, 2 planner plies,
+    the fixture's seed on both sides, game id = base + g) move for move and to the
+    same winner as the reference's evaluate_model."""
+    g = golden("arena_plans")
+    for c in g["cases"]:
+        pq = _arena_pq(c["calls"])
+        cur = O.make_params("easy", sims=c["easy_sims"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+        base = O.make_params("easy", sims=c["eval_num_sim"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+        for k, ref in enumerate(c["boards"]):
+            black, white = (cur, base) if k % 2 == 0 else (base, cur)
+            got = O.play_game(black, white, c["game_id_base"] + k)
+            assert got["moves"] == ref["moves"], (c["game_id_base"], k)
+            assert (got["winner"] or None) == ref["winner"]
+        # the evaluated AI plays black in even games: its wins / losses are the result's
+        won = [b["winner"] == (1 if k % 2 == 0 else 2) for k, b in enumerate(c["boards"])]
+        lost = [b["winner"] == (2 if k % 2 == 0 else 1) for k, b in enumerate(c["boards"])]
+        assert (sum(won), sum(lost)) == (c["result"]["wins"], c["result"]["losses"])
