@@ -532,10 +532,11 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
 // kept; any other board runs the full forward and keeps its maps in the job's slot.
 // Job slot: n + (job - j0) in round 0's chunks (slot_game 0), n + game afterwards
 // (one job per game).
-__global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int j1, int planner_steps, int final_round,
-                                    int inc, int slot_game) {
-    const int i = j0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= j1) return;
+__global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int count, int stride, int planner_steps,
+                                    int final_round, int inc, int slot_game) {
+    const int t_ = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t_ >= count) return;
+    const int i = j0 + t_ * stride;
     PlanJob& j = w.jobs[i];
     if (j.state != 1) return;
     BB black, white;
@@ -553,7 +554,7 @@ __global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int j1, i
         dst[3] = make_uint4(white.w[4], white.w[5], white.w[6], white.w[7]);
         if (inc) {
             GnTag t;
-            t.job = n + (slot_game ? j.game : i - j0);
+            t.job = n + (slot_game ? j.game : t_);
             t.mode = 1;
             t.nst = 0;
             t.cell = -1;
@@ -667,9 +668,10 @@ __global__ __launch_bounds__(WAVE) void plan_step_kernel(Workspace w, gz_planner
 }
 
 // offensive rollout (_simulate :276-285) of every job past its planner plies
-__global__ void plan_rollout_kernel(Workspace w, int n_jobs, int max_depth) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_jobs) return;
+__global__ void plan_rollout_kernel(Workspace w, int count, int stride, int max_depth) {
+    const int t_ = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t_ >= count) return;
+    const int i = t_ * stride;
     PlanJob& j = w.jobs[i];
     if (j.state != 2) return;
     BB black, white;
@@ -1005,7 +1007,6 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
     LeafSink sink{d_leaves, leaf_cap, d_leaf_count, gather ? d_leaf_meta : nullptr};
     const int n_jobs = n * S;
     const int C = (int)chunk_rows(n, S);
-    const int jb = (n_jobs + 255) / 256;
     // incremental GraphNet (gn_inc_kernel) unless GZ_GN_INC=0; GZ_FLAG_GN_CHECK also
     // runs the full forward on every row and counts the rows that differ
     const char* env = getenv("GZ_GN_INC");
@@ -1028,8 +1029,10 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         int r;
         // rows, pending (recomputed by the next resume), nfull, ninc
         if (hipMemsetAsync(&w.ctr->rows, 0, 16, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
-        plan_collect_kernel<<<(j1 - j0 + 255) / 256, 256, 0, s>>>(w, S, n, j0, j1, p->planner_steps, 0, inc ? 1 : 0,
-                                                                   slot_game);
+        // jobs j0 .. j1-1 (round 0's chunk), or (slot_game) the one job per game at g * S
+        const int cnt = slot_game ? n : j1 - j0, stride = slot_game ? S : 1;
+        plan_collect_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(w, S, n, j0, cnt, stride, p->planner_steps, 0,
+                                                               inc ? 1 : 0, slot_game);
         if ((r = plan_check("plan_collect_kernel"))) return r;
         if (!inc) {
             if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
@@ -1070,9 +1073,11 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
             for (int st = 0; st < p->planner_steps; st++)
                 if ((rc = planner_step(0, n_jobs, n, 1))) return rc;
         }
-        plan_collect_kernel<<<jb, 256, 0, s>>>(w, S, n, 0, n_jobs, p->planner_steps, 1, 0, 0);
+        // after round 0 the only jobs are the sequential simulations' (job g * S)
+        const int cnt = round == 0 ? n_jobs : n, stride = round == 0 ? 1 : S;
+        plan_collect_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(w, S, n, 0, cnt, stride, p->planner_steps, 1, 0, 0);
         if ((rc = plan_check("plan_collect_kernel"))) return rc;
-        plan_rollout_kernel<<<jb, 256, 0, s>>>(w, n_jobs, p->max_depth);
+        plan_rollout_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(w, cnt, stride, p->max_depth);
         if ((rc = plan_check("plan_rollout_kernel"))) return rc;
         if (hipMemsetAsync(&w.ctr->pending, 0, 4, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
         plan_resume_kernel<<<n, WAVE, 0, s>>>(n, *p, w, sink, gather ? 1 : 0, d_moves, d_stats);
