@@ -429,10 +429,20 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
 // Every output element takes gn_kernel's products in gn_kernel's order (the same
 // k-steps, MFMA operand splits and epilogues), so the records -- and p, q from
 // gn_heads_kernel -- are bitwise those of the full forward.
-constexpr int IG = 3;                     // boards per chunk
-constexpr int NTI = 512;                  // 8 waves: n-tile wave & 3, M half wave >> 2
+#ifndef GN_IG
+#define GN_IG 3  // boards per chunk (1: 4 waves and 2 workgroups per CU)
+#endif
+constexpr int IG = GN_IG;
+constexpr int IMH = IG == 1 ? 1 : 2;      // M parts: waves = 4 n-tiles x IMH
+constexpr int NTI = 256 * IMH;            // wave: n-tile wave & 3, M part wave >> 2
+constexpr int IWG = IG == 1 ? 2 : 1;      // workgroups per CU
 constexpr int IWIN_MAX = 169 * 256;       // bytes of a radius-6 window (2 planes x 8 cg x 169 x 16 B)
-constexpr int IA = IG * IWIN_MAX;         // windows / square rows
+// LDS: the windows at 0 (up to IG x 43 KB), each 3x3 layer's output rows at the top of
+// [0, IA) (B(ro): [plane][8 cg][ig_brows(ro)][8] halves at IA - 256 ig_brows(ro)), so
+// that the next window's fill can start as soon as the 3x3 k-loop has read its window
+constexpr int IA = IG == 1 ? 65536 : 153600;
+__host__ __device__ constexpr int ig_brows(int ro) { return (IG * (2 * ro + 1) * (2 * ro + 1) + 15) / 16 * 16; }
+__host__ __device__ constexpr int ig_boff(int ro) { return IA - 256 * ig_brows(ro); }
 constexpr int ICOL = IA;                  // embed im2col [IG][4][16][8] halves
 constexpr int IPC = ICOL + IG * 1024;     // policy-conv outputs [IG][2][128] floats
 constexpr int IU = IPC + IG * 2 * 128 * 4;
@@ -440,8 +450,10 @@ constexpr int ITAB = IU + IG * 128;         // row tables of the radius 1..5 pas
 __host__ __device__ constexpr int itab_off(int ro) { return ro <= 1 ? 0 : itab_off(ro - 1) + IG * (2 * ro - 1) * (2 * ro - 1); }
 constexpr int ITOT = itab_off(6);            // 855 entries
 constexpr int ILDS = ITAB + (ITOT + 8) * 4;
-constexpr int IROWS = 368;                // >= IG x 121 square rows, x16
-static_assert(ILDS <= 160 * 1024 && 2 * 8 * IROWS * 16 <= IA && IG * 121 <= IROWS, "LDS");
+static_assert(ILDS * IWG <= 160 * 1024 && IG * IWIN_MAX <= IA && ig_boff(5) >= 0, "LDS");
+// the next window vs the rows the 1x1 layer before it reads: map 1, 2 windows clear
+// of B(2), B(3); the map-3 window overlaps B(4) above ig_boff(4) (filled in two parts)
+static_assert(IG * 81 * 256 <= ig_boff(2) && IG * 121 * 256 <= ig_boff(3), "window / rows overlap");
 
 struct GnUnit {
     const _Float16* base;  // maps the chain adds stones to
@@ -486,36 +498,50 @@ __device__ __forceinline__ const _Float16* ig_rfl(const _Float16* p) {
 // unit's new square (radius MAP + 1, written by the producing epilogue), zeros off
 // the board; drained by the caller's barrier
 template <int MAP>
-__device__ __forceinline__ void ig_fill(char* lds, const GnUnit* U, int ng, int tid) {
-    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 16 * P, IT = (PER + NTI - 1) / NTI, rc = MAP + 1;
-    const int wb = tid & ~63;
-    for (int g = 0; g < ng; g++) {
+__device__ __forceinline__ void ig_fill(char* lds, const GnUnit* U, int ng, int tid, int lo = 0, int hi = 1 << 30) {
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, NB = (P + 63) / 64, rc = MAP + 1;
+    // work blocks (unit g, 64 window positions): the lane's position and its source
+    // are worked out once, then its 16 channel-group planes go by LDS-DMA (for a given
+    // plane a wave's 64 positions are contiguous in LDS)
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int blk = wave; blk < ng * NB; blk += NTI / 64) {
+        const int g = blk / NB, b0 = (blk - g * NB) * 64, loc = b0 + lane;
         const _Float16* base = ig_rfl(U[g].base) + MAP * SLOT_MAP_HALVES;
         const _Float16* job = ig_rfl(U[g].job) + MAP * SLOT_MAP_HALVES;
         const int cell = __builtin_amdgcn_readfirstlane(U[g].cell), nst = __builtin_amdgcn_readfirstlane(U[g].nst);
         const int cr = cell / 15, cc = cell - cr * 15;
-        char* dst = lds + (size_t)g * P * 256;
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int i = tid + k * NTI;
-            if ((k + 1) * NTI > PER && i >= PER) continue;
-            const int pcg = i / P, loc = i - pcg * P;
-            const int dr = loc / Wd - R, dc = loc % Wd - R;
-            const int pr = cr + dr, pc = cc + dc;
-            const bool on = pr >= 0 && pr < 15 && pc >= 0 && pc < 15;
-            if (on && iabs_(dr) <= rc && iabs_(dc) <= rc) continue;  // the new square (its epilogue writes it)
-            const void* src = (const void*)gz_gn_zero16;
-            if (on) {
-                bool mine = false;
-                for (int s = 0; s < nst; s++) {
-                    const int sc = U[g].st[s], sr = sc / 15, scc = sc - sr * 15;
-                    mine |= iabs_(pr - sr) <= rc && iabs_(pc - scc) <= rc;
-                }
-                src = (const void*)((mine ? job : base) + ((size_t)pcg * POS + pr * 15 + pc) * 8);
+        const int dr = loc / Wd - R, dc = loc % Wd - R;
+        const int pr = cr + dr, pc = cc + dc;
+        const bool on = pr >= 0 && pr < 15 && pc >= 0 && pc < 15;
+        // positions past the window, and the new square (its epilogue writes it): no load
+        const bool skip = loc >= P || (on && iabs_(dr) <= rc && iabs_(dc) <= rc);
+        const char* src = (const char*)gz_gn_zero16;
+        int step = 0;  // bytes between planes at the source
+        if (on) {
+            bool mine = false;
+            for (int s = 0; s < nst; s++) {
+                const int sc = U[g].st[s], sr = sc / 15, scc = sc - sr * 15;
+                mine |= iabs_(pr - sr) <= rc && iabs_(pc - scc) <= rc;
             }
-            __builtin_amdgcn_global_load_lds((ig_glb_t*)src, (ig_lds_t*)(dst + (size_t)(wb + k * NTI) * 16), 16, 0, 0);
+            src = (const char*)((mine ? job : base) + (pr * 15 + pc) * 8);
+            step = POS * 16;
+        }
+        char* dst = lds + (size_t)g * P * 256 + (size_t)b0 * 16;  // + lane * 16 by the DMA
+        const int byte0 = g * P * 256 + loc * 16;
+#pragma unroll
+        for (int pcg = 0; pcg < 16; pcg++) {
+            const int byte = byte0 + pcg * P * 16;
+            if (!skip && byte >= lo && byte < hi)
+                __builtin_amdgcn_global_load_lds((ig_glb_t*)(src + pcg * step), (ig_lds_t*)(dst + pcg * P * 16), 16, 0, 0);
         }
     }
+}
+
+// a workgroup barrier that waits for this wave's LDS accesses only, not for its
+// outstanding global loads -- a window fill (LDS-DMA) issued before it stays in flight
+__device__ __forceinline__ void ig_bar() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt, expcnt unconstrained
+    __builtin_amdgcn_s_barrier();
 }
 
 // the rows of a pass: every unit's square of radius ro (clipped, row-major), packed;
@@ -554,6 +580,18 @@ __device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng
     }
 }
 
+#ifndef IG_PROBE
+#define IG_PROBE 0
+#endif
+// tiles per group of the 3x3 k-loop: a group's 3 products interleave over its tiles, so
+// an MFMA's accumulator was last written GT - 1 MFMAs earlier
+#ifndef IG_GT
+#define IG_GT 3  // 6: ±0 (28 spilled VGPRs)
+#endif
+#if IG_PROBE
+#warning "IG_PROBE is a timing probe: the incremental GraphNet's results are wrong in this build"
+#endif
+
 // compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
 template <class F, int... I>
 __device__ __forceinline__ void ig_sfor(F&& f, std::integer_sequence<int, I...>) {
@@ -570,12 +608,13 @@ __device__ __forceinline__ void ig_sfor(F&& f, std::integer_sequence<int, I...>)
 template <int NT, int NMAX, int R>
 __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
                                             int nt, int lane, f32x4 (&acc)[NMAX]) {
-    constexpr int Wd = 2 * R + 1, P = Wd * Wd, KS = 18, LO = 64 * P, GT = 3, NG = (NT + GT - 1) / GT;
+    constexpr int Wd = 2 * R + 1, P = Wd * Wd, KS = 18, LO = 64 * P, GT = IG_GT < NT ? IG_GT : NT, NG = (NT + GT - 1) / GT;
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt * 64 + lane) * 16;
     auto wload = [&](int ks, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * 4096 + lo * KS * 4096, 0));
+        // (IG_PROBE 2, timing only: every k-step reads k-step 0 / 1's fragments, L1-resident)
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (IG_PROBE == 2 ? (ks & 1) : ks) * 4096 + lo * KS * 4096, 0));
     };
     h8 b[4][2];
 #pragma unroll
@@ -603,7 +642,11 @@ __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr
             if (m < NT) {
                 const int o = c8[m] + toff(tap) + CQ * 4 * P * 8;
                 fa[PB][j][0] = *(const h8*)(act + o);
+#if IG_PROBE == 1  // timing probe (wrong results): no lo-plane activation reads (half the LDS reads)
+                fa[PB][j][1] = fa[PB][j][0];
+#else
                 fa[PB][j][1] = *(const h8*)(act + LO + o);
+#endif
             }
         }
     };
@@ -645,8 +688,18 @@ __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr
             __builtin_amdgcn_sched_group_barrier(0x008, 3 * tiles_of(g), 0);  // MFMA
         }, std::make_integer_sequence<int, NK * NG>{});
     };
+#ifndef IG_UNROLL
+#define IG_UNROLL 0  // 1: 2 % slower (same box), 5 minutes of compile
+#endif
+#if IG_UNROLL
+    // fully unrolled: no loop back-edge, where the compiler would wait for every
+    // outstanding weight load (vmcnt(0)) instead of the one it needs
+    ig_sfor([&](auto tp_) { constexpr int tp = decltype(tp_)::value; ksteps(std::integral_constant<int, 4>{}, 4 * tp, 2 * tp); },
+            std::make_integer_sequence<int, 4>{});
+#else
 #pragma unroll 1
     for (int tp = 0; tp < 4; tp++) ksteps(std::integral_constant<int, 4>{}, 4 * tp, 2 * tp);  // taps 2tp, 2tp+1
+#endif
     ksteps(std::integral_constant<int, 2>{}, 16, 8);                                          // tap 8
 #pragma unroll
     for (int m = 0; m < NT; m++) acc[m] = c[m];
@@ -681,19 +734,35 @@ struct IgTiles {
 __device__ __forceinline__ IgTiles ig_tiles(const char* lds, int ro, int mh, int lane) {
     IgTiles t;
     t.total = ig_total(lds, ro);
-    const int T = (t.total + 15) >> 4, T0 = (T + 1) >> 1, t0 = mh * T0;
+    const int T = (t.total + 15) >> 4, T0 = (T + IMH - 1) / IMH, t0 = mh * T0;
     t.nt = T - t0 < T0 ? (T - t0 > 0 ? T - t0 : 0) : T0;
     t.i0 = t0 * 16 + (lane & 15);
     return t;
 }
 
-constexpr int ig_nmax(int ro) { return ((IG * (2 * ro + 1) * (2 * ro + 1) + 15) / 16 + 1) / 2; }
+constexpr int ig_nmax(int ro) { return ((IG * (2 * ro + 1) * (2 * ro + 1) + 15) / 16 + IMH - 1) / IMH; }
 
 // 3x3 layer (L0, L2, L4, L6: input map MAP window, output square radius MAP + 2) ->
-// relu(acc + bias) as hi / lo into the square rows [plane][cg][IROWS][8] at LDS 0
-template <int MAP, int NMAX>
+// relu(acc + bias) as hi / lo into the square rows B(ro); pre() (the next window's
+// fill) runs right after the k-loop's barrier
+struct Ig1x1W {  // a 1x1 layer's weight fragments and bias for the wave (loaded ahead)
+    h8 w0h, w1h, w0l, w1l;
+    f32x4 bias;
+};
+__device__ __forceinline__ Ig1x1W ig_w1x1(const float* __restrict__ W, int layer, int nt, int lane) {
+    const _Float16* wf = (const _Float16*)(W + h_layer_off(layer)) + ((size_t)nt * 64 + lane) * 8;
+    Ig1x1W w;
+    w.w0h = *(const h8*)wf;
+    w.w1h = *(const h8*)(wf + 4 * 64 * 8);
+    w.w0l = *(const h8*)(wf + 2 * 4 * 64 * 8);
+    w.w1l = *(const h8*)(wf + 3 * 4 * 64 * 8);
+    w.bias = *(const f32x4*)(W + layer_bias(layer) + nt * 16 + 4 * (lane >> 4));
+    return w;
+}
+
+template <int MAP, int NMAX, class Pre>
 __device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, const float* __restrict__ W, int layer,
-                                          int nt, int mh, int lane) {
+                                          int nt, int mh, int lane, Ig1x1W& next, Pre&& pre) {
     constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 2;
     static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
     const IgTiles t = ig_tiles(lds, ro, mh, lane);
@@ -736,8 +805,14 @@ __device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, co
     }
     const int ch0 = nt * 16 + 4 * (lane >> 4);
     const f32x4 bias = *(const f32x4*)(W + layer_bias(layer) + ch0);
+    next = ig_w1x1(W, layer + 1, nt, lane);
     __syncthreads();  // every wave is past the k-loop: the windows are dead
-    _Float16* sq = (_Float16*)lds;
+    // every global load so far has landed (the bias, the next 1x1 layer's weights): the
+    // fill issued next is the only VMEM traffic in flight until the 1x1 layer's end
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    pre();
+    constexpr int BR = ig_brows(ro);
+    _Float16* sq = (_Float16*)(lds + ig_boff(ro));
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
         const int i = t.i0 + 16 * m;
@@ -751,21 +826,18 @@ __device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, co
             hi[r] = h;
             lo[r] = (_Float16)(y - (float)h);
         }
-        const int o = ((ch0 >> 3) * IROWS + i) * 8 + (ch0 & 7);
+        const int o = ((ch0 >> 3) * BR + i) * 8 + (ch0 & 7);
         *(h4*)(sq + o) = hi;
-        *(h4*)(sq + 8 * IROWS * 8 + o) = lo;
+        *(h4*)(sq + 8 * BR * 8 + o) = lo;
     }
-    __syncthreads();
+    ig_bar();  // the rows are complete; the fill stays in flight through the 1x1 layer
 }
 
-// 1x1 layer (L1, L3, L5, L7) over the square rows at LDS 0 (radius ro): acc only
-template <int NMAX>
-__device__ __forceinline__ void ig_conv1(const char* lds, const IgTiles& t, const float* __restrict__ W,
-                                         int layer, int nt, int lane, f32x4 (&acc)[NMAX]) {
-    const _Float16* sq = (const _Float16*)lds;
-    const _Float16* wf = (const _Float16*)(W + h_layer_off(layer)) + ((size_t)nt * 64 + lane) * 8;
-    const h8 w0h = *(const h8*)wf, w1h = *(const h8*)(wf + 4 * 64 * 8);
-    const h8 w0l = *(const h8*)(wf + 2 * 4 * 64 * 8), w1l = *(const h8*)(wf + 3 * 4 * 64 * 8);
+// 1x1 layer (L1, L3, L5, L7) over the square rows B(ro): acc only
+template <int NMAX, int BR>
+__device__ __forceinline__ void ig_conv1(const _Float16* sq, const IgTiles& t, const Ig1x1W& w, int lane,
+                                         f32x4 (&acc)[NMAX]) {
+    const h8 w0h = w.w0h, w1h = w.w1h, w0l = w.w0l, w1l = w.w1l;
     const int q = lane >> 4;
 #pragma unroll
     for (int m = 0; m < NMAX; m++) acc[m] = zero4();
@@ -776,11 +848,11 @@ __device__ __forceinline__ void ig_conv1(const char* lds, const IgTiles& t, cons
         h8 a[3][4];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const int o = (q * IROWS + t.i0 + 16 * (g0 + j < NMAX ? g0 + j : g0)) * 8;
+            const int o = (q * BR + t.i0 + 16 * (g0 + j < NMAX ? g0 + j : g0)) * 8;
             a[j][0] = *(const h8*)(sq + o);
-            a[j][1] = *(const h8*)(sq + 8 * IROWS * 8 + o);
-            a[j][2] = *(const h8*)(sq + 4 * IROWS * 8 + o);
-            a[j][3] = *(const h8*)(sq + 8 * IROWS * 8 + 4 * IROWS * 8 + o);
+            a[j][1] = *(const h8*)(sq + 8 * BR * 8 + o);
+            a[j][2] = *(const h8*)(sq + 4 * BR * 8 + o);
+            a[j][3] = *(const h8*)(sq + 8 * BR * 8 + 4 * BR * 8 + o);
         }
 #define IG_P(W_, A_)                                                                                \
     _Pragma("unroll") for (int j = 0; j < 3; j++) if (g0 + j < NMAX)                                \
@@ -808,20 +880,21 @@ __device__ __forceinline__ void ig_split(const f32x4& acc, const f32x4& bias, h4
 }
 
 // 1x1 layer producing stored map MAP (L1 -> 1, L3 -> 2, L5 -> 3; square radius
-// MAP + 1): k-loop over the square rows, barrier, the next window's fill, then the
-// outputs into that window's new square and the row's map slot
-template <int MAP, int NMAX>
-__device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng, const float* __restrict__ W,
-                                              int layer, int nt, int mh, int lane, int tid) {
+// MAP + 1): k-loop over the square rows B(ro), barrier, rest() (what remains of the
+// next window's fill), then the outputs into that window's new square and the row's
+// map slot
+template <int MAP, int NMAX, class Rest>
+__device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng, const Ig1x1W& w, int nt, int mh,
+                                              int lane, Rest&& rest) {
     constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 1;
     static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
     const IgTiles t = ig_tiles(lds, ro, mh, lane);
     f32x4 acc[NMAX];
-    ig_conv1<NMAX>(lds, t, W, layer, nt, lane, acc);
+    ig_conv1<NMAX, ig_brows(ro)>((const _Float16*)(lds + ig_boff(ro)), t, w, lane, acc);
     const int ch0 = nt * 16 + 4 * (lane >> 4);
-    const f32x4 bias = *(const f32x4*)(W + layer_bias(layer) + ch0);
-    __syncthreads();  // the square rows are dead
-    ig_fill<MAP>(lds, U, ng, tid);
+    const f32x4 bias = w.bias;
+    ig_bar();  // the square rows are dead
+    rest();
     _Float16* win = (_Float16*)lds;
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
@@ -842,7 +915,7 @@ __device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng
     __syncthreads();  // the window is complete (the barrier drains the fill)
 }
 
-__global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards,
+__global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restrict__ W, const uint32_t* __restrict__ boards,
                                                         const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ list_count,
                                                         const GnTag* __restrict__ tags, char* __restrict__ slots,
@@ -878,6 +951,7 @@ __global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict_
             U[tid] = u;
         }
         __syncthreads();
+        GN_STAMP(8);
         ig_build_rows(lds, U, ng, tid);  // (read after the embed's barriers)
         // (the asm barriers keep the compiler from hoisting every section's per-lane
         // addresses out of the chunk loop, where they would all stay live, and spill)
@@ -911,6 +985,7 @@ __global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict_
             col[((g * 4 + (k >> 3)) * 16 + row) * 8 + (k & 7)] = v;
         }
         __syncthreads();  // the fill has landed; the im2col is complete
+        GN_STAMP(9);
         fresh(Wp, t_);
         {
             const int ln = t_ & 63, li = ln & 15, q = ln >> 4, ch0 = nt * 16 + 4 * q;
@@ -918,7 +993,7 @@ __global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict_
             const h8 wh = *(const h8*)wf, wl = *(const h8*)(wf + 4 * 64 * 8);
             const f32x4 bias = *(const f32x4*)(Wp + GE_B + ch0);
             constexpr int P0 = 49;
-            for (int g = mh; g < ng; g += 2) {
+            for (int g = mh; g < ng; g += IMH) {
                 const h8 a = *(const h8*)(col + ((g * 4 + q) * 16 + li) * 8);
                 f32x4 acc = zero4();
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a, acc, 0, 0, 0);
@@ -943,51 +1018,67 @@ __global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict_
         // ---- the tower: 3x3 over a window -> square rows; 1x1 -> the next map
         fresh(Wp, t_);
         // NMAX = the tiles of a wave's M half: ceil(ceil(IG (2 ro + 1)^2 / 16) / 2)
-        ig_layer3<0, 3>(lds, U, ng, Wp, 0, nt, mh, t_ & 63);        // L0: <= 75 rows
+        GN_STAMP(10);
+        // the window fills: maps 1 and 2 right after the 3x3 k-loop before them, map 3
+        // below B(4) then, the rest after L5's k-loop
+        auto none = [] {};
+        Ig1x1W w1;
+        ig_layer3<0, ig_nmax(2)>(lds, U, ng, Wp, 0, nt, mh, t_ & 63, w1, [&] { ig_fill<1>(lds, U, ng, t_); });  // L0
+        GN_STAMP(11);
         fresh(Wp, t_);
-        ig_layer1_map<1, 3>(lds, U, ng, Wp, 1, nt, mh, t_ & 63, t_);
+        ig_layer1_map<1, ig_nmax(2)>(lds, U, ng, w1, nt, mh, t_ & 63, none);
+        GN_STAMP(12);
         fresh(Wp, t_);
-        ig_layer3<1, 5>(lds, U, ng, Wp, 2, nt, mh, t_ & 63);        // L2: <= 147 rows
+        ig_layer3<1, ig_nmax(3)>(lds, U, ng, Wp, 2, nt, mh, t_ & 63, w1, [&] { ig_fill<2>(lds, U, ng, t_); });  // L2
+        GN_STAMP(13);
         fresh(Wp, t_);
-        ig_layer1_map<2, 5>(lds, U, ng, Wp, 3, nt, mh, t_ & 63, t_);
+        ig_layer1_map<2, ig_nmax(3)>(lds, U, ng, w1, nt, mh, t_ & 63, none);
+        GN_STAMP(14);
         fresh(Wp, t_);
-        ig_layer3<2, 8>(lds, U, ng, Wp, 4, nt, mh, t_ & 63);        // L4: <= 243 rows
+        ig_layer3<2, ig_nmax(4)>(lds, U, ng, Wp, 4, nt, mh, t_ & 63, w1,
+                        [&] { ig_fill<3>(lds, U, ng, t_, 0, ig_boff(4)); });  // L4: <= 243 rows
+        GN_STAMP(15);
         fresh(Wp, t_);
-        ig_layer1_map<3, 8>(lds, U, ng, Wp, 5, nt, mh, t_ & 63, t_);
+        ig_layer1_map<3, ig_nmax(4)>(lds, U, ng, w1, nt, mh, t_ & 63, [&] { ig_fill<3>(lds, U, ng, t_, ig_boff(4)); });
+        GN_STAMP(16);
         fresh(Wp, t_);
-        ig_layer3<3, 12>(lds, U, ng, Wp, 6, nt, mh, t_ & 63);       // L6: <= 363 rows
+        ig_layer3<3, ig_nmax(5)>(lds, U, ng, Wp, 6, nt, mh, t_ & 63, w1, none);  // L6
+        GN_STAMP(17);
         fresh(Wp, t_);
         {   // L7 (1x1) in place over the square rows, then the policy conv per row
             const int ln = t_ & 63;
-            static_assert(ig_nmax(5) <= 12, "tiles per M half");
+            constexpr int N5 = ig_nmax(5);
             const IgTiles t = ig_tiles(lds, 5, mh, ln);
-            f32x4 acc[12];
-            ig_conv1<12>(lds, t, Wp, 7, nt, ln, acc);
+            f32x4 acc[N5];
+            ig_conv1<N5, ig_brows(5)>((const _Float16*)(lds + ig_boff(5)), t, w1, ln, acc);
             const int ch0 = nt * 16 + 4 * (ln >> 4);
-            const f32x4 bias = *(const f32x4*)(Wp + layer_bias(7) + ch0);
+            const f32x4 bias = w1.bias;
             __syncthreads();
-            _Float16* sq = (_Float16*)lds;
+            constexpr int BR = ig_brows(5);
+            _Float16* sq = (_Float16*)(lds + ig_boff(5));
 #pragma unroll
-            for (int m = 0; m < 12; m++) {
+            for (int m = 0; m < N5; m++) {
                 const int i = t.i0 + 16 * m;
                 if (m >= t.nt || i >= t.total) continue;
                 h4 hi, lo;
                 ig_split(acc[m], bias, hi, lo);
-                const int o = ((ch0 >> 3) * IROWS + i) * 8 + (ch0 & 7);
+                const int o = ((ch0 >> 3) * BR + i) * 8 + (ch0 & 7);
                 *(h4*)(sq + o) = hi;
-                *(h4*)(sq + 8 * IROWS * 8 + o) = lo;
+                *(h4*)(sq + 8 * BR * 8 + o) = lo;
             }
             __syncthreads();
+            GN_STAMP(18);
             fresh(Wp, t_);
             const int total = ig_total(lds, 5);
             if (t_ < total) {
                 const IgRow r = ig_row(lds, 5, t_);
                 float p0, p1;
-                gn_pconv(Wp, sq + t_ * 8, sq + 8 * IROWS * 8 + t_ * 8, IROWS * 8, p0, p1);
+                gn_pconv(Wp, sq + t_ * 8, sq + 8 * BR * 8 + t_ * 8, BR * 8, p0, p1);
                 pcv[(r.g * 2 + 0) * 128 + r.j] = p0;
                 pcv[(r.g * 2 + 1) * 128 + r.j] = p1;
             }
             __syncthreads();
+            GN_STAMP(19);
         }
         // ---- records: policy-conv outputs (new square, else the predecessor's), stones
         for (int e = tid; e < ng * REC; e += NTI) {
@@ -1009,6 +1100,7 @@ __global__ __launch_bounds__(NTI, 1) void gn_inc_kernel(const float* __restrict_
             }
             u.rec[i] = v;
         }
+        GN_STAMP(20);
     }
 }
 }  // namespace
@@ -1071,7 +1163,7 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
     gn_kernel<<<max_rows < 2 * cus ? max_rows : 2 * cus, NT, 0, s>>>(d_weights, d_rows, max_rows, d_full_count, d_rec,
                                                                      d_full_list, (char*)d_slots, (const GnTag*)d_tags);
     const int chunks = (max_rows + IG - 1) / IG;
-    gn_inc_kernel<<<chunks < cus ? chunks : cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
+    gn_inc_kernel<<<chunks < IWG * cus ? chunks : IWG * cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
                                                               (const GnTag*)d_tags, (char*)d_slots, d_rec);
     gn_heads_kernel<<<(max_rows + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr);
     return gn_launch_check("gn_inc_kernel");

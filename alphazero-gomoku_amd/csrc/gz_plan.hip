@@ -532,19 +532,35 @@ __global__ __launch_bounds__(WAVE) void plan_begin_kernel(const gz_board_state* 
 // kept; any other board runs the full forward and keeps its maps in the job's slot.
 // Job slot: n + (job - j0) in round 0's chunks (slot_game 0), n + game afterwards
 // (one job per game).
+// one atomic per wave: lane's slot among the wave's `take` lanes in *ctr's range
+__device__ inline int wave_slot(bool take, int32_t* ctr) {
+    const uint64_t m = ballot(take);
+    if (!m) return -1;
+    const int lane = lane_id(), leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(ctr, __popcll(m));
+    base = __shfl(base, leader);
+    return take ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
+}
+
 __global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int count, int stride, int planner_steps,
                                     int final_round, int inc, int slot_game) {
+    // (every lane reaches the wave-wide slot allocations: no early returns)
     const int t_ = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t_ >= count) return;
     const int i = j0 + t_ * stride;
-    PlanJob& j = w.jobs[i];
-    if (j.state != 1) return;
-    BB black, white;
-    load_bb(black, j.black);
-    load_bb(white, j.white);
+    PlanJob* jp = t_ < count ? &w.jobs[i] : nullptr;
+    const bool st1 = jp && jp->state == 1;
     // (a planner move that ends the game sets state 3 itself, in plan_step_kernel)
-    if (!final_round && j.steps < planner_steps) {
-        const int row = atomicAdd(&w.ctr->rows, 1);
+    const bool want = st1 && !final_round && jp->steps < planner_steps;
+    if (st1 && !want) jp->state = 2;
+    const int row = wave_slot(want, &w.ctr->rows);
+    GnTag t;
+    t.mode = -1;
+    if (want) {
+        PlanJob& j = *jp;
+        BB black, white;
+        load_bb(black, j.black);
+        load_bb(white, j.white);
         j.row = row;
         w.rows[row] = i;
         uint4* dst = (uint4*)(w.gn_in + (size_t)row * 16);
@@ -553,7 +569,6 @@ __global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int count
         dst[2] = make_uint4(white.w[0], white.w[1], white.w[2], white.w[3]);
         dst[3] = make_uint4(white.w[4], white.w[5], white.w[6], white.w[7]);
         if (inc) {
-            GnTag t;
             t.job = n + (slot_game ? j.game : t_);
             t.mode = 1;
             t.nst = 0;
@@ -595,15 +610,16 @@ __global__ void plan_collect_kernel(Workspace w, int S, int n, int j0, int count
                 t.base = t.job;
                 j.bj = 1;
                 j.nst = 0;
-                w.full_list[atomicAdd(&w.ctr->nfull, 1)] = row;
-            } else {
-                if (!j.bj) j.st[j.nst++] = (uint8_t)t.cell;
-                w.inc_list[atomicAdd(&w.ctr->ninc, 1)] = row;
+            } else if (!j.bj) {
+                j.st[j.nst++] = (uint8_t)t.cell;
             }
             w.tags[row] = t;
         }
-    } else {
-        j.state = 2;
+    }
+    if (inc) {
+        const int f = wave_slot(t.mode == 0, &w.ctr->nfull), k = wave_slot(t.mode == 1, &w.ctr->ninc);
+        if (f >= 0) w.full_list[f] = row;
+        if (k >= 0) w.inc_list[k] = row;
     }
 }
 

@@ -28,9 +28,10 @@ def main():
     ap.add_argument("--bases", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--lib", default=None, help="a library to time instead (tools/_build/libgzgn_<var>.so)")
     a = ap.parse_args()
-    path = os.path.join(ROOT, "tools", "_build", "libgzgn_stamps.so") if a.stamps else \
-        os.path.join(ROOT, "alphazero-gomoku_amd", "gzero", "libgzero.so")
+    path = a.lib or (os.path.join(ROOT, "tools", "_build", "libgzgn_stamps.so") if a.stamps else
+                     os.path.join(ROOT, "alphazero-gomoku_amd", "gzero", "libgzero.so"))
     lib = ctypes.CDLL(path)
     P = ctypes.c_void_p
     lib.gz_gn_forward_chain.argtypes = [P, P, ctypes.c_int32, P, P, P, P, P, P]
