@@ -278,6 +278,9 @@ constexpr int LG_STRIDE = 228;   // logits rows
 constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
 static_assert(REC_X == 29 * 16 && REC - REC_X == 29 * 16 && REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
 
+// heads_gemm_block's products in its order, with the next k-block's A and B fragments
+// loaded while the current one's MFMAs run (4 waves per workgroup leave little else
+// to hide the loads behind)
 template <int KB, int NTILES>
 __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lane, const int (&nt)[4], int ntn,
                                            f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
@@ -285,7 +288,28 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
     for (int m = 0; m < 4; m++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[m][q] = zero4();
-    for (int kb = 0; kb < KB; kb++) heads_gemm_block(Wp, NTILES, kb, lane, nt, ntn, acc, arow);
+    const int g = lane >> 4;
+    auto load = [&](int kb, f32x4 (&a)[4], f32x4 (&b)[4]) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
+    };
+    f32x4 a[2][4], b[2][4];
+    load(0, a[0], b[0]);
+#pragma unroll 2
+    for (int kb = 0; kb < KB; kb++) {
+        const int cur = kb & 1;
+        if (kb + 1 < KB) load(kb + 1, a[cur ^ 1], b[cur ^ 1]);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][m][t], b[cur][q][t], acc[m][q], 0, 0, 0);
+    }
 }
 
 // acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles
