@@ -464,7 +464,7 @@ constexpr int IWIN_MAX = 169 * 256;       // bytes of a radius-6 window (2 plane
 // LDS: the windows at 0 (up to IG x 43 KB), each 3x3 layer's output rows at the top of
 // [0, IA) (B(ro): [plane][8 cg][ig_brows(ro)][8] halves at IA - 256 ig_brows(ro)), so
 // that the next window's fill can start as soon as the 3x3 k-loop has read its window
-constexpr int IA = IG == 1 ? 65536 : 153600;
+constexpr int IA = IG == 1 ? 65536 : 153344;
 __host__ __device__ constexpr int ig_brows(int ro) { return (IG * (2 * ro + 1) * (2 * ro + 1) + 15) / 16 * 16; }
 __host__ __device__ constexpr int ig_boff(int ro) { return IA - 256 * ig_brows(ro); }
 constexpr int ICOL = IA;                  // embed im2col [IG][4][16][8] halves
@@ -473,7 +473,7 @@ constexpr int IU = IPC + IG * 2 * 128 * 4;
 constexpr int ITAB = IU + IG * 128;         // row tables of the radius 1..5 passes, then their totals
 __host__ __device__ constexpr int itab_off(int ro) { return ro <= 1 ? 0 : itab_off(ro - 1) + IG * (2 * ro - 1) * (2 * ro - 1); }
 constexpr int ITOT = itab_off(6);            // 855 entries
-constexpr int ILDS = ITAB + (ITOT + 8) * 4;
+constexpr int ILDS = ITAB + (ITOT + 8 + 5 * IG * 8) * 4;
 static_assert(ILDS * IWG <= 160 * 1024 && IG * IWIN_MAX <= IA && ig_boff(5) >= 0, "LDS");
 // the next window vs the rows the 1x1 layer before it reads: map 1, 2 windows clear
 // of B(2), B(3); the map-3 window overlaps B(4) above ig_boff(4) (filled in two parts)
@@ -588,19 +588,27 @@ __device__ __forceinline__ int ig_total(const char* lds, int ro) { return ((cons
 // entry i of radius ro = unit | pr << 2 | pc << 6 | (index in its square) << 10
 __device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng, int tid) {
     int* tab = (int*)(lds + ITAB);
-    for (int e = tid; e < 5 * IG * 121; e += NTI) {
-        const int ro = 1 + e / (IG * 121), i = e - (ro - 1) * IG * 121;
+    int* sqt = tab + ITOT + 8;  // [radius - 1][unit]: r0, c0, h, w, first packed row
+    if (tid < 5) {
+        const int ro = tid + 1;
         int start = 0;
         for (int g = 0; g < ng; g++) {
             const Sq q = square(U[g].cell, ro);
-            const int n = q.h * q.w;
-            if (i >= start && i < start + n) {
-                const int j = i - start, rr = j / q.w;
-                tab[itab_off(ro) + i] = g | (q.r0 + rr) << 2 | (q.c0 + j - rr * q.w) << 6 | j << 10;
-            }
-            start += n;
+            int* e = sqt + ((ro - 1) * IG + g) * 8;
+            e[0] = q.r0, e[1] = q.c0, e[2] = q.h, e[3] = q.w, e[4] = start;
+            start += q.h * q.w;
         }
-        if (i == 0) tab[ITOT + ro] = start;
+        tab[ITOT + ro] = start;
+    }
+    __syncthreads();
+    for (int e = tid; e < 5 * IG * 121; e += NTI) {
+        const int ro = 1 + e / (IG * 121), r = e - (ro - 1) * IG * 121, g = r / 121, j = r - g * 121;
+        if (g >= ng) continue;
+        const int* q = sqt + ((ro - 1) * IG + g) * 8;
+        const int w = q[3];
+        if (j >= q[2] * w) continue;
+        const int rr = (int)(((float)j + 0.5f) / (float)w);  // exact: j < 121, w <= 11
+        tab[itab_off(ro) + q[4] + j] = g | (q[0] + rr) << 2 | (q[1] + j - rr * w) << 6 | j << 10;
     }
 }
 
@@ -1111,9 +1119,9 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
             float v = 0.f;
             if (i < 2 * POS) {
                 const int ch = i >= POS ? 1 : 0, p = i - ch * POS, pr = p / 15, pc = p - (p / 15) * 15;
-                const Sq q = square(u.cell, 5);
-                if (pr >= q.r0 && pr < q.r0 + q.h && pc >= q.c0 && pc < q.c0 + q.w)
-                    v = pcv[(g * 2 + ch) * 128 + (pr - q.r0) * q.w + (pc - q.c0)];
+                const int* q = (const int*)(lds + ITAB) + ITOT + 8 + (4 * IG + g) * 8;  // radius 5
+                if (pr >= q[0] && pr < q[0] + q[2] && pc >= q[1] && pc < q[1] + q[3])
+                    v = pcv[(g * 2 + ch) * 128 + (pr - q[0]) * q[3] + (pc - q[1])];
                 else
                     v = u.pol_src[i];
                 u.pol_job[i] = v;

@@ -970,10 +970,51 @@ __device__ __forceinline__ SibU sib_uniform(const SibUnit& u) {
     return s;
 }
 
+#ifndef SIB_FILL_POS
+#define SIB_FILL_POS 1
+#endif
 template <int MAP, bool GC>
 __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, int ng, int tid) {
     constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P, IT = (PER + NTS - 1) / NTS;
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
+#if SIB_FILL_POS
+    // position-major: work blocks (unit, 64 window positions); a lane works out its
+    // position's source once (root map, own square, parent's square or zero), then its
+    // 32 channel-group planes go by LDS-DMA (for one plane a wave's positions are
+    // contiguous in LDS; at the source the planes are a fixed stride apart)
+    (void)IT;
+    constexpr int NB = (P + 63) / 64;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int blk = wave; blk < ng * NB; blk += NTS / 64) {
+        const int g = blk / NB, b0 = (blk - g * NB) * 64, loc = b0 + lane;
+        const SibU u = sib_uniform(U[u0 + g]);
+        const int dr = loc / Wd - R, dc = loc % Wd - R;
+        const int pr = u.cr + dr, pc = u.cc + dc;
+        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
+        const bool own = on && iabs(dr) <= rc && iabs(dc) <= rc;
+        const _Float16* src = (const _Float16*)gz_sib_zero16;
+        int stride = 0;  // halves between channel-group planes at the source
+        if (on) {
+            src = u.gm + MAP * PV_MAP_HALVES + (pr * BN + pc) * 8;
+            stride = 256 * 8;
+        }
+        if (MAP > 0 && own) {
+            src = u.own + PATCH_OFF[MAP] + ((dr + rc) * S + (dc + rc)) * 8;
+            stride = SS * 8;
+        }
+        if (GC && on && !own && iabs(pr - u.r1) <= rc && iabs(pc - u.c1) <= rc) {
+            src = u.par + PATCH_OFF[MAP] + ((pr - u.r1 + rc) * S + (pc - u.c1 + rc)) * 8;
+            stride = SS * 8;
+        }
+        char* dst = lds + (size_t)g * PER * 16 + (size_t)b0 * 16;  // + lane * 16 by the DMA
+        if (loc < P) {
+#pragma unroll
+            for (int pcg = 0; pcg < 32; pcg++)
+                __builtin_amdgcn_global_load_lds((glb_void_t*)(src + pcg * stride), (lds_void_t*)(dst + pcg * P * 16), 16,
+                                                 0, 0);
+        }
+    }
+#else
     const int wb = tid & ~63;
     for (int g = 0; g < ng; g++) {
         const SibU u = sib_uniform(U[u0 + g]);
@@ -996,6 +1037,7 @@ __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, in
             __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + (size_t)(wb + k * NTS) * 16), 16, 0, 0);
         }
     }
+#endif
 }
 
 // The k-loop of a pass for the wave's n-tiles {nt0, nt0+1} over NT M tiles: win_conv_nt's
