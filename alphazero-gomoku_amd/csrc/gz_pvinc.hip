@@ -861,10 +861,13 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
 // (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
 // those of the full forward.
 #ifndef SIB_WAVES
-#define SIB_WAVES 8
+#define SIB_WAVES 4
 #endif
-// SIB_WAVES 8: two waves per SIMD; waves np and np + 4 own the same n-tile pair and
-// split a pass's M tiles (SIB_MH halves).  4: one wave per SIMD over all M tiles.
+// SIB_WAVES 4 (default): one wave per SIMD over all of a pass's M tiles, each weight
+// fragment read once per pass; 8: two waves per SIMD, waves np and np + 4 own the same
+// n-tile pair and split the M tiles (SIB_MH halves), reading the fragments twice.  With
+// item-major window fills 8 waves were 6 % faster (their VALU address work hid behind
+// the other wave); with position-major fills 4 waves are 1.5 % faster (same box).
 constexpr int NTS = 64 * SIB_WAVES, SIB_MH = SIB_WAVES / 4;
 constexpr int sib_tiles(int t) { return (t + SIB_MH - 1) / SIB_MH; }
 constexpr int SIB_G = 6;

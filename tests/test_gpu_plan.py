@@ -235,3 +235,19 @@ def test_incremental_graphnet_same_games(gnw, monkeypatch):
     off, st_off = run("0")
     assert st_on["incremental"] > 0 and st_off["incremental"] == 0
     assert on == off
+
+
+def test_incremental_graphnet_long_chains_fall_back_bitwise(gnw):
+    """planner_steps 8: chains pass the 6 stones a job can keep squares for, so later
+    plies fall back to the full forward (which then becomes the chain's base); every
+    row still equals the full forward bit for bit."""
+    from gzero.selfplay import SelfPlayEngine
+    eng = SelfPlayEngine(n_slots=32, num_simulations=60, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED + 11,
+                         plies_per_step=1, planner_steps=8, planner_difficulty="medium", gn_weights=gnw)
+    eng.advance(12)
+    eng.gn_stats(reset=True, check=True)
+    for _ in range(2):
+        eng.step()
+    st = eng.gn_stats()
+    assert st["incremental"] > 0 and st["full"] > 0, st
+    assert st["checked"] == st["incremental"] + st["full"] and st["mismatched"] == 0, st
