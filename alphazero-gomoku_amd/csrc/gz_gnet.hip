@@ -272,7 +272,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
 // the records gn_kernel left (heads_gemm_block, gz_f16conv.h).  DQN fc0 on the one-hot
 // planes = base + the (colour - empty) delta rows of the stones (gz_gnet.h): a GEMM
 // with K = 450 over the record's stone inputs.  Wave w: n-tiles {w, w+4, w+8, w+12}.
-constexpr int HB = 64;
+#ifndef GN_HB
+#define GN_HB 32  // boards per workgroup: 32 -> 66 KB of LDS, two workgroups per CU
+#endif
+constexpr int HB = GN_HB;
+constexpr int HMT = HB / 16;  // M tiles (16 boards each)
 constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;   // logits rows
 constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
@@ -283,20 +287,20 @@ static_assert(REC_X == 29 * 16 && REC - REC_X == 29 * 16 && REC % 4 == 0 && REC_
 // to hide the loads behind)
 template <int KB, int NTILES>
 __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lane, const int (&nt)[4], int ntn,
-                                           f32x4 (&acc)[4][4], const float* __restrict__ arow[4]) {
+                                           f32x4 (&acc)[HMT][4], const float* __restrict__ arow[HMT]) {
 #pragma unroll
-    for (int m = 0; m < 4; m++)
+    for (int m = 0; m < HMT; m++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[m][q] = zero4();
     const int g = lane >> 4;
-    auto load = [&](int kb, f32x4 (&a)[4], f32x4 (&b)[4]) {
+    auto load = [&](int kb, f32x4 (&a)[HMT], f32x4 (&b)[4]) {
 #pragma unroll
-        for (int m = 0; m < 4; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
+        for (int m = 0; m < HMT; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
 #pragma unroll
         for (int q = 0; q < 4; q++)
             b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
     };
-    f32x4 a[2][4], b[2][4];
+    f32x4 a[2][HMT], b[2][4];
     load(0, a[0], b[0]);
 #pragma unroll 2
     for (int kb = 0; kb < KB; kb++) {
@@ -305,7 +309,7 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
 #pragma unroll
         for (int t = 0; t < 4; t++)
 #pragma unroll
-            for (int m = 0; m < 4; m++)
+            for (int m = 0; m < HMT; m++)
 #pragma unroll
                 for (int q = 0; q < 4; q++)
                     if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][m][t], b[cur][q][t], acc[m][q], 0, 0, 0);
@@ -314,7 +318,7 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
 
 // acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles
 template <bool RELU>
-__device__ __forceinline__ void heads_put(const f32x4 (&acc)[4][4], const float* __restrict__ bias, int nmax,
+__device__ __forceinline__ void heads_put(const f32x4 (&acc)[HMT][4], const float* __restrict__ bias, int nmax,
                                           const int (&nt)[4], int ntn, int lane, float* dst, int stride) {
     const int li = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -324,7 +328,7 @@ __device__ __forceinline__ void heads_put(const f32x4 (&acc)[4][4], const float*
         if (o >= nmax) continue;
         const float bv = bias[o];
 #pragma unroll
-        for (int m = 0; m < 4; m++)
+        for (int m = 0; m < HMT; m++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = acc[m][q][r] + bv;
@@ -334,7 +338,7 @@ __device__ __forceinline__ void heads_put(const f32x4 (&acc)[4][4], const float*
     }
 }
 
-__global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restrict__ W, const float* __restrict__ rec,
+__global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* __restrict__ W, const float* __restrict__ rec,
                                                            int n, const int32_t* d_count, float* __restrict__ p_out,
                                                            float* __restrict__ q_out, float* __restrict__ logits_out) {
     __shared__ __attribute__((aligned(16))) float ra[HB * H_STRIDE];  // logits, then DQN hidden 2
@@ -350,9 +354,9 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
     const int li = lane & 15, g = lane >> 4;
     // board rows of the lane (row li of each of the 4 board tiles); rows past count
     // re-read the last board and their outputs are dropped
-    const float* arow[4];
+    const float* arow[HMT];
 #pragma unroll
-    for (int m = 0; m < 4; m++) {
+    for (int m = 0; m < HMT; m++) {
         const int b = b0 + 16 * m + li;
         arow[m] = rec + (size_t)(b < count ? b : count - 1) * REC;
     }
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
         nt[q] = wave + 4 * q;
         ntn_p += nt[q] < 15;
     }
-    f32x4 acc[4][4];
+    f32x4 acc[HMT][4];
     // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
     heads_gemm<REC_X / 16, 15>(W + GF_P, lane, nt, ntn_p, acc, arow);
     heads_put<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
@@ -399,23 +403,23 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
     }
     // ---- DQN fc0 (one-hot planes -> 256) + ReLU into rb
     {
-        const float* ax[4];
+        const float* ax[HMT];
 #pragma unroll
-        for (int m = 0; m < 4; m++) ax[m] = arow[m] + REC_X;
+        for (int m = 0; m < HMT; m++) ax[m] = arow[m] + REC_X;
         heads_gemm<(REC - REC_X) / 16, 16>(W + D0_P, lane, nt, 4, acc, ax);
         heads_put<true>(acc, W + D0_BASE, DQH, nt, 4, lane, rb, H_STRIDE);
     }
     __syncthreads();  // rb complete; ra (logits) no longer read
-    const float* ah[4];
+    const float* ah[HMT];
     // ---- fc1 256 -> 256 + ReLU into ra
 #pragma unroll
-    for (int m = 0; m < 4; m++) ah[m] = rb + (16 * m + li) * H_STRIDE;
+    for (int m = 0; m < HMT; m++) ah[m] = rb + (16 * m + li) * H_STRIDE;
     heads_gemm<DQH / 16, 16>(W + D1_P, lane, nt, 4, acc, ah);
     heads_put<true>(acc, W + D1_B, DQH, nt, 4, lane, ra, H_STRIDE);
     __syncthreads();
     // ---- fc2 256 -> 225: q
 #pragma unroll
-    for (int m = 0; m < 4; m++) ah[m] = ra + (16 * m + li) * H_STRIDE;
+    for (int m = 0; m < HMT; m++) ah[m] = ra + (16 * m + li) * H_STRIDE;
     heads_gemm<DQH / 16, 15>(W + D2_P, lane, nt, ntn_p, acc, ah);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(NTH_H, 1) void gn_heads_kernel(const float* __restr
         if (o >= POS) continue;
         const float bv = W[D2_B + o];
 #pragma unroll
-        for (int m = 0; m < 4; m++)
+        for (int m = 0; m < HMT; m++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int b = b0 + 16 * m + 4 * g + r;
