@@ -1286,6 +1286,9 @@ __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const 
 #ifndef SIB_LAG
 #define SIB_LAG 0
 #endif
+#ifndef SIB_SKIP_EARLY
+#define SIB_SKIP_EARLY 0  // 1 (skip inputs loaded before the k-loop): -0.5…-1.3 % same box
+#endif
 __device__ __forceinline__ void sib_lag(int mh) {
     if (SIB_LAG > 0 && mh) __builtin_amdgcn_s_sleep(SIB_LAG);
 }
@@ -1366,14 +1369,11 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    sib_lag(mh);
-    if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
-    st(si);
-    const float* Rw = W + RES0 + LAYER * RES_STRIDE;
-    // x1's skip input (x0) first: every load of the epilogue in flight at once (rows
-    // past the pass's end read a valid position and are dropped)
+    // x1's skip input (x0): every load of the epilogue in flight at once (rows past the
+    // pass's end read a valid position and are dropped); SIB_SKIP_EARLY: issued before
+    // the k-loop, so they have landed when the barrier after it waits for loads
     h4 skh[2][NMAX], skl[2][NMAX];
-    if (SKIP) {
+    auto skip_loads = [&]() {
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
             const MapLoc L = map_loc<0, GC>(U[tp.g[m]], tp.pr[m], tp.pc[m]);
@@ -1385,7 +1385,13 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
                 skl[n][m] = *(const h4*)(p + L.lo);
             }
         }
-    }
+    };
+    if (SKIP && SIB_SKIP_EARLY) skip_loads();
+    sib_lag(mh);
+    if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
+    st(si);
+    const float* Rw = W + RES0 + LAYER * RES_STRIDE;
+    if (SKIP && !SIB_SKIP_EARLY) skip_loads();
     // each row's destination in its node's square, read from the unit table before
     // any store (the stores go through generic pointers the compiler cannot separate
     // from the table)
@@ -1454,23 +1460,27 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
+    // the skip input (x1): every load in flight at once (SIB_SKIP_EARLY: before the k-loop)
+    h4 skh[2][NMAX], skl[2][NMAX];
+    auto skip_loads = [&]() {
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            const MapLoc L = map_loc<2, GC>(u, tp.pr[m], tp.pc[m]);
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
+                const _Float16* p = L.base + (ch0 >> 3) * L.cs + (ch0 & 7);
+                skh[n][m] = *(const h4*)p;
+                skl[n][m] = *(const h4*)(p + L.lo);
+            }
+        }
+    };
+    if (SIB_SKIP_EARLY) skip_loads();
     sib_lag(mh);
     if (nt > 0) sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* R = W + RES0 + layer * RES_STRIDE;
-    // the skip input (x1) first: every load in flight at once
-    h4 skh[2][NMAX], skl[2][NMAX];
-#pragma unroll
-    for (int m = 0; m < NMAX; m++) {
-        const MapLoc L = map_loc<2, GC>(u, tp.pr[m], tp.pc[m]);
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-            const _Float16* p = L.base + (ch0 >> 3) * L.cs + (ch0 & 7);
-            skh[n][m] = *(const h4*)p;
-            skl[n][m] = *(const h4*)(p + L.lo);
-        }
-    }
+    if (!SIB_SKIP_EARLY) skip_loads();
     f32x4 es[2], et[2], e0[2], e1[2], ev[2];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
