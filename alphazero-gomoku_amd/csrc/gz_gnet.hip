@@ -280,6 +280,9 @@ constexpr int HMT = HB / 16;  // M tiles (16 boards each)
 constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;   // logits rows
 constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
+#ifndef GN_HPF
+#define GN_HPF 1  // k-blocks of A/B fragments loaded ahead in heads_gemm (1 or 2)
+#endif
 static_assert(REC_X == 29 * 16 && REC - REC_X == 29 * 16 && REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
 
 // heads_gemm_block's products in its order, with the next k-block's A and B fragments
@@ -300,6 +303,29 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
         for (int q = 0; q < 4; q++)
             b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
     };
+#if GN_HPF == 2
+    // two k-blocks in flight: the block after next is loaded while the current one's
+    // MFMAs run (the buffers rotate by value; the unrolled loop renames them)
+    f32x4 a0[HMT], b0[4], a1[HMT], b1[4];
+    load(0, a0, b0);
+    if (KB > 1) load(1, a1, b1);
+#pragma unroll 3
+    for (int kb = 0; kb < KB; kb++) {
+        f32x4 a2[HMT], b2[4];
+        if (kb + 2 < KB) load(kb + 2, a2, b2);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int m = 0; m < HMT; m++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[m][t], b0[q][t], acc[m][q], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < HMT; m++) a0[m] = a1[m], a1[m] = a2[m];
+#pragma unroll
+        for (int q = 0; q < 4; q++) b0[q] = b1[q], b1[q] = b2[q];
+    }
+#else
     f32x4 a[2][HMT], b[2][4];
     load(0, a[0], b[0]);
 #pragma unroll 2
@@ -314,6 +340,7 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
                 for (int q = 0; q < 4; q++)
                     if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][m][t], b[cur][q][t], acc[m][q], 0, 0, 0);
     }
+#endif
 }
 
 // acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles

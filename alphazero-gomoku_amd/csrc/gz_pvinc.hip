@@ -875,7 +875,12 @@ constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
 static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
 constexpr int SIB_HP = SIB_WIN;                     // head partials [4 pairs][3][HP_ROWS]
 constexpr int SIB_U = SIB_HP + 4 * 3 * HP_ROWS * 4;  // unit table
-constexpr int LDS_S = SIB_U + SIB_G * 128;  // SibUnit: 128 B
+// SIB_NEXT 1: the next chunk's units are built at the end of this chunk's y1 pass and its
+// x0 windows are filled right after this chunk's last x2 k-loop (two unit tables)
+#ifndef SIB_NEXT
+#define SIB_NEXT 0
+#endif
+constexpr int LDS_S = SIB_U + (SIB_NEXT ? 2 : 1) * SIB_G * 128;  // SibUnit: 128 B
 static_assert(LDS_S <= 160 * 1024, "LDS budget");
 
 // phase stamps of pv_sib_kernel (workgroup 0, thread 0; -DGZ_PVINC_STAMPS builds only)
@@ -976,7 +981,15 @@ __device__ __forceinline__ SibU sib_uniform(const SibUnit& u) {
 #ifndef SIB_FILL_POS
 #define SIB_FILL_POS 1
 #endif
-template <int MAP, bool GC>
+// SIB_Y1LDS 1: the y1 epilogue also writes the new y1 squares of the first x1 pass's
+// nodes into their x1 windows in LDS, and the rest of those windows is filled (SKIPOWN:
+// every position but the node's own square) right after the y1 k-loop -- no fill round
+// trip between y1 and x1
+#ifndef SIB_Y1LDS
+#define SIB_Y1LDS 0
+#endif
+static_assert(!SIB_Y1LDS || SIB_FILL_POS, "SIB_Y1LDS needs the position-major fill");
+template <int MAP, bool GC, bool SKIPOWN = false>
 __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, int ng, int tid) {
     constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P, IT = (PER + NTS - 1) / NTS;
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
@@ -1010,7 +1023,7 @@ __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, in
             stride = SS * 8;
         }
         char* dst = lds + (size_t)g * PER * 16 + (size_t)b0 * 16;  // + lane * 16 by the DMA
-        if (loc < P) {
+        if (loc < P && !(SKIPOWN && own)) {
 #pragma unroll
             for (int pcg = 0; pcg < 32; pcg++)
                 __builtin_amdgcn_global_load_lds((glb_void_t*)(src + pcg * stride), (lds_void_t*)(dst + pcg * P * 16), 16,
@@ -1349,7 +1362,7 @@ __device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, i
 // One map layer (LAYER 0 = y1: X0 r3 windows -> y1 r2; 1 = x1: Y1 r4 -> x1 r3, + x0;
 // 2 = y2: X1 r5 -> y2 r4) over units [u0, u0 + ng): the k-loop, then the epilogue into
 // each node's own square (global)
-template <int LAYER, int NMAX, int G, bool GC, class Mid>
+template <int LAYER, int NMAX, int G, bool GC, bool TOLDS = false, class Mid>
 __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
                                               int mh, int lane, int32_t* tiles, SibStamp& st, int si, Mid&& mid) {
     constexpr int R = LAYER + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = R - 1;
@@ -1402,6 +1415,17 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         dst[m] = u.own + PATCH_OFF[MAPOUT] + ((tp.pr[m] - cr + ro) * S + (tp.pc[m] - cc + ro)) * 8;
     }
+    // TOLDS (y1 only): rows of nodes 0..2 also go to their x1 windows (R 4) at LDS 0
+    constexpr int P1 = 81, W1 = 9;
+    int ldst[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        ldst[m] = -1;
+        if (TOLDS && tp.g[m] < 3) {
+            const int cell = U[tp.g[m]].cell, cr = cell / BN, cc = cell - (cell / BN) * BN;
+            ldst[m] = tp.g[m] * 2 * 16 * P1 * 8 + ((tp.pr[m] - cr + 4) * W1 + (tp.pc[m] - cc + 4)) * 8;
+        }
+    }
     f32x4 es[2], et[2];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
@@ -1434,6 +1458,11 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
             _Float16* d = dst[m] + (ch0 >> 3) * SS * 8 + (ch0 & 7);
             sq_store(d, hi);
             sq_store(d + 16 * SS * 8, lo);
+            if (TOLDS && ldst[m] >= 0) {
+                _Float16* l = (_Float16*)lds + ldst[m] + (ch0 >> 3) * P1 * 8 + (ch0 & 7);
+                *(h4*)l = hi;
+                *(h4*)(l + 16 * P1 * 8) = lo;
+            }
         }
     }
 }
@@ -1579,7 +1608,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                                                        const int32_t* __restrict__ list,
                                                        const int32_t* __restrict__ list_count) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_S];
-    SibUnit* U = (SibUnit*)(lds + SIB_U);
+    SibUnit* const U0 = (SibUnit*)(lds + SIB_U);
     float* hpart = (float*)(lds + SIB_HP);
     const int count = *list_count;
     // XCD-aware interleave: XCD x = blockIdx % 8 takes a contiguous eighth of the list
@@ -1597,11 +1626,10 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     const float* W = A.W;
     int32_t* tiles = A.tiles ? A.tiles + (GC ? 1 : 0) : nullptr;
     SibStamp st;
-    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
-        __syncthreads();  // the previous chunk's readers of U are done
-        const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
-        if (wave == 0 && lane < ng) {  // the chunk's nodes
-            const int b = list[pos + lane];
+    // the units of the chunk at pos_ (wave 0, one lane per node)
+    auto build = [&](SibUnit* Ud, int pos_, int ng_) {
+        if (wave == 0 && lane < ng_) {  // the chunk's nodes
+            const int b = list[pos_ + lane];
             SibUnit u;
             const int ci = A.cinfo[b];
             const int o = (ci >> 8) & 0x3fffff;
@@ -1622,10 +1650,25 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 const int ps = A.pslot[b];
                 if (ps >= 0) u.own = A.patches + (size_t)ps * PATCH_HALVES;  // it has grandchildren: its patch
             }
-            U[lane] = u;
+            Ud[lane] = u;
         }
-        __syncthreads();
+    };
+    int cur = 0;
+    bool ready = false;  // this chunk's units are built and its x0 windows are in flight
+    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
+        __syncthreads();  // the previous chunk's readers of U are done
+        const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
+        SibUnit* const U = U0 + cur * SIB_G;
+        if (!ready) {
+            build(U, pos, ng);
+            __syncthreads();
+        }
         st(0);
+        const int posn = pos + per * SIB_G;
+        const bool nxt = SIB_NEXT && posn < xe;
+        const int ngn = nxt ? (xe - posn < SIB_G ? xe - posn : SIB_G) : 0;
+        SibUnit* const Un = U0 + (cur ^ 1) * SIB_G;
+        bool built = false;
 #ifdef GZ_PVINC_STAMPS
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, (unsigned long long)ng);
 #endif
@@ -1657,7 +1700,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
         {
             int t = tid;
             asm volatile("" : "+v"(t));
-            sib_fill<0, GC>(lds, U, 0, ng, t);
+            if (!ready) sib_fill<0, GC>(lds, U, 0, ng, t);
             sib_col((_Float16*)hpart, U, ng, t);
             __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
             st(1);
@@ -1678,6 +1721,8 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 pass_of(p + 1, L2, v0, g2);
                 pre = !(L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2);
             }
+            // y1 -> x1: the first x1 pass's windows come from the y1 epilogue + a SKIPOWN fill
+            const bool y1lds = SIB_Y1LDS && p == 0 && npass > 1;
             const float* Wp = W;
             int t = tid;
             asm volatile("" : "+s"(Wp), "+v"(t));
@@ -1686,13 +1731,15 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 __syncthreads();
                 st(1);
             }
-            filled = pre;
+            filled = pre || y1lds;
             auto mid = [&]() {
                 __syncthreads();  // every wave is past this pass's k-loop: the windows are free
                 if (pre) fill(L2, v0, g2, t);
+                else if (y1lds) sib_fill<1, GC, true>(lds, U, 0, g2, t);
+                else if (p + 1 == npass && built) sib_fill<0, GC>(lds, Un, 0, ngn, t);  // the next chunk's x0
             };
             if (L == 0) {
-                sib_map_layer<0, sib_tiles(10), SIB_G, GC>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
+                sib_map_layer<0, sib_tiles(10), SIB_G, GC, SIB_Y1LDS != 0>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
             } else if (L == 1) {
                 sib_map_layer<1, sib_tiles(10), 3, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 6, mid);
             } else if (L == 2) {
@@ -1711,9 +1758,15 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 st(15);
                 continue;
             }
+            if (nxt && p == 0) {  // wave 0's unit loads drain with the y1 squares' stores
+                build(Un, posn, ngn);
+                built = true;
+            }
             __syncthreads();  // the squares are stored; the next pass's windows have landed
             st(3 * L + 5);
         }
+        if (built) cur ^= 1;
+        ready = built;
     }
 }
 
