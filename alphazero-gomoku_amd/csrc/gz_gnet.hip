@@ -268,10 +268,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
 
 // ============================================================ batched heads
 // policy FC 450->225 + softmax (bg_planner.py:55-56, 243-246) and OpponentDQN
-// (bg_planner.py:68-78) for HB = 64 boards per workgroup as fp32-MFMA GEMMs over
+// (bg_planner.py:68-78) for HB (32) boards per workgroup as fp32-MFMA GEMMs over
 // the records gn_kernel left (heads_gemm_block, gz_f16conv.h).  DQN fc0 on the one-hot
 // planes = base + the (colour - empty) delta rows of the stones (gz_gnet.h): a GEMM
-// with K = 450 over the record's stone inputs.  Wave w: n-tiles {w, w+4, w+8, w+12}.
+// with K = 450 over the record's stone inputs (GN_HSKIP: only the k-blocks holding
+// a stone on one of the workgroup's boards).  Wave w: n-tiles {w, w+4, w+8, w+12}.
 #ifndef GN_HB
 #define GN_HB 32  // boards per workgroup: 32 -> 66 KB of LDS, two workgroups per CU
 #endif
@@ -343,6 +344,54 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
 #endif
 }
 
+// GN_HSKIP 1: DQN fc0 over the k-blocks of the one-hot stone inputs that hold a stone
+// on at least one of the workgroup's boards (mask: bit kb).  A skipped block's
+// products are all zero, and adding them leaves every accumulator bit unchanged (the
+// accumulators start at +0 and never become -0), so the outputs are bitwise those of
+// the dense GEMM
+#ifndef GN_HSKIP
+#define GN_HSKIP 1
+#endif
+template <int NTILES>
+__device__ __forceinline__ void heads_gemm_mask(const float* __restrict__ Wp, int lane, const int (&nt)[4], int ntn,
+                                                f32x4 (&acc)[HMT][4], const float* __restrict__ arow[HMT], uint32_t mask) {
+#pragma unroll
+    for (int m = 0; m < HMT; m++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[m][q] = zero4();
+    const int g = lane >> 4;
+    auto load = [&](int kb, f32x4 (&a)[HMT], f32x4 (&b)[4]) {
+#pragma unroll
+        for (int m = 0; m < HMT; m++) a[m] = *(const f32x4*)(arow[m] + 16 * kb + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
+    };
+    mask = __builtin_amdgcn_readfirstlane(mask);
+    if (!mask) return;
+    f32x4 a0[HMT], b0[4];
+    load(__builtin_ctz(mask), a0, b0);
+    mask &= mask - 1;
+    for (;;) {
+        f32x4 a1[HMT], b1[4];
+        const bool more = mask != 0;
+        if (more) load(__builtin_ctz(mask), a1, b1);  // the next live block while this one's MFMAs run
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int m = 0; m < HMT; m++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[m][t], b0[q][t], acc[m][q], 0, 0, 0);
+        if (!more) break;
+        mask &= mask - 1;
+#pragma unroll
+        for (int m = 0; m < HMT; m++) a0[m] = a1[m];
+#pragma unroll
+        for (int q = 0; q < 4; q++) b0[q] = b1[q];
+    }
+}
+
 // acc + bias (ReLU if RELU) into LDS rows dst[board][n] for the wave's n-tiles
 template <bool RELU>
 __device__ __forceinline__ void heads_put(const f32x4 (&acc)[HMT][4], const float* __restrict__ bias, int nmax,
@@ -395,6 +444,30 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
         ntn_p += nt[q] < 15;
     }
     f32x4 acc[HMT][4];
+#if GN_HSKIP
+    // the fc0 k-blocks with a stone on any of this workgroup's boards (visible after the
+    // barrier that follows the policy FC)
+    __shared__ uint32_t kmask;
+    if (tid == 0) kmask = 0;
+    __syncthreads();
+    {
+        constexpr int KBX = (REC - REC_X) / 16;
+        uint32_t mk = 0;
+        for (int e = tid; e < HB * KBX; e += NTH_H) {
+            const int bb = e / KBX, kb = e - bb * KBX;
+            const int b = b0 + bb < count ? b0 + bb : count - 1;
+            const f32x4* x = (const f32x4*)(rec + (size_t)b * REC + REC_X + 16 * kb);
+            bool nz = false;
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const f32x4 y = x[v];
+                nz |= y[0] != 0.f || y[1] != 0.f || y[2] != 0.f || y[3] != 0.f;
+            }
+            if (nz) mk |= 1u << kb;
+        }
+        if (mk) atomicOr(&kmask, mk);
+    }
+#endif
     // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
     heads_gemm<REC_X / 16, 15>(W + GF_P, lane, nt, ntn_p, acc, arow);
     heads_put<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
@@ -433,7 +506,11 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
         const float* ax[HMT];
 #pragma unroll
         for (int m = 0; m < HMT; m++) ax[m] = arow[m] + REC_X;
+#if GN_HSKIP
+        heads_gemm_mask<16>(W + D0_P, lane, nt, 4, acc, ax, kmask);
+#else
         heads_gemm<(REC - REC_X) / 16, 16>(W + D0_P, lane, nt, 4, acc, ax);
+#endif
         heads_put<true>(acc, W + D0_BASE, DQH, nt, 4, lane, rb, H_STRIDE);
     }
     __syncthreads();  // rb complete; ra (logits) no longer read
