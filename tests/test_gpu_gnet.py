@@ -63,6 +63,31 @@ def test_gnet_vs_torch_random(nets):
     np.testing.assert_allclose(q, qr, rtol=0, atol=1e-4)
 
 
+def test_gnet_sparse_boards_vs_torch(nets):
+    """The batched heads run DQN fc0 only over the one-hot k-blocks that hold a stone
+    on one of a workgroup's 32 boards (GN_HSKIP): whole workgroups of empty boards (no
+    block), single stones in the first / last cell, one colour only, and a workgroup
+    mixing them, against the fp32 torch nets."""
+    from gzero import device
+    _, gsd, dsd, w = nets
+    rng = np.random.default_rng(11)
+    cells = np.zeros((160, 225), np.int8)  # boards 0-31: empty (a workgroup with no block)
+    for i in range(32, 64):  # one stone each, black or white, first and last cells included
+        cells[i, [0, 224, 112, (7 * i) % 225][i % 4]] = 1 + (i % 2)
+    for i in range(64, 96):  # white only, a few stones
+        cells[i, rng.choice(225, size=1 + i % 5, replace=False)] = 2
+    cells[96:128] = 0  # half empty, half sparse black
+    for i in range(112, 128):
+        cells[i, rng.choice(225, size=i % 3 + 1, replace=False)] = 1
+    cells[128:160] = rng.choice(3, size=(32, 225), p=[0.9, 0.05, 0.05])
+    bl, wh = boards.cells_to_words(cells)
+    p, q, lg = device.gn_forward(w, boards.leaf_words(bl, wh))
+    lr, pr, qr = planner_nets.reference_forward(gsd, dsd, boards.planes_from_cells(cells))
+    np.testing.assert_allclose(lg, lr, rtol=0, atol=1e-4)
+    np.testing.assert_allclose(p, pr, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(q, qr, rtol=0, atol=1e-4)
+
+
 GN_TAG = np.dtype([("mode", "<i4"), ("base", "<i4"), ("job", "<i4"), ("cell", "<i4"), ("nst", "<i4"),
                    ("st", "u1", (6,)), ("pad", "u1", (2,)), ("pad2", "<i4")])
 
