@@ -104,6 +104,8 @@ class AlphaZeroGomokuAI:
         board with ``game_id = game_ids[i]``."""
         t0 = time.time()
         out = [None] * len(boards)
+        # per board: the search's (predicts, main_draws, sim_draws); None if no search ran
+        self.last_batch_stats = [None] * len(boards)
         groups = {}  # openings (< 6 plies) draw no simulation; the rest search
         for i, b in enumerate(boards):
             if b.get_valid_moves():
@@ -129,6 +131,8 @@ class AlphaZeroGomokuAI:
             for k, i in enumerate(idx):
                 m = int(mv[k])
                 out[i] = None if m < 0 else (m // 15, m % 15)
+                self.last_batch_stats[i] = (int(stats[k]["predicts"]), int(stats[k]["main_draws"]),
+                                            int(stats[k]["sim_draws"]))
             self.last_search_stats = stats[-1]
         self._last_decision_time = time.time() - t0
         self.games_played += len(boards)

@@ -500,7 +500,12 @@ struct SlotHeader {  // 128 bytes
     int32_t player;
     int32_t pad0, pad1;
     int64_t games_done;
-    int64_t pad2[3];
+    // RNG draws of every search this slot ran since init (main stream, simulation
+    // streams): the checker compares them with the oracle's per-ply counts
+    // (gz_selfplay_draws), which sees rollout and planner decisions a game's moves hide
+    int64_t main_draws;
+    int64_t sim_draws;
+    int64_t pad2;
 };
 static_assert(sizeof(SlotHeader) == 128, "slot header");
 
@@ -520,6 +525,7 @@ __global__ void selfplay_init_kernel(char* slots, int n_slots, int64_t base, int
     h->player = 1;
     h->pad0 = h->pad1 = 0;
     h->games_done = 0;
+    h->main_draws = h->sim_draws = h->pad2 = 0;
 }
 
 // training.play_one_game (training.py:141-218) for one slot, n_plies plies,
@@ -543,7 +549,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
     }
     int64_t game_id = h->game_id;
     const int64_t gstride = h->game_id_stride;
-    long long games = 0, moves_played = 0, mcts_played = 0;
+    long long games = 0, moves_played = 0, mcts_played = 0, dmain = 0, dsim = 0;
     Tree t = tree_at(smem, p.num_simulations);
     __syncthreads();
     for (int it = 0; it < n_plies; it++) {
@@ -551,6 +557,8 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         int mv = search_move(&rs, game_id, p, t, sink, gather != 0, grid, so);
         __syncthreads();
         if (mv < 0) break;  // unreachable: live games always have an empty cell
+        dmain += so.main_draws;
+        dsim += so.sim_draws;
         const int n_moves = rs.n_moves, player = rs.player;
         const int bit = cell_to_bit(mv);
         const bool win = bb_test(lds_bb(rs.W), bit);  // rs.W = winning cells of the mover
@@ -610,6 +618,8 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         h->n_moves = rs.n_moves;
         h->player = rs.player;
         h->games_done += games;
+        h->main_draws += dmain;
+        h->sim_draws += dsim;
         atomicAdd((unsigned long long*)&ctr->moves, (unsigned long long)moves_played);
         atomicAdd((unsigned long long*)&ctr->games, (unsigned long long)games);
         atomicAdd((unsigned long long*)&ctr->mcts_moves, (unsigned long long)mcts_played);
@@ -619,8 +629,8 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
 // The move-application half of selfplay_kernel for searches run elsewhere
 // (gz_plan_search): record, make_move, finish / restart (training.py:141-218).
 __global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int n_slots, const int32_t* moves,
-                                                              gz_record* records, int rec_cap,
-                                                              gz_selfplay_counters* ctr) {
+                                                              const gz_search_stats* stats, gz_record* records,
+                                                              int rec_cap, gz_selfplay_counters* ctr) {
     const int s = blockIdx.x;
     if (s >= n_slots) return;
     const int lane = lane_id();
@@ -681,6 +691,8 @@ __global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int 
         h->n_moves = over ? 0 : n_moves + 1;
         h->player = over ? 1 : 3 - player;
         h->games_done += games;
+        h->main_draws += stats[s].main_draws;
+        h->sim_draws += stats[s].sim_draws;
         atomicAdd((unsigned long long*)&ctr->moves, 1ull);
         if (n_moves >= 6) atomicAdd((unsigned long long*)&ctr->mcts_moves, 1ull);
         if (games) atomicAdd((unsigned long long*)&ctr->games, 1ull);
@@ -939,7 +951,8 @@ size_t gz_selfplay_plan_workspace_bytes(int32_t n_slots, int32_t num_simulations
     size_t a = ((size_t)n_slots * sizeof(gz_board_state) + 255) & ~(size_t)255;
     size_t b = ((size_t)n_slots * 8 + 255) & ~(size_t)255;
     size_t c = ((size_t)n_slots * 4 + 255) & ~(size_t)255;
-    return a + b + c + gz_plan_workspace_bytes(n_slots, num_simulations);
+    size_t d = ((size_t)n_slots * sizeof(gz_search_stats) + 255) & ~(size_t)255;
+    return a + b + c + d + gz_plan_workspace_bytes(n_slots, num_simulations);
 }
 
 // gz_plan_search with leaf tags (gz_plan.hip)
@@ -965,17 +978,19 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
     ws += ((size_t)n_slots * 8 + 255) & ~(size_t)255;
     int32_t* d_moves = (int32_t*)ws;
     ws += ((size_t)n_slots * 4 + 255) & ~(size_t)255;
+    gz_search_stats* d_stats = (gz_search_stats*)ws;
+    ws += ((size_t)n_slots * sizeof(gz_search_stats) + 255) & ~(size_t)255;
     hipStream_t st = as_stream(stream);
     for (int it = 0; it < n_plies; it++) {
         selfplay_boards_kernel<<<(n_slots + 255) / 256, 256, 0, st>>>((const char*)d_slots, n_slots, d_boards, d_gids);
         int rc = check_launch("selfplay_boards_kernel");
         if (rc) return rc;
-        rc = gz_internal_plan_search(d_boards, d_gids, n_slots, p, pp, d_gn_weights, ws, nullptr, d_moves, nullptr,
+        rc = gz_internal_plan_search(d_boards, d_gids, n_slots, p, pp, d_gn_weights, ws, nullptr, d_moves, d_stats,
                                      gather ? d_leaves : nullptr, leaf_cap, gather ? &d_counters->leaves : nullptr,
                                      gather ? d_leaf_meta : nullptr, stream);
         if (rc) return rc;
-        selfplay_commit_kernel<<<n_slots, WAVE, 0, st>>>((char*)d_slots, n_slots, d_moves, d_records, record_cap,
-                                                         d_counters);
+        selfplay_commit_kernel<<<n_slots, WAVE, 0, st>>>((char*)d_slots, n_slots, d_moves, d_stats, d_records,
+                                                         record_cap, d_counters);
         rc = check_launch("selfplay_commit_kernel");
         if (rc) return rc;
     }
@@ -991,7 +1006,22 @@ int gz_selfplay_plan_gn_stats(void* d_workspace, int32_t n_slots, int32_t num_si
     ws += ((size_t)n_slots * sizeof(gz_board_state) + 255) & ~(size_t)255;
     ws += ((size_t)n_slots * 8 + 255) & ~(size_t)255;
     ws += ((size_t)n_slots * 4 + 255) & ~(size_t)255;
+    ws += ((size_t)n_slots * sizeof(gz_search_stats) + 255) & ~(size_t)255;
     return gz_plan_gn_stats(ws, n_slots, num_simulations, out, reset, stream);
+}
+
+__global__ void selfplay_draws_kernel(const char* slots, int n_slots, int64_t* out) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots) return;
+    const SlotHeader* h = (const SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
+    out[2 * s] = h->main_draws;
+    out[2 * s + 1] = h->sim_draws;
+}
+
+int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream) {
+    if (!d_slots || n_slots <= 0 || !d_out) return fail(GZ_ERR_ARG, "gz_selfplay_draws: bad arguments");
+    selfplay_draws_kernel<<<(n_slots + 255) / 256, 256, 0, as_stream(stream)>>>((const char*)d_slots, n_slots, d_out);
+    return check_launch("selfplay_draws_kernel");
 }
 
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations, gz_board_state* d_out,

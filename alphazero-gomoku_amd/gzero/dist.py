@@ -154,21 +154,29 @@ class RecordExchange:
 
 class ReplayCollector:
     """Every rank's copy of one self-play iteration's replay, built on the device from
-    the per-step RecordExchange chunks (no host synchronisation per chunk).
+    the per-step RecordExchange chunks.  ``absorb`` itself never synchronises; its
+    caller decides when to read ``games`` (training.selfplay_device reads it once per
+    step, in the same device-to-host copy as the engine's counters and the loss
+    counters).
 
     ``absorb`` appends the rows of all ranks whose game id lies in [id_lo, id_hi) --
     the iteration's games; the engines' continuous refill plays on past them and
     those rows are dropped -- to a device buffer and counts the finished games (one
-    ply-0 row per game).  Every rank absorbs the same chunks, so every rank's buffer,
-    count and finish decision agree without another collective.  ``records`` sorts
-    the rows by (game id, ply): the union of the ranks' games in id order, which is
-    the order the reference's replay has (training.py:377-395: games in play order,
-    each game's plies in order)."""
+    ply-0 row per game).  With ``per_rank`` = G, a row sent by rank r is kept only
+    if its id lies in rank r's own share [id_lo + r G, id_lo + (r + 1) G): an
+    engine refills a slot with id + n_slots, so rank r's refill games carry rank
+    r + 1's ids (the same games, replayed from the same id-keyed RNG streams) and
+    must not be counted twice.  Every rank absorbs the same chunks, so every rank's
+    buffer, count and finish decision agree without another collective.
+    ``records`` sorts the rows by (game id, ply): the union of the ranks' games in
+    id order, which is the order the reference's replay has (training.py:377-395:
+    games in play order, each game's plies in order)."""
 
-    def __init__(self, capacity, id_lo, id_hi, device):
+    def __init__(self, capacity, id_lo, id_hi, device, per_rank=None):
         self.item = RECORD_DTYPE.itemsize
         self.cap = int(capacity)
         self.id_lo, self.id_hi = int(id_lo), int(id_hi)
+        self.per_rank = int(per_rank) if per_rank else None
         dev = torch.device(device)
         self.buf = torch.zeros((self.cap + 1, self.item), dtype=torch.uint8, device=dev)  # row cap = dummy
         self.n = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -181,7 +189,12 @@ class ReplayCollector:
         gid = rows[:, 64:72].contiguous().view(torch.int64).reshape(-1)
         ply = rows[:, 72:74].contiguous().view(torch.int16).reshape(-1)
         valid = (torch.arange(chunk, device=recv.device)[None, :] < counts[:, None]).reshape(-1)
-        keep = valid & (gid >= self.id_lo) & (gid < self.id_hi)
+        if self.per_rank:
+            lo = self.id_lo + self.per_rank * torch.arange(ws, device=recv.device, dtype=torch.int64)
+            lo = lo.repeat_interleave(chunk)
+            keep = valid & (gid >= lo) & (gid < torch.clamp(lo + self.per_rank, max=self.id_hi))
+        else:
+            keep = valid & (gid >= self.id_lo) & (gid < self.id_hi)
         k = keep.to(torch.int64)
         pos = self.n + torch.cumsum(k, 0) - 1
         ok = keep & (pos < self.cap)

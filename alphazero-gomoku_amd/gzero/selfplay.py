@@ -194,6 +194,15 @@ class SelfPlayEngine:
         return np.frombuffer(out.cpu().numpy().tobytes(), STATE_DTYPE), gids.cpu().numpy()
 
 
+    def draws(self):
+        """int64 [n_slots, 2]: (main-stream, simulation-stream) RNG draws of every
+        search each slot ran since the engine was created (gz_selfplay_draws)."""
+        out = torch.zeros(self.n_slots * 2, dtype=torch.int64, device="cuda")
+        _lib.check(self.lib.gz_selfplay_draws(ptr(self.d_slots), self.n_slots, ptr(out), stream()),
+                   "gz_selfplay_draws")
+        return out.cpu().numpy().reshape(self.n_slots, 2)
+
+
 def records_to_games(recs):
     """Group records by game id -> {game_id: dict(moves, players, z, cells)} (ply order)."""
     out = {}

@@ -224,9 +224,14 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
     [game_id_base, game_id_base + n_games) as ``selfplay`` does, and each step's
     finished games go through the sync-free RecordExchange (one all-gather per step,
     RCCL) into a ReplayCollector, so every rank ends with the rows of ALL ranks'
-    games in [id_lo, id_hi), sorted by (game id, ply), on the device.  The loop ends
-    when every one of those games has arrived (the count every rank computes from
-    the same chunks, so the ranks stop together).
+    games in [id_lo, id_hi), sorted by (game id, ply), on the device -- each game
+    once: rank r's rows count only for rank r's own ids (its slots' refill games
+    carry rank r + 1's ids).  One host synchronisation per step reads the played
+    moves, the finished-game count and every loss counter (exchange overflow,
+    collector drops, engine record drops: any of them raises at once).  The loop
+    ends when every one of those games has arrived (the count every rank computes
+    from the same chunks, so the ranks stop together), or raises after a bound on
+    the steps the games can take.
     Returns (device uint8 rows [n, 80], n, stats)."""
     from gzero import dist as gdist
     from gzero.selfplay import SelfPlayEngine
@@ -250,17 +255,32 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
     # outbox in one or a few steps even when many games end together
     ex = gdist.RecordExchange(eng.record_cap, max(2 * eng.n_slots * eng.plies_per_step, eng.record_cap // 4), "cuda")
     want = id_hi - id_lo
-    col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda")
+    if want != ws * n_games or not id_lo <= game_id_base < id_hi:
+        raise ValueError("selfplay_device: [id_lo, id_hi) must be the ranks' n_games-wide shares")
+    # rank r keeps only its own share from rank r's rows: its slots' refill games
+    # (id + n_slots) run into rank r + 1's ids
+    col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda", per_rank=n_games)
     moves = steps = 0
+    # a slot plays ceil(n_games / slots) games of <= 200 plies: past that bound a
+    # lost ply-0 row would otherwise keep every rank stepping forever
+    max_steps = (-(-n_games // slots) + 1) * 200 // eng.plies_per_step + 8
     t0 = time.time()
     while True:
         eng.step()
         ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
         col.absorb(*ex.exchange())
-        moves += int(eng.counters()["moves"])
         steps += 1
-        if int(col.games.item()) >= want:  # every game's first record is in
+        # the step's one host synchronisation: moves, finished games and every loss counter
+        c = torch.cat([eng.d_counters.view(torch.int64)[2:3], col.games, ex.overflow, col.dropped,
+                       eng.d_counters[0:4].view(torch.int32)[2:3].to(torch.int64)]).cpu().tolist()
+        moves += int(c[0])
+        if c[2] or c[3] or c[4]:
+            raise RuntimeError(f"selfplay_device: records lost (exchange overflow {c[2]}, collector {c[3]}, "
+                               f"engine buffer {c[4]})")
+        if c[1] >= want:  # every game's first record is in
             break
+        if steps >= max_steps:
+            raise RuntimeError(f"selfplay_device: {c[1]} of {want} games after {steps} steps")
     # drain: the outboxes may still hold later plies of those games; an exchange in
     # which every rank sent nothing means every outbox is empty (all ranks see the
     # same counts, so they stop together)
@@ -338,6 +358,7 @@ def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficul
     color_a = [GomokuBoard.BLACK if (g % 2 == 0 or not alternate) else GomokuBoard.WHITE for g in range(games)]
     active = list(range(games))
     moves = [[] for _ in range(games)]
+    plies = [[] for _ in range(games)]  # per move: the search's (predicts, main_draws, sim_draws)
     while active:
         groups = {}
         for g in active:
@@ -349,21 +370,25 @@ def evaluate_model(current, baseline, device=None, games: int = 8, eval_difficul
             agent = (ai_a if who == "a" else ai_b)[cp]
             if isinstance(agent, RandomAgent):
                 mv = [RandomAgent(agent.seed, gid[g]).get_move(boards[g]) for g in gs]
+                st = [None] * len(gs)
             else:
                 mv = agent.get_moves([boards[g] for g in gs], [gid[g] for g in gs])
-            for g, m in zip(gs, mv):
+                st = agent.last_batch_stats
+            for g, m, s in zip(gs, mv, st):
                 if m is None:
                     stopped.add(g)
                     continue
                 boards[g].make_move(*m)
                 moves[g].append(m[0] * 15 + m[1])
+                plies[g].append(s)
         active = [g for g in active if g not in stopped and not boards[g].game_over]
     wins = sum(1 for g in range(games) if boards[g].winner is not None and boards[g].winner == color_a[g])
     draws = sum(1 for g in range(games) if boards[g].winner is None)
     losses = games - wins - draws
     out = {"wins": wins, "losses": losses, "draws": draws, "win_rate": wins / max(1, games)}
     if return_games:
-        out["games"] = [{"moves": moves[g], "winner": boards[g].winner, "color_a": color_a[g]} for g in range(games)]
+        out["games"] = [{"moves": moves[g], "winner": boards[g].winner, "color_a": color_a[g], "plies": plies[g]}
+                        for g in range(games)]
         out["seeds"] = (seed_a, seed_b)
     return out
 

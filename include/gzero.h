@@ -158,6 +158,10 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
                          const float* d_gn_weights, void* d_workspace, int32_t n_plies, gz_record* d_records,
                          int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_meta,
                          gz_selfplay_counters* d_counters, void* stream);
+/* per slot, the RNG draws of every search it ran since gz_selfplay_init:
+ * d_out[2s] = main-stream draws, d_out[2s+1] = simulation-stream draws (the
+ * checker's view of rollout / planner decisions, ai_agent.py:168-285) */
+int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream);
 /* current board of every slot (for inspection / tests) */
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations,
                        gz_board_state* d_out, int64_t* d_game_ids, void* stream);

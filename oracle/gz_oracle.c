@@ -494,6 +494,28 @@ void or_gnet_forward(const float* blob, const or_board* b, float* logits, float*
     free(g);
 }
 
+/* Test-side trace (NULL = off): every planner move made inside a rollout, and
+   per played ply of or_play_game the search's (predicts, main_draws, sim_draws).
+   Lets the checker compare decisions that never show in a game's moves. */
+static int32_t* g_tr_mv;
+static int g_tr_mv_cap, g_tr_mv_n;
+static int64_t* g_tr_ply;
+static int g_tr_ply_cap, g_tr_ply_n;
+
+void or_trace_set(int32_t* planner_moves, int mv_cap, int64_t* ply_stats, int ply_cap) {
+    g_tr_mv = planner_moves;
+    g_tr_mv_cap = mv_cap;
+    g_tr_mv_n = 0;
+    g_tr_ply = ply_stats;
+    g_tr_ply_cap = ply_cap;
+    g_tr_ply_n = 0;
+}
+
+void or_trace_counts(int* n_moves, int* n_plies) {
+    *n_moves = g_tr_mv_n;
+    *n_plies = g_tr_ply_n;
+}
+
 /* _simulate, ai_agent.py:251-285: planner plies first, then the offensive policy */
 double or_rollout_planner(const or_board* start, int ai, const or_params* p, int64_t game_id, int32_t sim,
                           uint64_t key, uint64_t* draws, or_board* final_out) {
@@ -503,9 +525,16 @@ double or_rollout_planner(const or_board* start, int ai, const or_params* p, int
         int tmp[CELLS];
         float pv[CELLS], qv[CELLS];
         while (!b.over && steps < p->planner_steps) {
+            /* NaN until filled: a callback that fails to write its outputs can never
+               pass for valid net values (oracle.py re-raises its exception) */
+            for (int i = 0; i < CELLS; i++) pv[i] = qv[i] = NAN;
             if (p->pq) p->pq(p->pq_ctx, &b, game_id, sim, steps, pv, qv);
             else or_gnet_forward(p->gn_blob, &b, NULL, pv, qv);
             int mv = or_planner_move(&b, ai, &p->planner, pv, qv, key, draws);
+            if (g_tr_mv) {
+                if (g_tr_mv_n < g_tr_mv_cap) g_tr_mv[g_tr_mv_n] = mv;
+                g_tr_mv_n++;
+            }
             if (mv < 0) break;
             or_make_move(&b, mv / N, mv % N);
             steps++;
@@ -712,6 +741,14 @@ int or_play_game(const or_params* black, const or_params* white, int64_t game_id
         const or_params* p = (pl == 1) ? black : white;
         int mv = or_get_move(&b, pl, p, game_id, &info);
         pred += info.predicts;
+        if (g_tr_ply) {
+            if (g_tr_ply_n < g_tr_ply_cap) {
+                g_tr_ply[3 * g_tr_ply_n] = info.predicts;
+                g_tr_ply[3 * g_tr_ply_n + 1] = info.main_draws;
+                g_tr_ply[3 * g_tr_ply_n + 2] = info.sim_draws;
+            }
+            g_tr_ply_n++;
+        }
         if (mv < 0) break;
         if (n < cap) {
             if (cells_out) memcpy(cells_out + (size_t)n * CELLS, b.cell, CELLS);

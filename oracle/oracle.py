@@ -115,8 +115,36 @@ def lib():
         L.or_play_game.argtypes = [P(Params), P(Params), ctypes.c_int64, P(ctypes.c_int8),
                                    P(ctypes.c_int32), P(ctypes.c_int8), P(ctypes.c_int8), ctypes.c_int,
                                    P(ctypes.c_int), P(ctypes.c_int64), ctypes.c_int]
+        L.or_trace_set.argtypes = [P(ctypes.c_int32), ctypes.c_int, P(ctypes.c_int64), ctypes.c_int]
+        L.or_trace_counts.argtypes = [P(ctypes.c_int), P(ctypes.c_int)]
         _lib = L
     return _lib
+
+
+class Trace:
+    """Context manager recording, for the C calls made inside it, every planner
+    move chosen in a rollout (``.planner_moves``) and per played ply of
+    ``play_game`` the search's (predicts, main_draws, sim_draws) (``.plies``)."""
+
+    def __init__(self, cap=1 << 20):
+        self.cap = cap
+        self._mv = (ctypes.c_int32 * cap)()
+        self._ply = (ctypes.c_int64 * (3 * cap))()
+        self.planner_moves, self.plies = [], []
+
+    def __enter__(self):
+        lib().or_trace_set(self._mv, self.cap, self._ply, self.cap)
+        return self
+
+    def __exit__(self, *exc):
+        nm, npl = ctypes.c_int(0), ctypes.c_int(0)
+        lib().or_trace_counts(ctypes.byref(nm), ctypes.byref(npl))
+        lib().or_trace_set(None, 0, None, 0)
+        if nm.value > self.cap or npl.value > self.cap:
+            raise RuntimeError("oracle trace overflow")
+        self.planner_moves = list(self._mv[: nm.value])
+        self.plies = [tuple(self._ply[3 * i: 3 * i + 3]) for i in range(npl.value)]
+        return False
 
 
 def new_board(moves=()):
@@ -140,14 +168,40 @@ def make_params(difficulty="medium", sims=None, beta=0.2, seed=0, max_depth=100,
         arr = np.ascontiguousarray(gn_blob, np.float32)
         prm._gn_keep = arr
         prm.gn_blob = arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    prm._pq_err = []
     if pq is not None:
         def cb(ctx, bptr, game_id, sim, step, pp, qq):
-            pv, qv = pq(bptr.contents, game_id, sim, step)
-            ctypes.memmove(pp, np.ascontiguousarray(pv, np.float32).ctypes.data, 225 * 4)
-            ctypes.memmove(qq, np.ascontiguousarray(qv, np.float32).ctypes.data, 225 * 4)
+            # ctypes prints and swallows an exception raised inside a callback; keep
+            # the first one and re-raise it once the C call returns (_reraise), so a
+            # failing pq can never let a test pass (the C side leaves pp/qq at NaN)
+            if prm._pq_err:
+                return
+            try:
+                pv, qv = pq(bptr.contents, game_id, sim, step)
+                pv = np.ascontiguousarray(pv, np.float32).reshape(-1)
+                qv = np.ascontiguousarray(qv, np.float32).reshape(-1)
+                if pv.size != CELLS or qv.size != CELLS:
+                    raise ValueError(f"pq returned {pv.size}/{qv.size} values, want {CELLS}")
+                ctypes.memmove(pp, pv.ctypes.data, CELLS * 4)
+                ctypes.memmove(qq, qv.ctypes.data, CELLS * 4)
+            except BaseException as e:  # noqa: BLE001 -- re-raised by _reraise
+                prm._pq_err.append(e)
         prm._pq_keep = PQ_FN(cb)
         prm.pq = prm._pq_keep
     return prm
+
+
+class CallbackError(RuntimeError):
+    """A pq callback raised inside a C oracle call."""
+
+
+def _reraise(*params):
+    for prm in params:
+        errs = getattr(prm, "_pq_err", None)
+        if errs:
+            e = errs[0]
+            errs.clear()
+            raise CallbackError(f"pq callback failed: {e!r}") from e
 
 
 def planner_params(difficulty):
@@ -195,6 +249,7 @@ def rollout_planner(b, ai_player, params, game_id, sim, key):
     fb = Board()
     v = lib().or_rollout_planner(ctypes.byref(b), ai_player, ctypes.byref(params), game_id, sim, key,
                                  ctypes.byref(d), ctypes.byref(fb))
+    _reraise(params)
     return v, d.value, fb
 
 
@@ -224,6 +279,7 @@ def get_move(b, ai_player, params, game_id, cap=4096):
     val = (ctypes.c_double * cap)()
     info = TreeInfo(0, 0, 0, 0, par, mv, vis, val, cap)
     m = lib().or_get_move(ctypes.byref(b), ai_player, ctypes.byref(params), game_id, ctypes.byref(info))
+    _reraise(params)
     n = min(info.n_nodes, cap)
     tree = {"parent": list(par[:n]), "move": list(mv[:n]), "visits": list(vis[:n]),
             "value": list(val[:n]), "predicts": info.predicts, "main_draws": info.main_draws,
@@ -240,6 +296,7 @@ def play_game(black, white, game_id, cap=256, want_cells=False, max_plies=0):
     pred = ctypes.c_int64(0)
     n = lib().or_play_game(ctypes.byref(black), ctypes.byref(white), game_id, cells, moves, players, z,
                            cap, ctypes.byref(winner), ctypes.byref(pred), int(max_plies))
+    _reraise(black, white)
     out = {"n": n, "moves": list(moves[:n]), "players": list(players[:n]), "z": list(z[:n]),
            "winner": winner.value, "predicts": pred.value}
     if want_cells:

@@ -136,10 +136,18 @@ G_PER_RANK = 5
 
 def _games_of(rank):
     """(game id, plies) this rank's engine finishes, in finishing order: its 5 games
-    of the iteration (ids 10 + 5 rank + i, iteration base 10) and refill games past 20."""
+    of the iteration (ids 10 + 5 rank + i, iteration base 10), then its slots'
+    refill games, which follow the engine's real stride (id + n_slots, n_slots = 5):
+    rank 0's refills carry rank 1's ids 15..19 -- other plies, other moves, never to
+    be collected -- and rank 1's run past 20."""
     rng = np.random.default_rng(rank)
-    ids = list(10 + G_PER_RANK * rank + rng.permutation(G_PER_RANK)) + [20 + 2 * k + rank for k in range(6)]
-    return [(int(g), int(rng.integers(1, 30))) for g in ids]
+    own = list(10 + G_PER_RANK * rank + rng.permutation(G_PER_RANK))
+    refill = [10 + G_PER_RANK * (rank + 1) + k for k in range(G_PER_RANK)] + [30 + rank]
+    return [(int(g), int(rng.integers(1, 30))) for g in own + refill]
+
+
+def _move_of(rank, gid, ply):
+    return (gid * 7 + ply + 100 * (gid // G_PER_RANK - 2 != rank)) % 225
 
 
 def _collector_worker(rank, ws, port, q):
@@ -149,7 +157,7 @@ def _collector_worker(rank, ws, port, q):
     games = _games_of(rank)
     cap = 64
     ex = RecordExchange(cap, 8, "cpu", capacity=4096)  # chunk < a game: its plies span exchanges
-    col = ReplayCollector(ws * G_PER_RANK * 225, 10, 10 + ws * G_PER_RANK, "cpu")
+    col = ReplayCollector(ws * G_PER_RANK * 225, 10, 10 + ws * G_PER_RANK, "cpu", per_rank=G_PER_RANK)
     k = steps = 0
     while True:
         rows = []
@@ -159,7 +167,7 @@ def _collector_worker(rank, ws, port, q):
                 k += 1
                 r = np.zeros(plies, boards.RECORD_DTYPE)
                 r["game_id"], r["ply"] = gid, np.arange(plies)[::-1]  # plies in any order
-                r["move"] = (gid * 7 + np.arange(plies)[::-1]) % 225
+                r["move"] = [_move_of(rank, gid, p) for p in np.arange(plies)[::-1]]
                 rows.append(r)
         rec = np.concatenate(rows) if rows else np.zeros(0, boards.RECORD_DTYPE)
         buf = np.zeros(cap, boards.RECORD_DTYPE)
@@ -196,11 +204,14 @@ def test_replay_collector_world2_is_the_union_of_the_ranks_games():
     want = []
     for r in range(2):
         for gid, plies in _games_of(r):
-            if 10 <= gid < 20:
-                want += [(gid, p, (gid * 7 + p) % 225) for p in range(plies)]
+            if 10 + G_PER_RANK * r <= gid < 10 + G_PER_RANK * (r + 1):  # the rank's own share
+                want += [(gid, p, _move_of(r, gid, p)) for p in range(plies)]
     want.sort()
     g = got[0]
     assert [(int(a), int(b), int(c)) for a, b, c in zip(g["game_id"], g["ply"], g["move"])] == want
+    # every game exactly once: one ply-0 row per id, no (id, ply) twice
+    assert len(set(zip(g["game_id"].tolist(), g["ply"].tolist()))) == len(g)
+    assert sorted(g["game_id"][g["ply"] == 0].tolist()) == list(range(10, 20))
 
 
 # training.main under world size 2: rank 0 alone runs the arena (which draws from

@@ -7,6 +7,7 @@ reference's fixtures by test_gpu_api / test_gpu_plan) with per-game AIs of the
 same seeds and ``game_id = g`` -- which pins the batching: grouping, stream
 keys, colours, simulation counts and the draw / stop rules.
 """
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -103,7 +104,13 @@ def test_arena_with_planner_vs_oracle(monkeypatch, oracle):
     training.py:223) on the fixture's settings (tests/golden arena_plans.json.gz:
     planner nets of the fixture seeds, easy simulations lowered, one seed, game ids
     base + g): every batched GPU game equals the oracle's game driven by the GPU's own
-    planner-net outputs (gz_gn_forward), move for move.  With
+    planner-net outputs (gz_gn_forward), move for move, AND every ply's search
+    statistics -- predict count, main-stream draws and the draws summed over the
+    simulations' streams -- equal the oracle's.  At 3-4 simulations the moves
+    alone cannot see the planner (every root child gets one visit); the rollouts'
+    draw counts can: each planner ply draws, and a different planner move changes
+    the rollout that follows it.  A pq callback that fails raises (oracle wrapper).
+    With
     test_oracle_planner.test_arena_with_planner_exact_on_reference_outputs (the oracle
     on the reference's recorded outputs = the reference's games) this pins the
     planner-steered arena to the reference's evaluate_model; the games whose moves
@@ -142,7 +149,7 @@ def test_arena_with_planner_vs_oracle(monkeypatch, oracle):
         return p[0], q[0]
 
     cur, base = GomokuModel(device="cpu"), GomokuModel(device="cpu")
-    differ = 0
+    differ = planner_draws = 0
     for c in g["cases"]:
         res = evaluate_model(cur, base, games=c["games"], eval_difficulty="easy", eval_num_sim=c["eval_num_sim"],
                              eval_plans=2, seeds=(g["seed"], g["seed"]), game_id_base=c["game_id_base"],
@@ -151,9 +158,15 @@ def test_arena_with_planner_vs_oracle(monkeypatch, oracle):
         bp = oracle.make_params("easy", sims=c["eval_num_sim"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
         for k, got in enumerate(res["games"]):
             black, white = (cp, bp) if k % 2 == 0 else (bp, cp)
-            ref = oracle.play_game(black, white, c["game_id_base"] + k)
+            with oracle.Trace() as tr:
+                ref = oracle.play_game(black, white, c["game_id_base"] + k)
             assert got["moves"] == ref["moves"], (c["game_id_base"], k)
             assert got["winner"] == (ref["winner"] or None)
+            assert len(got["plies"]) == len(tr.plies)
+            for ply, (a, b) in enumerate(zip(got["plies"], tr.plies)):
+                assert a == b, (c["game_id_base"], k, ply, a, b)
+            planner_draws += sum(b[2] for b in tr.plies)
             differ += got["moves"] != c["boards"][k]["moves"]
+    assert planner_draws > 0
     print(f"planner-on arena: {differ} of {sum(c['games'] for c in g['cases'])} games differ from the "
-          "reference's own (net near-ties)")
+          f"reference's own (net near-ties); {planner_draws} simulation-stream draws compared")

@@ -11,7 +11,7 @@ are a near-tie (|gap| <= 1e-6) that the nets' rounding can flip.
 import numpy as np
 import pytest
 
-from conftest import SEED, golden, planner_net_flips
+from conftest import SEED, golden, oracle_slot_draws, planner_net_flips
 from gzero import _lib, boards, planner_nets
 
 pytestmark = pytest.mark.gpu
@@ -153,7 +153,10 @@ def test_plan_search_vs_reference(oracle, gnw):
 
 def test_selfplay_planner_games_vs_oracle(oracle, gnw):
     """gz_selfplay_plan_run: whole games (planner_steps 2, 3 sims) equal the oracle's
-    play_one_game driven by the GPU's net outputs."""
+    play_one_game driven by the GPU's net outputs -- moves, z, and every slot's RNG
+    draw counts over all the games it played (gz_selfplay_draws): at 3 simulations
+    the moves never depend on a rollout's value, the draw counts depend on every
+    planner and rollout decision."""
     from gzero.selfplay import SelfPlayEngine, records_to_games
     n_slots = 3
     eng = SelfPlayEngine(n_slots=n_slots, num_simulations=3, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED,
@@ -172,12 +175,21 @@ def test_selfplay_planner_games_vs_oracle(oracle, gnw):
         ref = oracle.play_game(prm, prm, gid)
         assert g["moves"] == ref["moves"], gid
         assert g["z"] == ref["z"], gid
+    st, cur = eng.boards()
+    got = eng.draws()
+    for s in range(n_slots):
+        done = list(range(s, int(cur[s]), n_slots))  # slot s plays ids s, s + n, s + 2n, ...
+        want = oracle_slot_draws(oracle, prm, prm, done, int(cur[s]), int(st["n_moves"][s]))
+        assert list(got[s]) == want, (s, list(got[s]), want)
+        assert want[1] > 0
 
 
 def test_config1_game_vs_oracle(oracle, gnw):
     """BASELINE config 1 (1 game, 50 sims, beta 0.2, planner_steps 5, medium), played to
     the end by the self-play engine: moves, players and z equal the oracle's
-    play_one_game driven by the GPU's net outputs (injected p / q)."""
+    play_one_game driven by the GPU's net outputs (injected p / q), and so do the
+    slot's RNG draw counts (every planner ply and rollout ply of the game's 50-sim
+    searches, gz_selfplay_draws)."""
     from gzero.selfplay import SelfPlayEngine, records_to_games
     eng = SelfPlayEngine(n_slots=1, num_simulations=50, c_puct=1.6, exploration=0.05, beta=0.2, seed=SEED,
                          plies_per_step=16, planner_steps=5, planner_difficulty="medium", gn_weights=gnw)
@@ -193,6 +205,9 @@ def test_config1_game_vs_oracle(oracle, gnw):
     ref = oracle.play_game(prm, prm, 0)
     assert game["moves"] == ref["moves"]
     assert game["players"] == ref["players"] and game["z"] == ref["z"]
+    st, cur = eng.boards()
+    want = oracle_slot_draws(oracle, prm, prm, [0], int(cur[0]), int(st["n_moves"][0]))
+    assert list(eng.draws()[0]) == want and want[1] > 0
 
 
 def test_incremental_graphnet_bitwise_on_planner_plies(gnw):

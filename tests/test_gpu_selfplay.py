@@ -115,7 +115,8 @@ def _leaf_rows(eng, n):
 def test_config2_200_sims_vs_oracle(oracle):
     """BASELINE config 2 per slot (200 sims, medium, beta 0, planner_steps 0, the
     PV forward on every node the searches create): 16 slots x 12 plies equal the
-    oracle's games, the forwards per step equal its predict() count, and the PV
+    oracle's games and RNG draw counts (every rollout ply), the forwards per step
+    equal its predict() count, and the PV
     outputs of the last step's nodes match torch fp32 (1e-4) and the oracle's
     masked prior (exact)."""
     from gzero import weights
@@ -133,13 +134,19 @@ def test_config2_200_sims_vs_oracle(oracle):
     st, gids = eng.boards()
     p = oracle.make_params("medium", sims=200, beta=0.0, seed=SEED)
     pred = 0
+    draws = eng.draws()
     for s in range(n_slots):
         assert int(gids[s]) == base + s
-        ref = oracle.play_game(p, p, base + s, max_plies=K)
+        with oracle.Trace() as tr:
+            ref = oracle.play_game(p, p, base + s, max_plies=K)
         assert ref["n"] == K
         cells = boards.words_to_cells(st["black"][s], st["white"][s])
         assert (cells == oracle.new_board(ref["moves"]).cells()).all(), s
         pred += ref["predicts"]
+        # the rollouts' draw counts: at 200 sims from the opening every root child
+        # gets one visit, so the moves alone never see a rollout
+        want = [sum(x[1] for x in tr.plies), sum(x[2] for x in tr.plies)]
+        assert list(draws[s]) == want and want[1] > 0, (s, list(draws[s]), want)
     assert leaves == pred
     # the last step's forwards: logits / value vs torch fp32, prior vs the oracle
     n = int(eng.counters()["leaves"])

@@ -146,18 +146,44 @@ def test_planner_search_vs_reference(idx):
         assert kids == c["children"]
 
 
-def _arena_pq(calls):
-    """pq callback from recorded planner calls: a board's p / q at its recorded top-k
-    cells (p / q depend on the board alone, so one board's calls merge)."""
-    tab = {}
-    for call in calls:
-        p, q = tab.setdefault(call["board"], (np.zeros(225, np.float32), np.zeros(225, np.float32)))
-        p[call["top"]] = _hexf(call["p"])
-        q[call["top"]] = _hexf(call["q"])
+def _replay_arena_case(g, c, perturb=None):
+    """Replay one arena_plans case in the oracle, every planner call fed the
+    reference's recorded net outputs IN ORDER, and check what the games' moves
+    alone cannot show (at 3-4 simulations every root child gets one visit, so the
+    move is the highest empty cell unless exploration fires -- SURVEY §0.4):
+    the i-th planner call sees the reference's i-th board (which pins every earlier
+    planner move, including the first ply's choice inside each rollout), every
+    planner move equals the reference's recorded move, and the call count matches.
+    ``perturb(p, q) -> (p, q)`` alters the injected outputs (sensitivity check).
+    Raises AssertionError (or oracle.CallbackError) on the first difference."""
+    calls = c["calls"]
+    pos = [0]
 
     def pq(board, game_id, sim, step):
-        return tab[_board_str(board)]
-    return pq
+        i = pos[0]
+        assert i < len(calls), f"planner call {i} beyond the reference's {len(calls)}"
+        call = calls[i]
+        assert _board_str(board) == call["board"], f"planner call {i}: board differs"
+        pos[0] += 1
+        p = np.zeros(225, np.float32)
+        q = np.zeros(225, np.float32)
+        p[call["top"]] = _hexf(call["p"])
+        q[call["top"]] = _hexf(call["q"])
+        return perturb(p, q) if perturb else (p, q)
+
+    cur = O.make_params("easy", sims=c["easy_sims"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+    base = O.make_params("easy", sims=c["eval_num_sim"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
+    with O.Trace() as tr:
+        games = []
+        for k in range(len(c["boards"])):
+            black, white = (cur, base) if k % 2 == 0 else (base, cur)
+            games.append(O.play_game(black, white, c["game_id_base"] + k))
+    for k, (got, ref) in enumerate(zip(games, c["boards"])):
+        assert got["moves"] == ref["moves"], (c["game_id_base"], k)
+        assert (got["winner"] or None) == ref["winner"]
+    assert pos[0] == len(calls), (pos[0], len(calls))
+    assert tr.planner_moves == [call["move"] for call in calls]
+    return games
 
 
 def test_arena_with_planner_exact_on_reference_outputs():
@@ -167,18 +193,44 @@ def test_arena_with_planner_exact_on_reference_outputs():
     outputs, the oracle plays each game (the evaluated AI on black in even games,
     easy difficulty with the fixture's simulation counts, beta 0.2, 2 planner plies,
     the fixture's seed on both sides, game id = base + g) move for move and to the
-    same winner as the reference's evaluate_model."""
+    same winner as the reference's evaluate_model -- and makes the reference's
+    planner calls, in order, on the same boards and with the same moves
+    (_replay_arena_case), so the planner's decisions are compared, not only the
+    games' moves."""
     g = golden("arena_plans")
     for c in g["cases"]:
-        pq = _arena_pq(c["calls"])
-        cur = O.make_params("easy", sims=c["easy_sims"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
-        base = O.make_params("easy", sims=c["eval_num_sim"], beta=0.2, seed=g["seed"], planner_steps=2, pq=pq)
-        for k, ref in enumerate(c["boards"]):
-            black, white = (cur, base) if k % 2 == 0 else (base, cur)
-            got = O.play_game(black, white, c["game_id_base"] + k)
-            assert got["moves"] == ref["moves"], (c["game_id_base"], k)
-            assert (got["winner"] or None) == ref["winner"]
+        _replay_arena_case(g, c)
         # the evaluated AI plays black in even games: its wins / losses are the result's
         won = [b["winner"] == (1 if k % 2 == 0 else 2) for k, b in enumerate(c["boards"])]
         lost = [b["winner"] == (2 if k % 2 == 0 else 1) for k, b in enumerate(c["boards"])]
         assert (sum(won), sum(lost)) == (c["result"]["wins"], c["result"]["losses"])
+
+
+@pytest.mark.parametrize("how", ["q+1e-4", "raise"])
+def test_arena_planner_check_detects_a_perturbed_net(how):
+    """The check above must be able to fail: with the injected DQN values moved by
+    1e-4 (the nets' own tolerance) times a fixed pattern over the cells, some
+    planner choice flips (a different board at a later call, or a different
+    recorded move), and a callback that raises is re-raised by the oracle wrapper
+    instead of being printed and swallowed by ctypes.
+    (Scaling p or q by 1.01 flips nothing in this fixture: the random-init
+    GraphNet's softmax is ~1/225 everywhere, so composed = a*p - (1-a)*q is ordered
+    like -q and a uniform scale keeps that order; an additive 1e-4 pattern flips 5
+    of the 4,006 recorded choices, 1e-3 flips 58.)"""
+    g = golden("arena_plans")
+
+    pattern = (np.float32(1e-4) * np.sin(np.arange(225) * 1.7)).astype(np.float32)
+
+    def scaled(p, q):
+        return p, q + pattern
+
+    def broken(p, q):
+        raise KeyError("no such board")
+
+    failed = 0
+    for c in g["cases"]:
+        try:
+            _replay_arena_case(g, c, perturb=scaled if how == "q+1e-4" else broken)
+        except (AssertionError, O.CallbackError):
+            failed += 1
+    assert failed == len(g["cases"]) if how == "raise" else failed >= 1
