@@ -500,12 +500,13 @@ struct SlotHeader {  // 128 bytes
     int32_t player;
     int32_t pad0, pad1;
     int64_t games_done;
-    // RNG draws of every search this slot ran since init (main stream, simulation
-    // streams): the checker compares them with the oracle's per-ply counts
-    // (gz_selfplay_draws), which sees rollout and planner decisions a game's moves hide
+    // totals over every search this slot ran since init: predict() calls and RNG
+    // draws (main stream, simulation streams).  The checker compares them with the
+    // oracle's per-ply counts (gz_selfplay_draws): they see the rollout and planner
+    // decisions a game's moves hide
+    int64_t predicts;
     int64_t main_draws;
     int64_t sim_draws;
-    int64_t pad2;
 };
 static_assert(sizeof(SlotHeader) == 128, "slot header");
 
@@ -525,7 +526,7 @@ __global__ void selfplay_init_kernel(char* slots, int n_slots, int64_t base, int
     h->player = 1;
     h->pad0 = h->pad1 = 0;
     h->games_done = 0;
-    h->main_draws = h->sim_draws = h->pad2 = 0;
+    h->predicts = h->main_draws = h->sim_draws = 0;
 }
 
 // training.play_one_game (training.py:141-218) for one slot, n_plies plies,
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
     }
     int64_t game_id = h->game_id;
     const int64_t gstride = h->game_id_stride;
-    long long games = 0, moves_played = 0, mcts_played = 0, dmain = 0, dsim = 0;
+    long long games = 0, moves_played = 0, mcts_played = 0, npred = 0, dmain = 0, dsim = 0;
     Tree t = tree_at(smem, p.num_simulations);
     __syncthreads();
     for (int it = 0; it < n_plies; it++) {
@@ -557,6 +558,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         int mv = search_move(&rs, game_id, p, t, sink, gather != 0, grid, so);
         __syncthreads();
         if (mv < 0) break;  // unreachable: live games always have an empty cell
+        npred += so.predicts;
         dmain += so.main_draws;
         dsim += so.sim_draws;
         const int n_moves = rs.n_moves, player = rs.player;
@@ -618,6 +620,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         h->n_moves = rs.n_moves;
         h->player = rs.player;
         h->games_done += games;
+        h->predicts += npred;
         h->main_draws += dmain;
         h->sim_draws += dsim;
         atomicAdd((unsigned long long*)&ctr->moves, (unsigned long long)moves_played);
@@ -691,6 +694,7 @@ __global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int 
         h->n_moves = over ? 0 : n_moves + 1;
         h->player = over ? 1 : 3 - player;
         h->games_done += games;
+        h->predicts += stats[s].predicts;
         h->main_draws += stats[s].main_draws;
         h->sim_draws += stats[s].sim_draws;
         atomicAdd((unsigned long long*)&ctr->moves, 1ull);
@@ -1014,8 +1018,9 @@ __global__ void selfplay_draws_kernel(const char* slots, int n_slots, int64_t* o
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
     const SlotHeader* h = (const SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
-    out[2 * s] = h->main_draws;
-    out[2 * s + 1] = h->sim_draws;
+    out[3 * s] = h->predicts;
+    out[3 * s + 1] = h->main_draws;
+    out[3 * s + 2] = h->sim_draws;
 }
 
 int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream) {

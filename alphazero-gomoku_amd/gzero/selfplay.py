@@ -195,12 +195,13 @@ class SelfPlayEngine:
 
 
     def draws(self):
-        """int64 [n_slots, 2]: (main-stream, simulation-stream) RNG draws of every
-        search each slot ran since the engine was created (gz_selfplay_draws)."""
-        out = torch.zeros(self.n_slots * 2, dtype=torch.int64, device="cuda")
+        """int64 [n_slots, 3]: (predict calls, main-stream RNG draws, simulation-stream
+        RNG draws) summed over every search each slot ran since the engine was created
+        (gz_selfplay_draws)."""
+        out = torch.zeros(self.n_slots * 3, dtype=torch.int64, device="cuda")
         _lib.check(self.lib.gz_selfplay_draws(ptr(self.d_slots), self.n_slots, ptr(out), stream()),
                    "gz_selfplay_draws")
-        return out.cpu().numpy().reshape(self.n_slots, 2)
+        return out.cpu().numpy().reshape(self.n_slots, 3)
 
 
 def records_to_games(recs):

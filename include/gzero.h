@@ -158,9 +158,9 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
                          const float* d_gn_weights, void* d_workspace, int32_t n_plies, gz_record* d_records,
                          int32_t record_cap, uint32_t* d_leaves, int32_t leaf_cap, int32_t* d_leaf_meta,
                          gz_selfplay_counters* d_counters, void* stream);
-/* per slot, the RNG draws of every search it ran since gz_selfplay_init:
- * d_out[2s] = main-stream draws, d_out[2s+1] = simulation-stream draws (the
- * checker's view of rollout / planner decisions, ai_agent.py:168-285) */
+/* per slot, totals over every search it ran since gz_selfplay_init: d_out[3s] =
+ * predict() calls, d_out[3s+1] = main-stream RNG draws, d_out[3s+2] = simulation-
+ * stream draws (the checker's view of rollout / planner decisions, ai_agent.py:168-285) */
 int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream);
 /* current board of every slot (for inspection / tests) */
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations,
@@ -231,7 +231,12 @@ int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
  * and its nets d_gn_weights (gz_gn_forward).  Host-driven: launches on `stream`
  * and synchronises it once per simulation round.  d_workspace:
  * gz_plan_workspace_bytes(n, num_simulations) bytes.  d_trees (optional) gets
- * gz_tree_bytes(num_simulations) bytes per game in gz_search's layout. */
+ * gz_tree_bytes(num_simulations) bytes per game in gz_search's layout.
+ * Footprint (C = max(n, 65536) GN rows per planner step, capped at n*S): per game
+ * its context + tree and S 128-B jobs; per row 0.9 KB of p / q, a 3.6 KB net record
+ * and, always reserved, the same again for GZ_FLAG_GN_CHECK's full-forward copy
+ * (0.36 GB at C = 65536); and n + C incremental-GraphNet map slots of 232 KB
+ * (16.2 GB at n = 4096, S = 200 -- 16.9 GB in all). */
 size_t gz_plan_workspace_bytes(int32_t n, int32_t num_simulations);
 int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
                    const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,

@@ -77,19 +77,20 @@ def planner_net_flips(calls, gnw, alpha):
 
 
 def oracle_slot_draws(oracle, black, white, slot_gids, cur_gid, cur_moves):
-    """(main, simulation) RNG draws the oracle makes playing a self-play slot's
-    games: every finished game in ``slot_gids`` to the end, then ``cur_gid``'s
-    first ``cur_moves`` plies -- what gz_selfplay_draws reports for the slot.  The
-    draw counts see every rollout and planner decision, which the games' moves do
-    not (a move at few simulations per child ignores the rollout values)."""
-    tot = [0, 0]
+    """(predicts, main draws, simulation draws) the oracle makes playing a
+    self-play slot's games: every finished game in ``slot_gids`` to the end, then
+    ``cur_gid``'s first ``cur_moves`` plies -- what gz_selfplay_draws reports for
+    the slot.  The draw counts see every rollout and planner decision, which the
+    games' moves do not (a move at few simulations per child ignores the rollout
+    values)."""
+    tot = [0, 0, 0]
     plays = [(g, 0) for g in slot_gids] + ([(cur_gid, cur_moves)] if cur_moves else [])
     for gid, cap in plays:
         with oracle.Trace() as tr:
             ref = oracle.play_game(black, white, gid, max_plies=cap)
         if cap:
             assert ref["n"] == cap
-        tot[0] += sum(p[1] for p in tr.plies)
-        tot[1] += sum(p[2] for p in tr.plies)
+        for i in range(3):
+            tot[i] += sum(p[i] for p in tr.plies)
     return tot
 

@@ -145,8 +145,8 @@ def test_config2_200_sims_vs_oracle(oracle):
         pred += ref["predicts"]
         # the rollouts' draw counts: at 200 sims from the opening every root child
         # gets one visit, so the moves alone never see a rollout
-        want = [sum(x[1] for x in tr.plies), sum(x[2] for x in tr.plies)]
-        assert list(draws[s]) == want and want[1] > 0, (s, list(draws[s]), want)
+        want = [sum(x[i] for x in tr.plies) for i in range(3)]
+        assert list(draws[s]) == want and want[2] > 0, (s, list(draws[s]), want)
     assert leaves == pred
     # the last step's forwards: logits / value vs torch fp32, prior vs the oracle
     n = int(eng.counters()["leaves"])
