@@ -5,31 +5,26 @@
 // 522-523).  A root child differs from the root by one stone at cell m, so in
 // layer L of the tower (x0 = conv0, y1, x1, y2, x2) only the positions within
 // Chebyshev radius L+1 of m can differ from the root's maps: 3x3, 5x5, 7x7, 9x9,
-// 11x11 windows (clipped to the board) -- about 31 % of the 4 x 225 positions of
+// 11x11 squares (clipped to the board) -- about 31 % of the 4 x 225 positions of
 // the residual convs.  The root is evaluated by the full kernel, which also
-// stores its x0, y1, x1, y2 maps (gz_pvnet.hip, pv_kernel_f16x3<.., true>); each
-// child then recomputes only its windows, reading the root's values around them.
+// stores its x0, y1, x1, y2 maps (gz_pvnet.hip, pv_kernel_f16x3<.., true>) and, for
+// the delta mode, its pre-BN accumulators.  Two kernels compute the root children:
 //
-// Exactness: every recomputed position takes the same products in the same order
-// as the full kernel (k = tap*128 + cin in 32-deep MFMA k-steps, hi*hi, w_lo*a_hi,
-// w_hi*a_lo; the same epilogue, the same hi/lo split, the same head-conv partial
-// sums per wave), and an MFMA output element depends only on its own row and
-// column operands, so the child's logits, value, softmax and prior are bit for
-// bit those of a full forward of the child's board (tests/test_gpu_pvinc.py).
+// * pv_sib_kernel (tree mode "exact"): every recomputed position takes the same
+//   products in the same order as the full kernel (k = tap*128 + cin in 32-deep MFMA
+//   k-steps, hi*hi, w_lo*a_hi, w_hi*a_lo; the same epilogue, the same hi/lo split,
+//   the same head-conv partial sums per wave), and an MFMA output element depends
+//   only on its own row and column operands, so the child's logits, value, softmax
+//   and prior are bit for bit those of a full forward of the child's board
+//   (tests/test_gpu_pvinc.py).  Windows of the root's maps around m are filled into
+//   LDS, the child's own squares overlaid.
+// * pv_delta_kernel (tree mode "delta"): the root's accumulators plus the
+//   convolution of the child's input differences (below; tests/test_gpu_pvdelta.py).
 //
 // Grandchildren (a child of a root child, one more stone at m2): the parent also
 // stores its recomputed squares (its "patch"), and the grandchild's windows are the
 // root's maps overlaid with the parent's patch around the parent's stone; the rest
-// is the same computation around m2 (pv_grandchild_kernel).
-//
-// One 512-thread workgroup per node at a time (8 waves; per layer wave = n-tile, or
-// n-tile pair x M half as the full kernel).  LDS holds the layer inputs as windows around m in
-// the full kernel's hi/lo plane layout ([16 channel groups][P positions][8]):
-//   X0 r3 (7x7)  Y1 r4 (9x9)  X1 r5 (11x11)  Y2 r6 (13x13)
-// -- the input of layer L needs the previous map at radius L+2; positions outside
-// the recomputed radius are the root's, off-board positions are zero (the
-// convolution's padding).  X0 and Y1 are dead once x1 is computed, so Y2 reuses
-// their space: 62 KB (X1) + 86.5 KB (Y2) + 7 KB.
+// is the same computation around m2 (pv_sib_kernel<true>, both modes).
 #include <hip/hip_runtime.h>
 #include <type_traits>
 
@@ -46,42 +41,15 @@ namespace {
 
 using namespace gzc;
 
-constexpr int NTC = 512;
-
 // Phase stamps (tools/pvinc_bench.py only): -DGZ_PVINC_STAMPS accumulates s_memtime
-// deltas of workgroup 0 / wave 0 per phase (vector atomics); compiled out otherwise.
+// deltas of workgroup 0 / thread 0 per phase (vector atomics); compiled out otherwise.
 #ifdef GZ_PVINC_STAMPS
-__device__ unsigned long long gz_pvinc_stamps[16];
-__device__ unsigned long long gz_pvinc_stamps_n;
-#define PI_T0() unsigned long long pit_ = __builtin_amdgcn_s_memtime()
-#define PI_STAMP(i)                                                                   \
-    do {                                                                              \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
-            atomicAdd(&gz_pvinc_stamps[i], t_ - pit_);                                \
-            pit_ = t_;                                                                \
-        }                                                                             \
-    } while (0)
-#else
-#define PI_T0() \
-    do {        \
-    } while (0)
-#define PI_STAMP(i) \
-    do {            \
-    } while (0)
+__device__ unsigned long long gz_pvinc_stamps[32];  // [0, 16): pv_sib_kernel, [16, 32): pv_delta_kernel
+__device__ unsigned long long gz_pvinc_stamps_n[2];
 #endif
-constexpr int P_X0 = 49, P_Y1 = 81, P_X1 = 121, P_Y2 = 169;
-constexpr int wbytes(int P) { return 2 * 16 * P * 16; }  // hi + lo planes
-constexpr int OFF_X1 = 0;
-constexpr int OFF_Y2 = OFF_X1 + wbytes(P_X1);
-constexpr int OFF_X0 = OFF_Y2;                   // aliases Y2 (dead by then)
-constexpr int OFF_Y1 = OFF_X0 + wbytes(P_X0);    // aliases Y2
-constexpr int OFF_HP = OFF_Y2 + wbytes(P_Y2);
-constexpr int HP_ROWS = 128;                     // >= 121 rows of the x2 window
-constexpr int OFF_COL = OFF_HP + 4 * 3 * HP_ROWS * 4;
-constexpr int LDS_C = OFF_COL + 16 * 32 * 2;
-static_assert(OFF_Y1 + wbytes(P_Y1) <= OFF_HP, "X0 + Y1 fit in the Y2 region");
-static_assert(LDS_C <= 160 * 1024, "LDS budget");
+constexpr int P_X0 = 49, P_Y1 = 81, P_X1 = 121, P_Y2 = 169;  // window positions, radius 3..6
+constexpr int wbytes(int P) { return 2 * 16 * P * 16; }       // hi + lo planes
+constexpr int HP_ROWS = 128;                                  // >= 121 rows of the x2 square
 
 // A window of a map: radius R around the child's stone (cr, cc), width w = 2R+1,
 // P = w*w positions, hi plane then lo plane, each [16 cg][P][8].  The geometry is
@@ -94,117 +62,6 @@ struct Win {
     __device__ static constexpr int plane() { return 16 * P * 8; }
     __device__ static constexpr int off(int ch0, int loc) { return ((ch0 >> 3) * P + loc) * 8 + (ch0 & 7); }
 };
-
-template <int R>
-__device__ inline Win<R> make_win(char* lds, int off) {
-    Win<R> x;
-    x.hi = (_Float16*)(lds + off);
-    return x;
-}
-
-// root's values (global map, full kernel layout [plane][16 cg][256][8]) into the
-// window, except the recomputed square of radius rc; zeros off the board.  Split in
-// a load half (every item of the thread issued at once, into registers) and a
-// store half, so a fill costs one memory latency, not one per item.
-template <int IT>
-struct FillBuf {
-    uint4 v[IT];
-    uint32_t skip;  // bit k: item k is not stored (recomputed there, or past the window)
-    uint32_t zero;  // bit k: item k is off the board (stored as zeros)
-};
-
-// Fill of window radius R (compile-time, so the index arithmetic divides by
-// constants) from the root's map gm.  Every item issues its load unconditionally
-// (items that are skipped or off the board read the map's first 16 bytes): no
-// branch between the loads, so all of a thread's loads are in flight together.
-// Skipped: the positions the layer recomputes (on the board within rc of the stone)
-// and, for a grandchild, the square of radius rcp around its parent's stone (r1, c1),
-// which patch_fill takes from the parent's patch.
-template <int R, int IT, bool GC>
-__device__ __forceinline__ void fill_load(FillBuf<IT>& f, int rc, const _Float16* __restrict__ gm, int cr, int cc,
-                                          int tid, int r1 = 0, int c1 = 0, int rcp = -1) {
-    constexpr int Wd = 2 * R + 1, P = Wd * Wd, n = 2 * 16 * P;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)gm, 0, 0x7fffffff, 0x00020000);
-    f.skip = 0;
-    f.zero = 0;
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        const int i = tid + k * NTC;
-        const int plane = i / (16 * P);
-        const int rem = i - plane * 16 * P;
-        const int cg = rem / P, loc = rem - cg * P;
-        const int pr = cr - R + loc / Wd, pc = cc - R + loc % Wd;
-        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
-        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-        bool keep = i < n && !(on && dr <= rc && dc <= rc);  // else the layer that recomputes it writes it
-        if (GC) {  // on-board positions of the parent's square come from its patch (off-board: zeros here)
-            const int er = pr > r1 ? pr - r1 : r1 - pr, ec = pc > c1 ? pc - c1 : c1 - pc;
-            keep = keep && !(on && er <= rcp && ec <= rcp);
-        }
-        const int off = (keep && on) ? (plane * PV_MAP_PLANE + (cg * 256 + pr * BN + pc) * 8) * 2 : 0;
-        f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        f.skip |= keep ? 0u : (1u << k);
-        f.zero |= on ? 0u : (1u << k);
-    }
-}
-
-// A grandchild's values of window x (radius R) in the square of radius RC around
-// its parent's stone (r1, c1): the parent's patch pt of that map
-// ([plane][16 cg][(2RC+1)^2][8], off-board entries zero), except the positions
-// this layer recomputes (on the board within rc of the grandchild's stone).
-template <int R, int RC>
-struct PatchFill {
-    static constexpr int S = 2 * RC + 1, n = 2 * 16 * S * S, IT = (n + NTC - 1) / NTC;
-    uint4 v[IT];
-    uint32_t put;
-};
-template <int R, int RC>
-__device__ __forceinline__ void patch_load(PatchFill<R, RC>& f, const _Float16* __restrict__ pt, int rc, int cr,
-                                           int cc, int r1, int c1, int tid) {
-    using F = PatchFill<R, RC>;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pt, 0, 0x7fffffff, 0x00020000);
-    f.put = 0;
-#pragma unroll
-    for (int k = 0; k < F::IT; k++) {
-        const int i = tid + k * NTC;
-        const int loc = i % (F::S * F::S);
-        const int pr = r1 - RC + loc / F::S, pc = c1 - RC + loc % F::S;
-        const int wr = pr - cr + R, wc = pc - cc + R;
-        const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
-        const int dr = pr > cr ? pr - cr : cr - pr, dc = pc > cc ? pc - cc : cc - pc;
-        // off-board entries of a patch are never read (the window fill stores zeros there),
-        // so a patch need only hold its on-board positions
-        const bool put = i < F::n && on && wr >= 0 && wr <= 2 * R && wc >= 0 && wc <= 2 * R && !(dr <= rc && dc <= rc);
-        f.v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i < F::n ? i : 0) * 16, 0, 0));
-        f.put |= put ? (1u << k) : 0u;
-    }
-}
-template <int R, int RC>
-__device__ __forceinline__ void patch_store(const PatchFill<R, RC>& f, const Win<R>& x, int cr, int cc, int r1, int c1,
-                                            int tid) {
-    using F = PatchFill<R, RC>;
-#pragma unroll
-    for (int k = 0; k < F::IT; k++) {
-        if (!(f.put & (1u << k))) continue;
-        const int i = tid + k * NTC;
-        const int pcg = i / (F::S * F::S), loc = i - pcg * (F::S * F::S);  // pcg = plane * 16 + cg
-        const int wl = (r1 - RC + loc / F::S - cr + R) * x.w + (c1 - RC + loc % F::S - cc + R);
-        *(uint4*)(x.hi + (pcg * x.P + wl) * 8) = f.v[k];
-    }
-}
-
-template <int R, int IT>
-__device__ __forceinline__ void fill_store(const FillBuf<IT>& f, const Win<R>& x, int tid) {
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        if (f.skip & (1u << k)) continue;
-        const int i = tid + k * NTC;  // = plane * 16P + cg * P + loc: the window's own layout
-        *(uint4*)(x.hi + i * 8) = (f.zero & (1u << k)) ? make_uint4(0u, 0u, 0u, 0u) : f.v[k];
-    }
-}
-
-constexpr int fill_items(int P) { return (2 * 16 * P + NTC - 1) / NTC; }
-static_assert(fill_items(169) <= 32, "skip / zero masks are 32-bit");
 
 // the recomputed rows of one layer: the square of radius rl around (cr, cc),
 // clipped, row-major
@@ -222,170 +79,6 @@ __device__ inline Rows make_rows(int cr, int cc, int rl) {
     return q;
 }
 
-// implicit-GEMM 3x3 conv of the window `in` at the positions ctr[m] (window-local
-// index of the output position, per lane) for the wave's NTW n-tiles nt0.. and its
-// first nt (runtime, <= NMAX) M tiles: the k-steps, products and their order per
-// accumulator are those of f16_conv (gz_f16conv.h).  The weight fragments of the
-// next 4 k-steps are in flight (ring slot = cq, so the indexing stays static).
-template <int NTW, int NT, int NMAX, class WI>
-__device__ __forceinline__ void win_conv_nt(const WI& in, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
-                                            int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
-    constexpr int CQ = 4, KS = 9 * CQ;
-    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
-    const int q = lane >> 4;
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
-    const int wo = (nt0 * 64 + lane) * 16;
-    // PI_WPROBE (wrong results, timing probe only): 1 = every weight load reads k-step 0
-    // (L1-resident: no weight stream), 2 = only the pair layers' second M half does
-#ifndef PI_WPROBE
-#define PI_WPROBE 0
-#endif
-#if PI_WPROBE
-#warning "PI_WPROBE is a timing probe: the tree forward's results are wrong in this build"
-#endif
-    const bool wprobe = PI_WPROBE == 1 || (PI_WPROBE == 2 && NTW == 2 && (threadIdx.x >> 8));
-    auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (wprobe ? 0 : ks * KS_BYTES) + n * 1024 + lo * LO_BYTES, 0));
-    };
-    const _Float16* lo_plane = in.hi + in.plane();
-    // weight ring: the next 4 k-steps' fragments in flight (an L2 hit takes longer
-    // than one short k-step); slot = cq % RING keeps the indexing static
-#ifndef PI_RING2
-#define PI_RING2 2
-#endif
-#ifndef PI_RING1
-#define PI_RING1 4
-#endif
-#ifndef PI_RING_L1
-#define PI_RING_L1 PI_RING1
-#endif
-    constexpr int RING = NTW == 1 ? (NMAX <= 2 ? PI_RING_L1 : PI_RING1) : PI_RING2;
-    static_assert(RING == 1 || RING == 2 || RING == 4 || RING == 8, "ring depth");
-    h8 b[RING][NTW][2];
-#pragma unroll
-    for (int c = 0; c < RING; c++)
-#pragma unroll
-        for (int n = 0; n < NTW; n++) {
-            b[c][n][0] = wload(c, n, 0);
-            b[c][n][1] = wload(c, n, 1);
-        }
-    // activation fragments double-buffered: the next k-step's ds_reads are issued
-    // before this k-step's MFMAs (buffer = cq & 1; 4 k-steps per tap keep it static)
-    int nb[NT];
-#pragma unroll
-    for (int m = 0; m < NT; m++) nb[m] = (ctr[m] - in.w - 1 + q * in.P) * 8;  // tap 0 = (-1, -1)
-    h8 ah[2][NT], al[2][NT];
-#pragma unroll
-    for (int m = 0; m < NT; m++) {
-        ah[0][m] = *(const h8*)(in.hi + nb[m]);
-        al[0][m] = *(const h8*)(lo_plane + nb[m]);
-    }
-    // one tap's 4 k-steps; PAR = tap parity (an 8-deep ring holds two taps: slot =
-    // 4 PAR + cq, so the taps run in unrolled pairs and the indexing stays static)
-    auto tap_body = [&](int tap, auto par) {
-        constexpr int PAR = decltype(par)::value;
-#pragma unroll
-        for (int cq = 0; cq < CQ; cq++) {
-            const int cur = cq & 1, nxt = cur ^ 1;
-            if (cq < CQ - 1) {
-                const int ao = (cq + 1) * 4 * in.P * 8;
-#pragma unroll
-                for (int m = 0; m < NT; m++) {
-                    ah[nxt][m] = *(const h8*)(in.hi + ao + nb[m]);
-                    al[nxt][m] = *(const h8*)(lo_plane + ao + nb[m]);
-                }
-            } else {  // first k-step of the next tap (past the last: tap 0 again, unused)
-                const int t2 = tap + 1 < 9 ? tap + 1 : 0;
-                const int toff = (t2 / 3 - 1) * in.w + (t2 % 3 - 1);
-#pragma unroll
-                for (int m = 0; m < NT; m++) {
-                    nb[m] = (ctr[m] + toff + q * in.P) * 8;
-                    ah[nxt][m] = *(const h8*)(in.hi + nb[m]);
-                    al[nxt][m] = *(const h8*)(lo_plane + nb[m]);
-                }
-            }
-            const int sl = (RING == 8 ? 4 * PAR : 0) + cq % (RING < 4 ? RING : 4);  // static
-#pragma unroll
-            for (int m = 0; m < NT; m++) {
-#pragma unroll
-                for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[cur][m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[cur][m], acc[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NTW; n++)
-                    acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[cur][m], acc[n][m], 0, 0, 0);
-            }
-            // refill this slot with k-step ks + RING (past the end: the first k-steps again, unused)
-            const int ksr = tap * CQ + cq + RING;
-            const int kn = ksr < KS ? ksr : ksr - KS;
-#pragma unroll
-            for (int n = 0; n < NTW; n++) {
-                b[sl][n][0] = wload(kn, n, 0);
-                b[sl][n][1] = wload(kn, n, 1);
-            }
-        }
-    };
-    if constexpr (RING == 8) {
-#pragma unroll 1
-        for (int tap = 0; tap < 8; tap += 2) {
-            tap_body(tap, std::integral_constant<int, 0>{});
-            tap_body(tap + 1, std::integral_constant<int, 1>{});
-        }
-        tap_body(8, std::integral_constant<int, 0>{});
-    } else {
-#pragma unroll 1
-        for (int tap = 0; tap < 9; tap++) tap_body(tap, std::integral_constant<int, 0>{});
-    }
-}
-
-// win_conv_nt for the runtime tile count nt (1 <= nt <= NMAX): one branch per
-// layer, none inside the k-loop (a guard per tile there splits the loop into
-// basic blocks and the compiler then waits for every load at each boundary)
-template <int NTW, int NMAX, class WI>
-__device__ __forceinline__ void win_conv(const WI& in, const int (&ctr)[NMAX], int nt, const _Float16* __restrict__ Wf,
-                                         int nt0, int lane, f32x4 (&acc)[NTW][NMAX]) {
-    static_assert(NMAX >= 1 && NMAX <= 12, "tile counts");
-    switch (nt) {
-        case 1: win_conv_nt<NTW, 1, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 2: if constexpr (NMAX >= 2) win_conv_nt<NTW, 2, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 3: if constexpr (NMAX >= 3) win_conv_nt<NTW, 3, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 4: if constexpr (NMAX >= 4) win_conv_nt<NTW, 4, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 5: if constexpr (NMAX >= 5) win_conv_nt<NTW, 5, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 6: if constexpr (NMAX >= 6) win_conv_nt<NTW, 6, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 7: if constexpr (NMAX >= 7) win_conv_nt<NTW, 7, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 8: if constexpr (NMAX >= 8) win_conv_nt<NTW, 8, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 9: if constexpr (NMAX >= 9) win_conv_nt<NTW, 9, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 10: if constexpr (NMAX >= 10) win_conv_nt<NTW, 10, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 11: if constexpr (NMAX >= 11) win_conv_nt<NTW, 11, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        case 12: if constexpr (NMAX >= 12) win_conv_nt<NTW, 12, NMAX, WI>(in, ctr, Wf, nt0, lane, acc); break;
-        default: break;
-    }
-}
-
-// Output positions of a wave's tiles: row i of the layer's recomputed square
-// (row-major) -> board (pr, pc); rows past the square recompute the tile's first row
-// (discarded).  Lane li of tile t takes row 16 t + perm(li): the permutation of the
-// input window of radius R that spreads a tile's 16 window slots over the LDS banks
-// (ds_read_b128 serves lanes {0-3, 12-15} with {4-11} of the next channel group, and
-// a square row that wraps inside a tile puts two lanes on one bank); found by a
-// local search over every stone cell's tiles, it cuts the modelled LDS cycles per
-// activation read from 8.6 / 8.2 / 9.8 / 9.9 to 7.2 / 7.2 / 7.6 / 7.7 (R = 3..6,
-// conflict-free = 4).  Only the lane <-> row assignment changes: every output is
-// computed exactly as before.  Measured 1 % SLOWER on the tree forward (the layers
-// are not LDS-bound), so off by default (PI_PERM=1 builds it).
-#ifndef PI_PERM
-#define PI_PERM 0
-#endif
-constexpr uint64_t tile_perm(int R) {
-    return !PI_PERM ? 0xfedcba9876543210ull
-                    : R == 3 ? 0xfba980531276e4cdull
-                    : R == 4 ? 0xdb9a742015638fceull
-                    : R == 5 ? 0xabcd50384612e97full
-                             : 0xfb8d534912706aecull;
-}
-
 template <int NMAX>
 struct TilePos {
     int pr[NMAX], pc[NMAX], row[NMAX];
@@ -394,7 +87,7 @@ struct TilePos {
 
 template <int NMAX, int R>
 __device__ __forceinline__ void tile_positions(const Rows& rows, int t0, int lane, TilePos<NMAX>& tp) {
-    const int pl = (int)((tile_perm(R) >> (4 * (lane & 15))) & 15ull);
+    const int pl = lane & 15;
     const float inv = 1.0f / (float)rows.wr;
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
@@ -408,186 +101,19 @@ __device__ __forceinline__ void tile_positions(const Rows& rows, int t0, int lan
     }
 }
 
-// epilogue of a map layer: y = relu(acc*S + T (+ skip)) at the wave's rows into the
-// output window, hi/lo split (f16_put4)
-template <int NTW, int NMAX, bool SKIP, class WO, class WS>
-__device__ __forceinline__ void child_store(const f32x4 (&acc)[NTW][NMAX], const TilePos<NMAX>& tp, int nt,
-                                            const WO& out, const WS& skw, int cr, int cc, const float* __restrict__ R,
-                                            int nt0, int lane) {
-#pragma unroll
-    for (int n = 0; n < NTW; n++) {
-        const int ch0 = (nt0 + n) * 16 + 4 * (lane >> 4);
-        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
-#pragma unroll
-        for (int m = 0; m < NMAX; m++) {
-            if (m >= nt || !tp.valid[m]) continue;
-            const int pr = tp.pr[m], pc = tp.pc[m];
-            f32x4 sk = zero4();
-            if (SKIP) {
-                const int sl = WS::off(ch0, (pr - cr + WS::r) * WS::w + (pc - cc + WS::r));
-                const h4 xh = *(const h4*)(skw.hi + sl);
-                const h4 xl = *(const h4*)(skw.hi + WS::plane() + sl);
-#pragma unroll
-                for (int r = 0; r < 4; r++) sk[r] = (float)xh[r] + (float)xl[r];
-            }
-            h4 hi, lo;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]);
-                if (SKIP) y += sk[r];
-                y = y > 0.f ? y : 0.f;
-                const _Float16 h = (_Float16)y;
-                hi[r] = h;
-                lo[r] = (_Float16)(y - (float)h);
-            }
-            const int o = WO::off(ch0, (pr - cr + WO::r) * WO::w + (pc - cc + WO::r));
-            *(h4*)(out.hi + o) = hi;
-            *(h4*)(out.hi + WO::plane() + o) = lo;
-        }
-    }
-}
-
 template <int NMAX, class WI>
 __device__ __forceinline__ void tile_centres(const TilePos<NMAX>& tp, int cr, int cc, int (&ctr)[NMAX]) {
 #pragma unroll
     for (int m = 0; m < NMAX; m++) ctr[m] = (tp.pr[m] - cr + WI::r) * WI::w + (tp.pc[m] - cc + WI::r);
 }
 
-// NTW = 1: wave w = n-tile w over all the layer's M tiles (each weight fragment read
-// once per child, each activation fragment feeds 3 MFMAs); NTW = 2: wave = (n-tile
-// pair, balanced M half), as the full kernel (activation fragments feed 6 MFMAs,
-// weights read by both halves).  NMAX = the layer's tiles per wave at most.
-template <int NTW, int NMAX, bool SKIP, class WI, class WO, class WS>
-__device__ __forceinline__ void child_map_layer(const WI& in, const WO& out, const WS& skw, int cr, int cc,
-                                                const float* __restrict__ W, int layer, int wave, int lane) {
-    const Rows rows = make_rows(cr, cc, WI::r - 1);
-    const int T = (rows.n + 15) >> 4;
-    int t0 = 0, nt = T, nt0 = wave;
-    if (NTW == 2) {
-        const int T0 = (T + 1) >> 1, mg = wave >> 2;
-        t0 = mg ? T0 : 0;
-        nt = mg ? T - T0 : T0;
-        nt0 = 2 * (wave & 3);
-    }
-    TilePos<NMAX> tp;
-    tile_positions<NMAX, WI::r>(rows, t0, lane, tp);
-    int ctr[NMAX];
-    tile_centres<NMAX, WI>(tp, cr, cc, ctr);
-    f32x4 acc[NTW][NMAX];
-#pragma unroll
-    for (int n = 0; n < NTW; n++)
-#pragma unroll
-        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    if (nt > 0)
-        win_conv<NTW, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), nt0, lane, acc);
-    child_store<NTW, NMAX, SKIP>(acc, tp, nt, out, skw, cr, cc, W + RES0 + layer * RES_STRIDE, nt0, lane);
-}
-
-#ifndef PI_NTW1
-#define PI_NTW1 1  // n-tiles per wave of y1 / x1 / y2 (tools/Makefile variants)
-#endif
-#ifndef PI_NTW2
-#define PI_NTW2 1
-#endif
-#ifndef PI_NTW3
-#define PI_NTW3 2
-#endif
-
-// the last residual layer (x2): the 1x1 head convs' partial sums need a wave's
-// 32 channels (n-tiles 2np, 2np+1) in one fma chain per lane (f16_store_heads), so
-// here wave = (n-tile pair np, M half); the M tiles are split evenly
-template <int NMAX, class WI, class WS>
-__device__ __forceinline__ void child_head_layer(const WI& in, const WS& skw, int cr, int cc,
-                                                 const float* __restrict__ W, int wave, int lane,
-                                                 float* __restrict__ hpart) {
-    constexpr int layer = 3;
-    const int np = wave & 3, mg = wave >> 2;
-    const Rows rows = make_rows(cr, cc, 5);
-    const int T = (rows.n + 15) >> 4;
-    const int T0 = (T + 1) >> 1;
-    const int t0 = mg ? T0 : 0, nt = mg ? T - T0 : T0;
-    TilePos<NMAX> tp;
-    tile_positions<NMAX, WI::r>(rows, t0, lane, tp);
-    int ctr[NMAX];
-    tile_centres<NMAX, WI>(tp, cr, cc, ctr);
-    f32x4 acc[2][NMAX];
-#pragma unroll
-    for (int n = 0; n < 2; n++)
-#pragma unroll
-        for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    if (nt > 0) win_conv<2, NMAX>(in, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
-    const float* R = W + RES0 + layer * RES_STRIDE;
-    float s0[NMAX], s1[NMAX], sv[NMAX];
-#pragma unroll
-    for (int m = 0; m < NMAX; m++) s0[m] = s1[m] = sv[m] = 0.f;
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
-        const f32x4 s = *(const f32x4*)(R + RES_S + ch0), t = *(const f32x4*)(R + RES_T + ch0);
-        const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
-        const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
-#pragma unroll
-        for (int m = 0; m < NMAX; m++) {
-            if (m >= nt) continue;
-            const int sl = WS::off(ch0, (tp.pr[m] - cr + WS::r) * WS::w + (tp.pc[m] - cc + WS::r));
-            const h4 xh = *(const h4*)(skw.hi + sl);
-            const h4 xl = *(const h4*)(skw.hi + WS::plane() + sl);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float y = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + ((float)xh[r] + (float)xl[r]);
-                y = y > 0.f ? y : 0.f;
-                s0[m] = __builtin_fmaf(w0[r], y, s0[m]);
-                s1[m] = __builtin_fmaf(w1[r], y, s1[m]);
-                sv[m] = __builtin_fmaf(wv[r], y, sv[m]);
-            }
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < NMAX; m++) {
-        if (m >= nt) continue;
-        float a = s0[m], c = s1[m], v = sv[m];
-        a += __shfl_xor(a, 16);
-        c += __shfl_xor(c, 16);
-        v += __shfl_xor(v, 16);
-        a += __shfl_xor(a, 32);
-        c += __shfl_xor(c, 32);
-        v += __shfl_xor(v, 32);
-        const int i = tp.row[m];
-        if (lane < 16 && tp.valid[m]) {
-            hpart[(np * 3 + 0) * HP_ROWS + i] = a;
-            hpart[(np * 3 + 1) * HP_ROWS + i] = c;
-            hpart[(np * 3 + 2) * HP_ROWS + i] = v;
-        }
-    }
-}
-
 __device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
 
 // A parent's patch for its grandchildren: the recomputed squares of its maps
 // (x0 r1, y1 r2, x1 r3, y2 r4), [plane][16 cg][(2r+1)^2][8] each, in that order
-constexpr int PATCH_R[4] = {1, 2, 3, 4};
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // halves
 constexpr int PATCH_HALVES = 164 * 256;
 
-
-// copy the square of radius RC around (cr, cc) of window x into patch slot pt
-template <int R, int RC>
-__device__ __forceinline__ void patch_dump(const Win<R>& x, _Float16* __restrict__ pt, int tid) {
-    constexpr int S = 2 * RC + 1, n = 2 * 16 * S * S;
-    for (int i = tid; i < n; i += NTC) {
-        const int pc_ = i / (S * S), loc = i - pc_ * (S * S);  // pc_ = plane * 16 + cg
-        const int wl = (loc / S - RC + R) * x.w + (loc % S - RC + R);
-#ifndef PI_PATCH_NT
-#define PI_PATCH_NT 1
-#endif
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = *(const u32x4*)(x.hi + (pc_ * x.P + wl) * 8);
-        if (PI_PATCH_NT)  // streamed out: keeps the roots' maps in L2
-            __builtin_nontemporal_store(v, (u32x4*)(pt + i * 8));
-        else
-            *(u32x4*)(pt + i * 8) = v;
-    }
-}
 
 struct TreeArgs {
     const int32_t* cinfo;  // per leaf (tree_lists_kernel): -1, or (GC << 30) | (root map slot << 8) | stone cell
@@ -600,244 +126,8 @@ struct TreeArgs {
     _Float16* patches;
     float* hbuf;
     int32_t* tiles;  // pv_sib_kernel: 16-row MFMA tiles executed per residual conv [children, grandchildren]
+    const float* pres;  // pv_delta_kernel: the roots' pre-BN accumulator maps (4 x PV_PRE_FLOATS per root)
 };
-
-// The incremental forward of node b relative to node base (its parent): the root
-// child of root rb (GC = false; base = rb) or the grandchild of root rb through the
-// root child base (GC = true: the parent's maps are the root's overlaid with the
-// parent's patch).  dump >= 0: also store b's patch in slot dump (b has grandchildren).
-template <bool GC>
-__device__ __forceinline__ void tree_node(const TreeArgs& A, char* lds, int b, int base, int rb, int ci, int c1cell,
-                                          int dump) {
-    const float* W = A.W;
-    // opaque per node (bit 0: child kernel, bit 1: grandchild kernel): keeps the
-    // compiler from hoisting every layer's per-lane weight addresses out of the node
-    // loop (they would stay live, and spill, across it)
-#ifndef PI_OPQ_W
-#define PI_OPQ_W 3
-#endif
-#ifndef PI_OPQ_T
-#define PI_OPQ_T 2
-#endif
-    if (PI_OPQ_W & (GC ? 2 : 1)) asm volatile("" : "+s"(W));
-    const auto X0 = make_win<3>(lds, OFF_X0);
-    const auto Y1 = make_win<4>(lds, OFF_Y1);
-    const auto X1 = make_win<5>(lds, OFF_X1);
-    const auto Y2 = make_win<6>(lds, OFF_Y2);
-    float* hpart = (float*)(lds + OFF_HP);
-    _Float16* col = (_Float16*)(lds + OFF_COL);
-    PI_T0();
-    const int o = (ci >> 8) & 0x3fffff;  // the root's map slot
-    int tid = threadIdx.x;
-    if (PI_OPQ_T & (GC ? 2 : 1)) asm volatile("" : "+v"(tid));  // likewise the fills' index arithmetic
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t* cb = A.boards + (size_t)b * 16;
-    const int cell = ci & 0xff;  // the stone b adds to base (tree_lists_kernel)
-    const int cr = cell / BN, cc = cell % BN;
-    int r1 = 0, c1 = 0;
-    const _Float16* pt = nullptr;
-    if (GC) {
-        r1 = c1cell / BN;
-        c1 = c1cell % BN;
-        pt = A.patches + (size_t)__builtin_amdgcn_readfirstlane(A.pslot[base]) * PATCH_HALVES;
-    }
-    const _Float16* gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
-    PI_STAMP(0);
-
-    // phase 0: the parent's values around the recomputed windows; conv0's im2col
-    {
-        FillBuf<fill_items(P_X0)> f0;
-        FillBuf<fill_items(P_Y1)> f1;
-        FillBuf<fill_items(P_X1)> f2;
-        fill_load<3, fill_items(P_X0), GC>(f0, 1, gm, cr, cc, tid, r1, c1, PATCH_R[0]);
-        fill_load<4, fill_items(P_Y1), GC>(f1, 2, gm + PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[1]);
-        fill_load<5, fill_items(P_X1), GC>(f2, 3, gm + 2 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[2]);
-        if (GC) {  // the parent's recomputed squares (disjoint from the positions above)
-            PatchFill<3, PATCH_R[0]> p0;
-            PatchFill<4, PATCH_R[1]> p1;
-            PatchFill<5, PATCH_R[2]> p2;
-            patch_load(p0, pt + PATCH_OFF[0], 1, cr, cc, r1, c1, tid);
-            patch_load(p1, pt + PATCH_OFF[1], 2, cr, cc, r1, c1, tid);
-            patch_load(p2, pt + PATCH_OFF[2], 3, cr, cc, r1, c1, tid);
-            patch_store(p0, X0, cr, cc, r1, c1, tid);
-            patch_store(p1, Y1, cr, cc, r1, c1, tid);
-            patch_store(p2, X1, cr, cc, r1, c1, tid);
-        }
-        fill_store<3>(f0, X0, tid);
-        fill_store<4>(f1, Y1, tid);
-        fill_store<5>(f2, X1, tid);
-    }
-    {
-        const Rows r0w = make_rows(cr, cc, 1);
-        const int row = tid >> 5, k = tid & 31;  // 16 rows x 32 k
-        _Float16 v = (_Float16)0.f;
-        if (row < r0w.n && k < 27) {
-            const int pr = r0w.r0 + row / r0w.wr, pc = r0w.c0 + row % r0w.wr;
-            const int tap = k / 3, cin = k % 3;
-            const int rr = pr + tap / 3 - 1, c2 = pc + tap % 3 - 1;
-            if (rr >= 0 && rr < BN && c2 >= 0 && c2 < BN) {
-                const int bit = bit_of_board(rr, c2);
-                const uint32_t bl = (cb[bit >> 5] >> (bit & 31)) & 1u, wh = (cb[8 + (bit >> 5)] >> (bit & 31)) & 1u;
-                v = (_Float16)(float)(cin == 0 ? bl : (cin == 1 ? wh : 1u - (bl | wh)));
-            }
-        }
-        col[row * 32 + k] = v;
-    }
-    __syncthreads();
-    PI_STAMP(1);
-    // conv0 + BN + ReLU at the <= 9 positions around the stone (conv0_f16: wave = n-tile)
-    {
-        const Rows r0w = make_rows(cr, cc, 1);
-        const int li = lane & 15, q = lane >> 4, nt = wave;
-        const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
-        const h8 bh = *(const h8*)wf, bl = *(const h8*)(wf + 8 * 64 * 8);
-        const int ch0 = nt * 16 + 4 * q;
-        const f32x4 s = *(const f32x4*)(W + C0_S + ch0), t = *(const f32x4*)(W + C0_T + ch0);
-        const h8 a = *(const h8*)(col + li * 32 + 8 * q);
-        f32x4 acc = zero4();
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a, acc, 0, 0, 0);
-        if (li < r0w.n) {
-            const int pr = r0w.r0 + li / r0w.wr, pc = r0w.c0 + li % r0w.wr;
-            h4 hi, lo;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float y = __builtin_fmaf(acc[r], s[r], t[r]);
-                y = y > 0.f ? y : 0.f;
-                const _Float16 h = (_Float16)y;
-                hi[r] = h;
-                lo[r] = (_Float16)(y - (float)h);
-            }
-            const int off = X0.off(ch0, (pr - cr + 3) * 7 + (pc - cc + 3));
-            *(h4*)(X0.hi + off) = hi;
-            *(h4*)(X0.hi + X0.plane() + off) = lo;
-        }
-    }
-    __syncthreads();
-    PI_STAMP(2);
-    child_map_layer<PI_NTW1, 2 / PI_NTW1, false>(X0, Y1, X0, cr, cc, W, 0, wave, lane);  // y1
-    __syncthreads();
-    PI_STAMP(3);
-    // Y2's values from the root's map: loaded before x1 so their latency hides behind
-    // it (44 VGPRs held across the layer), stored once X0 / Y1 are dead
-#ifndef PI_Y2EARLY
-#define PI_Y2EARLY 0
-#endif
-    FillBuf<fill_items(P_Y2)> f3;
-    if (PI_Y2EARLY) fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
-    child_map_layer<PI_NTW2, 4 / PI_NTW2, true>(Y1, X1, X0, cr, cc, W, 1, wave, lane);  // x1 = relu(.. + x0)
-    __syncthreads();
-    if (!GC && dump >= 0) {  // b has grandchildren: keep its x0 / y1 / x1 squares before Y2 reuses X0 / Y1
-        _Float16* ps = A.patches + (size_t)dump * PATCH_HALVES;
-        patch_dump<3, 1>(X0, ps + PATCH_OFF[0], tid);
-        patch_dump<4, 2>(Y1, ps + PATCH_OFF[1], tid);
-        patch_dump<5, 3>(X1, ps + PATCH_OFF[2], tid);
-        __syncthreads();
-    }
-    PI_STAMP(4);
-    {  // X0 / Y1 are dead
-        if (!PI_Y2EARLY) fill_load<6, fill_items(P_Y2), GC>(f3, 4, gm + 3 * PV_MAP_HALVES, cr, cc, tid, r1, c1, PATCH_R[3]);
-        if (GC) {
-            PatchFill<6, PATCH_R[3]> p3;
-            patch_load(p3, pt + PATCH_OFF[3], 4, cr, cc, r1, c1, tid);
-            patch_store(p3, Y2, cr, cc, r1, c1, tid);
-        }
-        fill_store<6>(f3, Y2, tid);
-    }
-    PI_STAMP(5);
-    child_map_layer<PI_NTW3, 6 / PI_NTW3, false>(X1, Y2, X1, cr, cc, W, 2, wave, lane);  // y2
-    __syncthreads();
-    if (!GC && dump >= 0) patch_dump<6, 4>(Y2, A.patches + (size_t)dump * PATCH_HALVES + PATCH_OFF[3], tid);
-    PI_STAMP(6);
-    child_head_layer<4>(Y2, X1, cr, cc, W, wave, lane, hpart);  // x2 -> head convs
-    __syncthreads();
-    PI_STAMP(7);
-    // b's head-conv record: recomputed positions from hpart (bias first, then the 4
-    // waves' partials in order, as the full kernel), the rest is the parent's
-    {
-        const Rows r4 = make_rows(cr, cc, 5);
-        const float* hr = A.hbuf + (size_t)base * HSTRIDE;
-        float* h = A.hbuf + (size_t)b * HSTRIDE;
-        for (int j = tid; j < HSTRIDE; j += NTC) {
-            float v = hr[j];
-            int pos = -1, which = 0;
-            if (j < POS) {
-                pos = j;
-            } else if (j < 2 * POS) {
-                pos = j - POS;
-                which = 1;
-            } else if (j >= HV_OFF && j < HV_OFF + POS) {
-                pos = j - HV_OFF;
-                which = 2;
-            }
-            if (pos >= 0) {
-                const int pr = pos / BN, pc = pos % BN;
-                if (pr >= r4.r0 && pr < r4.r0 + r4.n / r4.wr && pc >= r4.c0 && pc < r4.c0 + r4.wr) {
-                    const int i = (pr - r4.r0) * r4.wr + (pc - r4.c0);
-                    float acc = which == 0 ? W[P_B] : (which == 1 ? W[P_B + 1] : W[V_B]);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) acc += hpart[(q * 3 + which) * HP_ROWS + i];
-                    v = acc;
-                }
-            }
-            h[j] = v;
-        }
-    }
-    PI_STAMP(8);
-#ifdef GZ_PVINC_STAMPS
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, 1ull);
-#endif
-    // no barrier: the next node writes X0 / Y1 / X1 (read before the last barrier)
-    // and hpart only after several more barriers
-}
-
-// Root children, in leaf order (a root's children follow it in the leaf buffer): a
-// leaf is one iff meta >= 0 names a root with a map slot (ord >= 0).
-__global__ __launch_bounds__(NTC, 1) void pv_child_kernel(TreeArgs A, int n, const int32_t* __restrict__ d_count) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
-    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
-    // XCD-aware order: workgroup g runs on XCD g % 8 (round-robin dispatch); each XCD
-    // takes a contiguous eighth of the leaves and its workgroups interleave over it,
-    // so the CUs of one XCD work on neighbouring children -- the same root, whose
-    // maps then stay in that XCD's L2 (placement only affects speed, not results)
-    const int nx = gridDim.x >= 8 ? 8 : 1;
-    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
-    const int chunk = (count + nx - 1) / nx;
-    if (k >= per) return;  // grids that are not a multiple of 8: the remainder idles
-    const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
-    for (int b = beg; b < end; b += per) {
-        // one round of independent loads per leaf: its tag word and parent
-        const int ci = __builtin_amdgcn_readfirstlane(A.cinfo[b]);
-        const int rb = __builtin_amdgcn_readfirstlane(A.meta[b]);
-        const int ps = __builtin_amdgcn_readfirstlane(A.pslot[b]);
-        if (ci < 0 || (ci & (1 << 30))) continue;  // not a root child with a mapped root
-        tree_node<false>(A, lds, b, rb, rb, ci, 0, ps);
-    }
-}
-
-// Grandchildren (children of root children whose patch was stored), from their list
-__global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const int32_t* __restrict__ list,
-                                                               const int32_t* __restrict__ list_count) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_C];
-    const int count = *list_count;
-    // XCD-aware, as pv_child_kernel: a contiguous eighth of the list per XCD, so the
-    // grandchildren of one root (adjacent in the list) share that XCD's L2 copy of
-    // the root's maps
-    const int nx = gridDim.x >= 8 ? 8 : 1;
-    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
-    const int chunk = (count + nx - 1) / nx;
-    if (k >= per) return;
-    const int beg = xcd * chunk + k, end = (xcd + 1) * chunk < count ? (xcd + 1) * chunk : count;
-    for (int it = beg; it < end; it += per) {
-        const int b = __builtin_amdgcn_readfirstlane(list[it]);
-        const int p = __builtin_amdgcn_readfirstlane(A.meta[b]);
-        const int ci = __builtin_amdgcn_readfirstlane(A.cinfo[b]);
-        const int rb = __builtin_amdgcn_readfirstlane(A.meta[p]);
-        const int c1cell = __builtin_amdgcn_readfirstlane(A.cinfo[p]) & 0xff;
-        tree_node<true>(A, lds, b, p, rb, ci, c1cell, -1);
-    }
-}
 
 // ============================================================ sibling-batched incremental forward
 // pv_sib_kernel: the same node computation as tree_node, scheduled so that one pass
@@ -858,39 +148,28 @@ __global__ __launch_bounds__(NTC, 1) void pv_grandchild_kernel(TreeArgs A, const
 // weight fragment is read once per pass and each activation fragment feeds 6 MFMAs.
 // Weight bytes per node: 576 KB x (1/6 + 1/3 + 1/2 + 1) = 1.15 MB (was 3.7 MB).
 // Every output element takes the full kernel's products in the full kernel's order
-// (the k-loop is win_conv's; the epilogues are tree_node's), so results stay bitwise
-// those of the full forward.
-#ifndef SIB_WAVES
-#define SIB_WAVES 4
-#endif
-// SIB_WAVES 4 (default): one wave per SIMD over all of a pass's M tiles, each weight
-// fragment read once per pass; 8: two waves per SIMD, waves np and np + 4 own the same
-// n-tile pair and split the M tiles (SIB_MH halves), reading the fragments twice.  With
-// item-major window fills 8 waves were 6 % faster (their VALU address work hid behind
-// the other wave); with position-major fills 4 waves are 1.5 % faster (same box).
-constexpr int NTS = 64 * SIB_WAVES, SIB_MH = SIB_WAVES / 4;
-constexpr int sib_tiles(int t) { return (t + SIB_MH - 1) / SIB_MH; }
+// (the full kernel's k-loop and epilogues), so results stay bitwise those of the full
+// forward.  (Two waves per SIMD splitting the M tiles, reading each fragment twice,
+// measured 1.5 % slower with the position-major fills.)
+constexpr int NTS = 256, SIB_MH = 1;  // 4 waves; SIB_MH: M halves per n-tile pair
+constexpr int sib_tiles(int t) { return t; }
 constexpr int SIB_G = 6;
 constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
 static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
 constexpr int SIB_HP = SIB_WIN;                     // head partials [4 pairs][3][HP_ROWS]
 constexpr int SIB_U = SIB_HP + 4 * 3 * HP_ROWS * 4;  // unit table
-// SIB_NEXT 1: the next chunk's units are built at the end of this chunk's y1 pass and its
-// x0 windows are filled right after this chunk's last x2 k-loop (two unit tables)
-#ifndef SIB_NEXT
-#define SIB_NEXT 0
-#endif
-constexpr int LDS_S = SIB_U + (SIB_NEXT ? 2 : 1) * SIB_G * 128;  // SibUnit: 128 B
+constexpr int LDS_S = SIB_U + SIB_G * 128;  // SibUnit: 128 B
 static_assert(LDS_S <= 160 * 1024, "LDS budget");
 
 // phase stamps of pv_sib_kernel (workgroup 0, thread 0; -DGZ_PVINC_STAMPS builds only)
+template <int BASE = 0>
 struct SibStamp {
 #ifdef GZ_PVINC_STAMPS
     unsigned long long t = __builtin_amdgcn_s_memtime();
     __device__ void operator()(int i) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();
-            atomicAdd(&gz_pvinc_stamps[i], t_ - t);
+            atomicAdd(&gz_pvinc_stamps[BASE + i], t_ - t);
             t = t_;
         }
     }
@@ -978,27 +257,16 @@ __device__ __forceinline__ SibU sib_uniform(const SibUnit& u) {
     return s;
 }
 
-#ifndef SIB_FILL_POS
-#define SIB_FILL_POS 1
-#endif
-// SIB_Y1LDS 1: the y1 epilogue also writes the new y1 squares of the first x1 pass's
-// nodes into their x1 windows in LDS, and the rest of those windows is filled (SKIPOWN:
-// every position but the node's own square) right after the y1 k-loop -- no fill round
-// trip between y1 and x1
-#ifndef SIB_Y1LDS
-#define SIB_Y1LDS 0
-#endif
-static_assert(!SIB_Y1LDS || SIB_FILL_POS, "SIB_Y1LDS needs the position-major fill");
-template <int MAP, bool GC, bool SKIPOWN = false>
+template <int MAP, bool GC>
 __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, int ng, int tid) {
-    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P, IT = (PER + NTS - 1) / NTS;
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P;
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
-#if SIB_FILL_POS
     // position-major: work blocks (unit, 64 window positions); a lane works out its
     // position's source once (root map, own square, parent's square or zero), then its
     // 32 channel-group planes go by LDS-DMA (for one plane a wave's positions are
-    // contiguous in LDS; at the source the planes are a fixed stride apart)
-    (void)IT;
+    // contiguous in LDS; at the source the planes are a fixed stride apart).  (The
+    // item-major fill, one 16-B item per thread, spent ~60 VALU per item: 136.7 vs
+    // 141.0 ms per forward.)
     constexpr int NB = (P + 63) / 64;
     const int lane = tid & 63, wave = tid >> 6;
     for (int blk = wave; blk < ng * NB; blk += NTS / 64) {
@@ -1023,53 +291,26 @@ __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, in
             stride = SS * 8;
         }
         char* dst = lds + (size_t)g * PER * 16 + (size_t)b0 * 16;  // + lane * 16 by the DMA
-        if (loc < P && !(SKIPOWN && own)) {
+        if (loc < P) {
 #pragma unroll
             for (int pcg = 0; pcg < 32; pcg++)
                 __builtin_amdgcn_global_load_lds((glb_void_t*)(src + pcg * stride), (lds_void_t*)(dst + pcg * P * 16), 16,
                                                  0, 0);
         }
     }
-#else
-    const int wb = tid & ~63;
-    for (int g = 0; g < ng; g++) {
-        const SibU u = sib_uniform(U[u0 + g]);
-        char* dst = lds + (size_t)g * PER * 16;
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int i = tid + k * NTS;
-            if ((k + 1) * NTS > PER && i >= PER) continue;  // past this unit's window (EXEC-masked)
-            const int pcg = i / P, loc = i - pcg * P;        // pcg = plane * 16 + cg
-            const int dr = loc / Wd - R, dc = loc % Wd - R;  // relative to the stone
-            const int pr = u.cr + dr, pc = u.cc + dc;
-            const bool on = pr >= 0 && pr < BN && pc >= 0 && pc < BN;
-            const bool own = on && iabs(dr) <= rc && iabs(dc) <= rc;
-            const void* src = on ? (const void*)(u.gm + MAP * PV_MAP_HALVES + (pcg >> 4) * PV_MAP_PLANE +
-                                                 ((pcg & 15) * 256 + pr * BN + pc) * 8)
-                                 : (const void*)gz_sib_zero16;
-            if (MAP > 0 && own) src = u.own + PATCH_OFF[MAP] + (pcg * SS + (dr + rc) * S + (dc + rc)) * 8;
-            if (GC && on && !own && iabs(pr - u.r1) <= rc && iabs(pc - u.c1) <= rc)
-                src = u.par + PATCH_OFF[MAP] + (pcg * SS + (pr - u.r1 + rc) * S + (pc - u.c1 + rc)) * 8;
-            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + (size_t)(wb + k * NTS) * 16), 16, 0, 0);
-        }
-    }
-#endif
 }
 
-// The k-loop of a pass for the wave's n-tiles {nt0, nt0+1} over NT M tiles: win_conv_nt's
+// The k-loop of a pass for the wave's n-tiles {nt0, nt0+1} over NT M tiles: the full kernel's
 // k-steps, products and accumulation order, with one wave per SIMD: each tile's
 // activation fragments for the next k-step are read right after its MFMAs (the other
 // tiles' MFMAs cover the LDS latency), weight fragments 4 k-steps ahead.  act = the
 // pass's windows (each [plane][16 cg][P][8]); ctr[m] = the lane's window-local row
 // (unit offset included).
-#ifndef SIB_RING
-#define SIB_RING 4
-#endif
 template <int NT, int NMAX, int R>
 __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
                                             int nt0, int lane, f32x4 (&acc)[2][NMAX]) {
     constexpr int Wd = 2 * R + 1, P = Wd * Wd, CQ = 4, KS = 9 * CQ, PLANE = 16 * P * 8;
-    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES, RING = SIB_RING;
+    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES, RING = 4;
     static_assert(RING == 4, "ring depth");
     // Weight fragments 3 k-steps ahead: at the START of k-step j, k-step j + 3 is loaded
     // into the slot k-step j - 1 has just released.  So at the tap loop's back-edge --
@@ -1078,21 +319,11 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
-    // SIB_PROBE (timing probes, wrong results): 1 = every activation read is the
-    // conflict-free pattern of consecutive rows, 2 = every weight load reads k-step 0
-    // (L1-resident: no weight stream), 3 = only the first SIB_PROBE_TAPS of the 9 taps
-    // (the MFMA work a delta convolution would leave)
-#ifndef SIB_PROBE_TAPS
-#define SIB_PROBE_TAPS 5
-#endif
-#ifndef SIB_PROBE
-#define SIB_PROBE 0
-#endif
-#if SIB_PROBE
-#warning "SIB_PROBE is a timing probe: the tree forward's results are wrong in this build"
-#endif
     auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (SIB_PROBE == 2 ? 0 : ks * KS_BYTES) + n * 1024 + lo * LO_BYTES, 0));
+#ifdef DL_PROBE_W  // timing probe (tools/ variant, wrong results): every weight load reads k-step 0
+        ks = 0;
+#endif
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     h8 b[RING][2][2];
 #pragma unroll
@@ -1113,7 +344,7 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
     h8 ah[NT], al[NT];
     int ctr_[NMAX];
 #pragma unroll
-    for (int m = 0; m < NMAX; m++) ctr_[m] = SIB_PROBE == 1 ? m * 16 + (lane & 15) + Wd + 1 : ctr[m];
+    for (int m = 0; m < NMAX; m++) ctr_[m] = ctr[m];
 #pragma unroll
     for (int m = 0; m < NT; m++) {
         nb[m] = (ctr_[m] - Wd - 1 + q * P) * 8;  // tap 0 = (-1, -1)
@@ -1121,7 +352,7 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
         al[m] = *(const h8*)(act + PLANE + nb[m]);
     }
 #pragma unroll 1
-    for (int tap = 0; tap < (SIB_PROBE == 3 ? SIB_PROBE_TAPS : 9); tap++) {
+    for (int tap = 0; tap < 9; tap++) {
         const int t2 = tap + 1 < 9 ? tap + 1 : 0;  // past the last tap: tap 0 again (unused)
         const int toff = (t2 / 3 - 1) * Wd + (t2 % 3 - 1);
 #pragma unroll
@@ -1151,7 +382,7 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
                 if (cq < CQ - 1) {
                     o = nb[m] + (cq + 1) * 4 * P * 8;
                 } else {
-                    nb[m] = (ctr_[m] + (SIB_PROBE == 1 ? 0 : toff) + q * P) * 8;
+                    nb[m] = (ctr_[m] + toff + q * P) * 8;
                     o = nb[m];
                 }
                 ah[m] = *(const h8*)(act + o);
@@ -1195,28 +426,18 @@ __device__ __forceinline__ void sib_conv(const _Float16* act, const int (&ctr)[N
     }
 }
 
-// A node's recomputed squares: plain stores.  SIB_SQ_PLAIN=0 writes them as
-// agent-scope (sc1) stores, which do not keep their lines in the XCD's L2
-// (MI355X_MICROARCH.md, stores), to leave L2 to the roots' maps: HBM-side fetches
-// 220 -> 194 GB per launch but 2.6 % slower (143.1 vs 146.9 ms), so off.
-#ifndef SIB_SQ_PLAIN
-#define SIB_SQ_PLAIN 1
-#endif
-__device__ __forceinline__ void sq_store(_Float16* p, h4 v) {
-    if (SIB_SQ_PLAIN) {
-        *(h4*)p = v;
-    } else {
-        typedef __attribute__((address_space(1))) uint64_t g64;  // a global (not flat) store
-        __hip_atomic_store((g64*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
+// A node's recomputed squares: plain stores.  (Agent-scope (sc1) stores, which do
+// not keep their lines in the XCD's L2, cut HBM-side fetches 220 -> 194 GB per launch
+// but were 2.6 % slower.)
+__device__ __forceinline__ void sq_store(_Float16* p, h4 v) { *(h4*)p = v; }
 
 // conv0's im2col for every unit (16 rows x 32 k fp16 each, the columns tree_node
 // stages), all units in parallel, into col (the head-partials area, dead during y1)
-__device__ __forceinline__ void sib_col(_Float16* col, const SibUnit* U, int ng, int tid) {
+template <class UT>
+__device__ __forceinline__ void sib_col(_Float16* col, const UT* U, int ng, int tid) {
     for (int e = tid; e < ng * 512; e += NTS) {
         const int g = e >> 9, row = (e >> 5) & 15, k = e & 31;
-        const SibUnit& u = U[g];
+        const UT& u = U[g];
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         const Rows r0w = make_rows(cr, cc, 1);
         _Float16 v = (_Float16)0.f;
@@ -1294,18 +515,6 @@ __device__ __forceinline__ void sib_conv0(char* lds, const _Float16* col, const 
     }
 }
 
-// SIB_LAG (8 waves): the second M half's waves start their k-loop SIB_LAG x 64
-// cycles late, so their weight loads follow their partners' and can hit the CU's L1
-#ifndef SIB_LAG
-#define SIB_LAG 0
-#endif
-#ifndef SIB_SKIP_EARLY
-#define SIB_SKIP_EARLY 0  // 1 (skip inputs loaded before the k-loop): -0.5…-1.3 % same box
-#endif
-__device__ __forceinline__ void sib_lag(int mh) {
-    if (SIB_LAG > 0 && mh) __builtin_amdgcn_s_sleep(SIB_LAG);
-}
-
 // The rows of a pass: units u0 .. u0+ng-1 in order, each its recomputed square of
 // radius ro (clipped, row-major), packed back to back; lane li of tile m takes row
 // 16m + li (rows past the end repeat the pass's first row, outputs discarded).
@@ -1362,9 +571,9 @@ __device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, i
 // One map layer (LAYER 0 = y1: X0 r3 windows -> y1 r2; 1 = x1: Y1 r4 -> x1 r3, + x0;
 // 2 = y2: X1 r5 -> y2 r4) over units [u0, u0 + ng): the k-loop, then the epilogue into
 // each node's own square (global)
-template <int LAYER, int NMAX, int G, bool GC, bool TOLDS = false, class Mid>
+template <int LAYER, int NMAX, int G, bool GC, class Mid>
 __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
-                                              int mh, int lane, int32_t* tiles, SibStamp& st, int si, Mid&& mid) {
+                                              int mh, int lane, int32_t* tiles, SibStamp<>& st, int si, Mid&& mid) {
     constexpr int R = LAYER + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = R - 1;
     constexpr int MAPOUT = LAYER + 1, S = 2 * ro + 1, SS = S * S;
     constexpr bool SKIP = LAYER == 1;
@@ -1383,8 +592,8 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
     // x1's skip input (x0): every load of the epilogue in flight at once (rows past the
-    // pass's end read a valid position and are dropped); SIB_SKIP_EARLY: issued before
-    // the k-loop, so they have landed when the barrier after it waits for loads
+    // pass's end read a valid position and are dropped), issued after the k-loop
+    // (before it: -0.5 to -1.3 %), so they have landed when the barrier waits for loads
     h4 skh[2][NMAX], skl[2][NMAX];
     auto skip_loads = [&]() {
 #pragma unroll
@@ -1399,12 +608,10 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
             }
         }
     };
-    if (SKIP && SIB_SKIP_EARLY) skip_loads();
-    sib_lag(mh);
     if (nt > 0) sib_conv<NMAX, R>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* Rw = W + RES0 + LAYER * RES_STRIDE;
-    if (SKIP && !SIB_SKIP_EARLY) skip_loads();
+    if (SKIP) skip_loads();
     // each row's destination in its node's square, read from the unit table before
     // any store (the stores go through generic pointers the compiler cannot separate
     // from the table)
@@ -1414,17 +621,6 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
         const SibUnit& u = U[tp.g[m]];
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         dst[m] = u.own + PATCH_OFF[MAPOUT] + ((tp.pr[m] - cr + ro) * S + (tp.pc[m] - cc + ro)) * 8;
-    }
-    // TOLDS (y1 only): rows of nodes 0..2 also go to their x1 windows (R 4) at LDS 0
-    constexpr int P1 = 81, W1 = 9;
-    int ldst[NMAX];
-#pragma unroll
-    for (int m = 0; m < NMAX; m++) {
-        ldst[m] = -1;
-        if (TOLDS && tp.g[m] < 3) {
-            const int cell = U[tp.g[m]].cell, cr = cell / BN, cc = cell - (cell / BN) * BN;
-            ldst[m] = tp.g[m] * 2 * 16 * P1 * 8 + ((tp.pr[m] - cr + 4) * W1 + (tp.pc[m] - cc + 4)) * 8;
-        }
     }
     f32x4 es[2], et[2];
 #pragma unroll
@@ -1458,11 +654,6 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
             _Float16* d = dst[m] + (ch0 >> 3) * SS * 8 + (ch0 & 7);
             sq_store(d, hi);
             sq_store(d + 16 * SS * 8, lo);
-            if (TOLDS && ldst[m] >= 0) {
-                _Float16* l = (_Float16*)lds + ldst[m] + (ch0 >> 3) * P1 * 8 + (ch0 & 7);
-                *(h4*)l = hi;
-                *(h4*)(l + 16 * P1 * 8) = lo;
-            }
         }
     }
 }
@@ -1473,7 +664,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
 template <bool GC, class Mid>
 __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, const float* __restrict__ W, int np,
                                                int mh, int lane, float* __restrict__ hpart, int32_t* tiles,
-                                               SibStamp& st, int si, Mid&& mid) {
+                                               SibStamp<>& st, int si, Mid&& mid) {
     constexpr int layer = 3, NMAX = sib_tiles(8);
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
     const Rows rows = make_rows(cr, cc, 5);
@@ -1489,7 +680,8 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     for (int n = 0; n < 2; n++)
 #pragma unroll
         for (int m = 0; m < NMAX; m++) acc[n][m] = zero4();
-    // the skip input (x1): every load in flight at once (SIB_SKIP_EARLY: before the k-loop)
+    // the skip input (x1): every load in flight at once, after the k-loop (issued before
+    // it, held 44 registers: -0.5 to -1.3 %)
     h4 skh[2][NMAX], skl[2][NMAX];
     auto skip_loads = [&]() {
 #pragma unroll
@@ -1504,12 +696,10 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
             }
         }
     };
-    if (SIB_SKIP_EARLY) skip_loads();
-    sib_lag(mh);
     if (nt > 0) sib_conv<NMAX, 6>((const _Float16*)lds, ctr, nt, (const _Float16*)(W + F16_RES0 + layer * F16_STRIDE), 2 * np, lane, acc);
     st(si);
     const float* R = W + RES0 + layer * RES_STRIDE;
-    if (!SIB_SKIP_EARLY) skip_loads();
+    skip_loads();
     f32x4 es[2], et[2], e0[2], e1[2], ev[2];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
@@ -1565,7 +755,8 @@ constexpr int SIB_REC = (HSTRIDE + NTS - 1) / NTS;  // record entries per thread
 
 // node b's head-conv record: its recomputed radius-5 square from hpart (bias, then the
 // 4 pairs' partials in order), the rest copied from its base's record
-__device__ __forceinline__ void sib_record(const SibUnit& u, const float* __restrict__ W, float* __restrict__ hbuf,
+template <class UT>
+__device__ __forceinline__ void sib_record(const UT& u, const float* __restrict__ W, float* __restrict__ hbuf,
                                            const float* __restrict__ hpart, const float (&rec)[SIB_REC], int tid) {
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
     const Rows r4 = make_rows(cr, cc, 5);
@@ -1625,7 +816,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
     const float* W = A.W;
     int32_t* tiles = A.tiles ? A.tiles + (GC ? 1 : 0) : nullptr;
-    SibStamp st;
+    SibStamp<> st;
     // the units of the chunk at pos_ (wave 0, one lane per node)
     auto build = [&](SibUnit* Ud, int pos_, int ng_) {
         if (wave == 0 && lane < ng_) {  // the chunk's nodes
@@ -1653,24 +844,15 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
             Ud[lane] = u;
         }
     };
-    int cur = 0;
-    bool ready = false;  // this chunk's units are built and its x0 windows are in flight
     for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
         __syncthreads();  // the previous chunk's readers of U are done
         const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
-        SibUnit* const U = U0 + cur * SIB_G;
-        if (!ready) {
-            build(U, pos, ng);
-            __syncthreads();
-        }
+        SibUnit* const U = U0;
+        build(U, pos, ng);
+        __syncthreads();
         st(0);
-        const int posn = pos + per * SIB_G;
-        const bool nxt = SIB_NEXT && posn < xe;
-        const int ngn = nxt ? (xe - posn < SIB_G ? xe - posn : SIB_G) : 0;
-        SibUnit* const Un = U0 + (cur ^ 1) * SIB_G;
-        bool built = false;
 #ifdef GZ_PVINC_STAMPS
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n, (unsigned long long)ng);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n[0], (unsigned long long)ng);
 #endif
         // The chunk's passes: y1 over all nodes, x1 in passes of 3, y2 in passes of 2,
         // x2 + heads one node at a time.  After each pass's k-loop, a barrier and then
@@ -1700,7 +882,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
         {
             int t = tid;
             asm volatile("" : "+v"(t));
-            if (!ready) sib_fill<0, GC>(lds, U, 0, ng, t);
+            sib_fill<0, GC>(lds, U, 0, ng, t);
             sib_col((_Float16*)hpart, U, ng, t);
             __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
             st(1);
@@ -1721,8 +903,6 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 pass_of(p + 1, L2, v0, g2);
                 pre = !(L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2);
             }
-            // y1 -> x1: the first x1 pass's windows come from the y1 epilogue + a SKIPOWN fill
-            const bool y1lds = SIB_Y1LDS && p == 0 && npass > 1;
             const float* Wp = W;
             int t = tid;
             asm volatile("" : "+s"(Wp), "+v"(t));
@@ -1731,15 +911,13 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 __syncthreads();
                 st(1);
             }
-            filled = pre || y1lds;
+            filled = pre;
             auto mid = [&]() {
                 __syncthreads();  // every wave is past this pass's k-loop: the windows are free
                 if (pre) fill(L2, v0, g2, t);
-                else if (y1lds) sib_fill<1, GC, true>(lds, U, 0, g2, t);
-                else if (p + 1 == npass && built) sib_fill<0, GC>(lds, Un, 0, ngn, t);  // the next chunk's x0
             };
             if (L == 0) {
-                sib_map_layer<0, sib_tiles(10), SIB_G, GC, SIB_Y1LDS != 0>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
+                sib_map_layer<0, sib_tiles(10), SIB_G, GC>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
             } else if (L == 1) {
                 sib_map_layer<1, sib_tiles(10), 3, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 6, mid);
             } else if (L == 2) {
@@ -1758,15 +936,9 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 st(15);
                 continue;
             }
-            if (nxt && p == 0) {  // wave 0's unit loads drain with the y1 squares' stores
-                build(Un, posn, ngn);
-                built = true;
-            }
             __syncthreads();  // the squares are stored; the next pass's windows have landed
             st(3 * L + 5);
         }
-        if (built) cur ^= 1;
-        ready = built;
     }
 }
 
@@ -1962,6 +1134,643 @@ __global__ void tree_grand_order_kernel(int n, const int32_t* __restrict__ d_cou
     for (int g = h; g >= 0; g = gnext[g]) grand[at++] = g;
 }
 
+// ============================================================ delta (scatter) incremental forward
+// pv_delta_kernel: the root children's forward as a DELTA of the root's (tree mode
+// "delta"; results within the fp32 tolerance of a full forward, not bitwise).  A
+// child's input differs from its root's only in the square of radius L-1 around its
+// stone at layer L's input (x0 r1, y1 r2, x1 r3, y2 r4 for y1, x1, y2, x2), so its
+// pre-BN accumulator is the root's plus the convolution of that difference:
+//     B_child(p) = B_root(p) + sum_t W_t * D(p + t),   D = child - root (zero elsewhere).
+// Scatter form: every row of D (the packed on-board positions of the nodes' squares
+// -- exact row counts, no window of root values) is multiplied by all 9 taps' weights
+// and tap t's product is added to output row p = q - t of an fp32 accumulator in
+// LDS.  Per node that is 164 instead of 276 row-convolutions (the 9 + 25 + 49 + 81
+// changed inputs instead of the 25 + 49 + 81 + 121 changed outputs; 0.59 of the exact
+// incremental forward's MFMA work, 0.67 with tile padding and the board's edges).
+// The epilogue adds the root's accumulator (gz_pvnet.hip's dump of the roots,
+// PV_PRE_FLOATS per layer), applies BN / skip / ReLU as the full kernel does, and
+// writes the node's next difference D = child - root (the root's map value, hi + lo)
+// to its squares; the x2 pass reduces the 1x1 heads as pv_sib_kernel does.
+// Layout and schedule follow pv_sib_kernel: chunks of 6 consecutive children, y1 over
+// all 6, x1 in passes of 3, y2 of 2, x2 + heads one node at a time, 4 waves (wave np:
+// output channels [32 np, 32 np + 32) in the MFMAs, the accumulator RMW and the
+// epilogue, so no two waves ever touch the same accumulator word).  Accumulation is
+// in a fixed order (taps 0..8, each tap's products in the k-loop's order): results
+// are deterministic.  A node with grandchildren also writes its CHILD values (hi/lo,
+// the patch layout) for pv_sib_kernel<true>.
+constexpr int DL_RIN = 112;                      // input rows per pass (7 tiles): y1 6x9, x1 3x25, y2 2x49, x2 81
+constexpr int DL_ROUT = 176;                     // output rows per pass (11 tiles): 150, 147, 162, 121
+constexpr int DL_AS = CH + 4;                    // floats per accumulator row: 528 B spreads rows over the banks
+constexpr int DL_IN_PLANE = 16 * DL_RIN * 8;     // halves per hi / lo plane of the input rows
+constexpr int DL_OFF_ACC = 2 * DL_IN_PLANE * 2;  // bytes
+constexpr int DL_OFF_HP = DL_OFF_ACC + DL_ROUT * DL_AS * 4;
+constexpr int DL_OFF_U = DL_OFF_HP + 4 * 3 * HP_ROWS * 4;
+constexpr int LDS_D = DL_OFF_U + SIB_G * 128;
+static_assert(LDS_D <= 160 * 1024, "LDS budget");
+static_assert(4 * 3 * HP_ROWS * 4 >= SIB_G * 512 * 2, "conv0's im2col fits the head partials");
+
+struct DlUnit {
+    const _Float16* gm;  // the root's maps x0, y1, x1, y2 (hi / lo)
+    _Float16* own;       // this node's differences D (patch layout), workgroup scratch
+    _Float16* patch;     // its patch slot (child values for its grandchildren), or nullptr
+    const float* pre;    // the root's pre-BN accumulators of y1, x1, y2, x2
+    int leaf, base, cell, pad0;
+    int pad[4];
+    uint32_t board[16];  // the node's bit-plane board (conv0's input)
+};
+static_assert(sizeof(DlUnit) == 128, "unit size");
+
+// per pass, for its g <= G nodes and radius R: each node's clipped square (row-major)
+// and its first row in the pass -- wave-uniform (scalar registers)
+template <int G>
+struct DlGeo {
+    int start[G + 1], r0[G], c0[G], wr[G], n[G];
+};
+template <int G>
+__device__ __forceinline__ DlGeo<G> dl_geo(const DlUnit* U, int ng, int R) {
+    DlGeo<G> o;
+    o.start[0] = 0;
+#pragma unroll
+    for (int h = 0; h < G; h++) {
+        Rows q = make_rows(0, 0, 0);
+        q.n = 0;
+        if (h < ng) {
+            const int cell = __builtin_amdgcn_readfirstlane(U[h].cell);
+            q = make_rows(cell / BN, cell % BN, R);
+        }
+        o.r0[h] = q.r0;
+        o.c0[h] = q.c0;
+        o.wr[h] = q.wr;
+        o.n[h] = q.n;
+        o.start[h + 1] = o.start[h] + q.n;
+    }
+    return o;
+}
+// row i of the pass -> its node g and position (pr, pc); valid = false past the rows
+template <int G>
+__device__ __forceinline__ bool dl_row(const DlGeo<G>& geo, int i, int& g, int& pr, int& pc) {
+    g = 0;
+#pragma unroll
+    for (int h = 1; h < G; h++) g += i >= geo.start[h] ? 1 : 0;
+    int j = i, R0 = 0, C0 = 0, WR = 1;
+#pragma unroll
+    for (int h = 0; h < G; h++)
+        if (h == g) {
+            j = i - geo.start[h];
+            R0 = geo.r0[h];
+            C0 = geo.c0[h];
+            WR = geo.wr[h];
+        }
+    const int rr = (int)(((float)j + 0.5f) / (float)WR);  // exact: j < 121, WR <= 11
+    pr = R0 + rr;
+    pc = C0 + (j - rr * WR);
+    return i < geo.start[G];
+}
+
+// The pass's scatter k-loop for the wave's n-tiles {nt0, nt0 + 1} over its NT input
+// tiles: per tap the 4 k-steps of the full kernel's k-loop (3 products each),
+// started from zero, then added into the accumulator rows q - t (read during the
+// tap's first k-step, written after its last; a wave's own LDS accesses stay in
+// order).  pr / pc: the lane's input row position (pr < -1: no row); ob / ow: its
+// node's output row of position (pr, pc) and the output square's width.  A lane
+// whose row q - t is off the board reads and writes the trash row DL_TRASH (no exec
+// masks).  Weights: a ring of 4 k-steps, refilled 3 k-steps ahead; issue order per
+// k-step: tile 0's MFMAs, then the refill, then the other tiles, so the wait the
+// compiler puts at the loop header covers only loads issued a k-step earlier.  (Taps
+// in pairs with an 8-deep ring spill 110+ registers.)
+constexpr int DL_TRASH = DL_ROUT - 1;
+template <int NT, int NMAX>
+__device__ __forceinline__ void dl_conv_nt(const _Float16* in, float* acc, const int (&pr)[NMAX],
+                                           const int (&pc)[NMAX], const int (&ob)[NMAX], const int (&ow)[NMAX],
+                                           const _Float16* __restrict__ Wf, int nt0, int lane) {
+    constexpr int CQ = 4, KS = 9 * CQ, RING = 4;
+    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
+    const int q = lane >> 4, li = lane & 15;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = (nt0 * 64 + lane) * 16;
+    auto wload = [&](int ks, int n, int lo) -> h8 {
+#ifdef DL_PROBE_W  // timing probe (tools/ variant, wrong results): every weight load reads k-step 0
+        ks = 0;
+#endif
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+    };
+    h8 b[RING][2][2];
+#pragma unroll
+    for (int c = 0; c < RING - 1; c++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            b[c][n][0] = wload(c, n, 0);
+            b[c][n][1] = wload(c, n, 1);
+        }
+    // B operand: row 16 m + li of the input rows, channel group cq * 4 + q -- the same
+    // for every tap (the scatter form reads each row at its own position), so all of
+    // it is read once and held (NT x 32 registers; MFMAs take B from AGPRs too): the
+    // only LDS traffic of the taps is the accumulator rows' read-add-write
+    const _Float16* bp = in + (q * DL_RIN + li) * 8;
+    h8 ah[NT][CQ], al[NT][CQ];
+#pragma unroll
+    for (int m = 0; m < NT; m++)
+#pragma unroll
+        for (int cq = 0; cq < CQ; cq++) {
+            ah[m][cq] = *(const h8*)(bp + m * 128 + cq * 4 * DL_RIN * 8);
+            al[m][cq] = *(const h8*)(bp + DL_IN_PLANE + m * 128 + cq * 4 * DL_RIN * 8);
+        }
+    const int cl = nt0 * 16 + 4 * q;  // the lane's first accumulator channel
+    int base[NT], step[NT];           // float offset of output row (pr, pc); per output row
+#pragma unroll
+    for (int m = 0; m < NT; m++) {
+        base[m] = ob[m] * DL_AS + cl;
+        step[m] = ow[m] * DL_AS;
+    }
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap++) {
+        constexpr int h = 0;
+        const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+        int ad[NT];
+        f32x4 old[2][NT];
+        f32x4 c[2][NT];
+#pragma unroll
+        for (int cq = 0; cq < CQ; cq++) {
+            const int sl = (h * CQ + cq) % RING, sr = (h * CQ + cq + RING - 1) % RING;
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[m][cq], cq == 0 ? zero4() : c[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[m][cq], c[n][m], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[m][cq], c[n][m], 0, 0, 0);
+                if (m == 0) {  // k-step ks + RING - 1 into the slot of ks - 1 (past the end: unused)
+                    const int ksr = tap * CQ + cq + RING - 1;
+                    const int kn = ksr < KS ? ksr : ksr - KS;
+#pragma unroll
+                    for (int n2 = 0; n2 < 2; n2++) {
+                        b[sr][n2][0] = wload(kn, n2, 0);
+                        b[sr][n2][1] = wload(kn, n2, 1);
+                    }
+                }
+#ifdef DL_PROBE_NORMW
+                if (false) {
+#else
+                if (cq == 0) {  // this tap's output row and its current sum
+#endif
+                    const int r = pr[m] - dy, cc = pc[m] - dx;
+                    const bool ok = (unsigned)r < (unsigned)BN && (unsigned)cc < (unsigned)BN;
+                    ad[m] = ok ? base[m] - dy * step[m] - dx * DL_AS : DL_TRASH * DL_AS + cl;
+#ifndef DL_ATOMIC
+                    old[0][m] = *(const f32x4*)(acc + ad[m]);
+                    old[1][m] = *(const f32x4*)(acc + ad[m] + 16);
+#endif
+                }
+#ifdef DL_PROBE_NORMW
+                if (false) {
+#else
+                if (cq == CQ - 1 && m > 0) {  // the previous tile's sum is complete
+#endif
+#ifdef DL_ATOMIC
+#pragma unroll
+                    for (int n = 0; n < 2; n++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++)
+                            __hip_atomic_fetch_add(acc + ad[m - 1] + 16 * n + r, c[n][m - 1][r], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+                    *(f32x4*)(acc + ad[m - 1]) = old[0][m - 1] + c[0][m - 1];
+                    *(f32x4*)(acc + ad[m - 1] + 16) = old[1][m - 1] + c[1][m - 1];
+#endif
+                }
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA (tile 0)
+            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);  // VMEM read
+#pragma unroll
+            for (int m = 1; m < NT; m++) __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA
+        }
+#ifdef DL_PROBE_NORMW
+        f32x4 keep = zero4();
+#pragma unroll
+        for (int m = 0; m < NT; m++) keep += c[0][m] + c[1][m];
+        if (keep[0] == 1234.5f) acc[cl] = keep[1];  // keep the MFMAs alive
+#elif defined(DL_ATOMIC)
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                __hip_atomic_fetch_add(acc + ad[NT - 1] + 16 * n + r, c[n][NT - 1][r], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+        *(f32x4*)(acc + ad[NT - 1]) = old[0][NT - 1] + c[0][NT - 1];
+        *(f32x4*)(acc + ad[NT - 1] + 16) = old[1][NT - 1] + c[1][NT - 1];
+#endif
+    }
+}
+
+template <int NMAX>
+__device__ __forceinline__ void dl_conv(const _Float16* in, float* acc, int nt, const int (&pr)[NMAX],
+                                        const int (&pc)[NMAX], const int (&ob)[NMAX], const int (&ow)[NMAX],
+                                        const _Float16* __restrict__ Wf, int nt0, int lane) {
+    static_assert(NMAX == 7, "tile counts");
+    switch (nt) {
+        case 1: dl_conv_nt<1, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 2: dl_conv_nt<2, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 3: dl_conv_nt<3, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 4: dl_conv_nt<4, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 5: dl_conv_nt<5, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 6: dl_conv_nt<6, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        case 7: dl_conv_nt<7, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
+        default: break;
+    }
+}
+
+// hi / lo of the 4 channels at ch0 of position pos in a root map (x0, y1, x1, y2) or a
+// node's square of radius R (patch layout), as fp32
+__device__ __forceinline__ f32x4 dl_map4(const _Float16* m, int ch0, int pos) {
+    const _Float16* p = m + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);
+    const h4 h = *(const h4*)p, l = *(const h4*)(p + PV_MAP_PLANE);
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = (float)h[r] + (float)l[r];
+    return v;
+}
+// raw hi / lo halves of 4 channels (converted where they are used, so that a
+// pipelined load phase never waits for its own loads)
+struct H4x2 {
+    h4 h, l;
+};
+__device__ __forceinline__ H4x2 dl_map4_raw(const _Float16* m, int ch0, int pos) {
+    const _Float16* p = m + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);
+    return H4x2{*(const h4*)p, *(const h4*)(p + PV_MAP_PLANE)};
+}
+__device__ __forceinline__ H4x2 dl_sq4_raw(const _Float16* sq, int SS, int ch0, int idx) {
+    const _Float16* p = sq + ((ch0 >> 3) * SS + idx) * 8 + (ch0 & 7);
+    return H4x2{*(const h4*)p, *(const h4*)(p + 16 * SS * 8)};
+}
+__device__ __forceinline__ float h2f(const H4x2& x, int r) { return (float)x.h[r] + (float)x.l[r]; }
+__device__ __forceinline__ void dl_put_sq(_Float16* sq, int SS, int ch0, int idx, const f32x4& v) {
+    h4 hi, lo;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const _Float16 h = (_Float16)v[r];
+        hi[r] = h;
+        lo[r] = (_Float16)(v[r] - (float)h);
+    }
+    _Float16* p = sq + ((ch0 >> 3) * SS + idx) * 8 + (ch0 & 7);
+    *(h4*)p = hi;
+    *(h4*)(p + 16 * SS * 8) = lo;
+}
+
+// One pass of layer LAYER (0 y1, 1 x1, 2 y2, 3 x2 + heads) over nodes U[0, g): the
+// scatter k-loop over the nodes' difference rows (radius LAYER + 1) into the
+// accumulator rows of their output squares (radius LAYER + 2); then, for every output
+// row of the wave, the loads of the epilogue are issued at once -- the root's pre-ReLU
+// value z (gz_pvnet.hip's dump: BN(acc) [+ the skip input]) and, for x1 / x2 near the
+// stone, the difference of the skip input -- before the caller's barrier (mid: the
+// barrier and the next pass's fill), so their latency hides behind it; then
+//   child = relu(z + s * sum [+ D(skip)]),  root = relu(z),  D = child - root
+// into the node's square LAYER + 1 (the child value into its patch); x2 reduces the
+// child values into the 1x1 heads' partials instead.  The accumulator rows read go
+// back to zero.  NMO: output tiles of the pass at most.
+template <int LAYER, int G, int NMO, class Mid>
+__device__ __forceinline__ void dl_pass(const _Float16* in, float* acc, const DlUnit* U, int g,
+                                        const float* __restrict__ W, int np, int lane, int32_t* tiles,
+                                        float* __restrict__ hpart, Mid&& mid) {
+    constexpr int NMAX = 7, RO = LAYER + 2, S = 2 * RO + 1, SS = S * S;
+    constexpr bool SKIP = LAYER == 1 || LAYER == 3;
+    constexpr int RS = LAYER == 1 ? 1 : 3;  // radius of the skip input's difference (x0 r1, x1 r3)
+    constexpr int SS_SK = (2 * RS + 1) * (2 * RS + 1);
+    const DlGeo<G> gi = dl_geo<G>(U, g, LAYER + 1), go = dl_geo<G>(U, g, RO);
+    const int q = lane >> 4, li = lane & 15;
+    {
+        const int nt = (gi.start[G] + 15) >> 4;
+        if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);
+        int pr[NMAX], pc[NMAX], ob[NMAX], ow[NMAX];
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            int h, r, c;
+            const bool v = dl_row<G>(gi, m * 16 + li, h, r, c);
+            int b = 0, w = 1;
+#pragma unroll
+            for (int k = 0; k < G; k++)
+                if (k == h) {
+                    w = go.wr[k];
+                    b = go.start[k] + (r - go.r0[k]) * w + (c - go.c0[k]);
+                }
+            pr[m] = v ? r : -64;
+            pc[m] = c;
+            ob[m] = b;
+            ow[m] = w;
+        }
+        dl_conv<NMAX>(in, acc, nt, pr, pc, ob, ow, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np,
+                      lane);
+    }
+    const int nto = (go.start[G] + 15) >> 4;
+    f32x4 z[2][NMO];
+    H4x2 dsk[2][NMO];
+    int hh[NMO], sq[NMO];
+    bool near[NMO];
+#pragma unroll
+    for (int mo = 0; mo < NMO; mo++) {
+        int h, pr, pc;
+        const bool v = dl_row<G>(go, mo * 16 + li, h, pr, pc) && mo < nto;
+        const DlUnit& u = U[v ? h : 0];
+        const int cell = u.cell, cr = cell / BN, cc = cell - cr * BN;
+        const int pos = v ? pr * BN + pc : 0;
+        hh[mo] = v ? h : -1;
+        sq[mo] = (pr - cr + RO) * S + (pc - cc + RO);
+        near[mo] = SKIP && iabs(pr - cr) <= RS && iabs(pc - cc) <= RS;
+        const int ssq = near[mo] ? (pr - cr + RS) * (2 * RS + 1) + (pc - cc + RS) : 0;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * q;
+            z[n][mo] = *(const f32x4*)(u.pre + LAYER * PV_PRE_FLOATS + pos * CH + ch0);
+            if constexpr (SKIP) dsk[n][mo] = dl_sq4_raw(u.own + PATCH_OFF[LAYER - 1], SS_SK, ch0, ssq);
+        }
+    }
+    const float* Rw = W + RES0 + LAYER * RES_STRIDE;
+    f32x4 es[2], e0[2], e1[2], ev[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int ch0 = (2 * np + n) * 16 + 4 * q;
+        es[n] = *(const f32x4*)(Rw + RES_S + ch0);
+        if (LAYER == 3) {
+            e0[n] = *(const f32x4*)(W + P_W + ch0);
+            e1[n] = *(const f32x4*)(W + P_W + CH + ch0);
+            ev[n] = *(const f32x4*)(W + V_W + ch0);
+        }
+    }
+    mid();  // every wave's taps are in the accumulator rows; the next pass's fill is in flight
+#pragma unroll
+    for (int mo = 0; mo < NMO; mo++) {
+        if (mo >= nto) continue;
+        const int i = mo * 16 + li;
+        const bool v = hh[mo] >= 0;
+        float s0 = 0.f, s1 = 0.f, sv = 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * q;
+            float* ap = acc + (v ? i : 0) * DL_AS + ch0;
+            const f32x4 a = *(const f32x4*)ap;
+            f32x4 y, d;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float dk = 0.f;
+                if constexpr (SKIP) dk = near[mo] ? h2f(dsk[n][mo], r) : 0.f;
+                float tc = __builtin_fmaf(a[r], es[n][r], z[n][mo][r]) + dk;
+                tc = tc > 0.f ? tc : 0.f;
+                if (LAYER == 3) {
+                    s0 = __builtin_fmaf(e0[n][r], tc, s0);
+                    s1 = __builtin_fmaf(e1[n][r], tc, s1);
+                    sv = __builtin_fmaf(ev[n][r], tc, sv);
+                } else {
+                    const float tr = z[n][mo][r] > 0.f ? z[n][mo][r] : 0.f;
+                    y[r] = tc;
+                    d[r] = tc - tr;
+                }
+            }
+            if (v) {
+                if (LAYER < 3) {
+                    const DlUnit& u = U[hh[mo]];
+                    dl_put_sq(u.own + PATCH_OFF[LAYER + 1], SS, ch0, sq[mo], d);
+                    if (u.patch) dl_put_sq(u.patch + PATCH_OFF[LAYER + 1], SS, ch0, sq[mo], y);
+                }
+                *(f32x4*)ap = zero4();
+            }
+        }
+        if (LAYER == 3) {
+            s0 += __shfl_xor(s0, 16);
+            s1 += __shfl_xor(s1, 16);
+            sv += __shfl_xor(sv, 16);
+            s0 += __shfl_xor(s0, 32);
+            s1 += __shfl_xor(s1, 32);
+            sv += __shfl_xor(sv, 32);
+            if (lane < 16 && v) {
+                hpart[(np * 3 + 0) * HP_ROWS + i] = s0;
+                hpart[(np * 3 + 1) * HP_ROWS + i] = s1;
+                hpart[(np * 3 + 2) * HP_ROWS + i] = sv;
+            }
+        }
+    }
+}
+
+// conv0 + BN + ReLU at the <= 9 positions around each node's stone (as sib_conv0),
+// then D(x0) = child - root into the y1 pass's input rows (LDS) and the node's square
+__device__ __forceinline__ void dl_conv0(_Float16* in, const _Float16* col, const DlUnit* U, int ng,
+                                         const float* __restrict__ W, int np, int lane) {
+    const int li = lane & 15, q = lane >> 4;
+    const DlGeo<SIB_G> gi = dl_geo<SIB_G>(U, ng, 1);
+    h8 wh[2], wl[2];
+    f32x4 ws[2], wt[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int nt = 2 * np + n, ch0 = nt * 16 + 4 * q;
+        const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
+        wh[n] = *(const h8*)wf;
+        wl[n] = *(const h8*)(wf + 8 * 64 * 8);
+        ws[n] = *(const f32x4*)(W + C0_S + ch0);
+        wt[n] = *(const f32x4*)(W + C0_T + ch0);
+    }
+#pragma unroll
+    for (int g = 0; g < SIB_G; g++) {
+        if (g >= ng) break;
+        const h8 a = *(const h8*)(col + g * 512 + li * 32 + 8 * q);
+        const DlUnit& u = U[g];
+        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+        const bool rowok = li < gi.n[g];
+        const int wr = gi.wr[g];
+        const int rr = rowok ? (int)(((float)li + 0.5f) / (float)wr) : 0;
+        const int pr = gi.r0[g] + rr, pc = gi.c0[g] + (li - rr * wr), pos = pr * BN + pc;
+        const int row = gi.start[g] + li, idx = (pr - cr + 1) * 3 + (pc - cc + 1);
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * q;
+            f32x4 acc = zero4();
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a, acc, 0, 0, 0);
+            if (rowok) {
+                const f32x4 rt = dl_map4(u.gm, ch0, pos);
+                f32x4 y, d;
+                h4 dh, dl;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float t = __builtin_fmaf(acc[r], ws[n][r], wt[n][r]);
+                    t = t > 0.f ? t : 0.f;
+                    y[r] = t;
+                    d[r] = t - rt[r];
+                    const _Float16 hh = (_Float16)d[r];
+                    dh[r] = hh;
+                    dl[r] = (_Float16)(d[r] - (float)hh);
+                }
+                _Float16* ip = in + ((ch0 >> 3) * DL_RIN + row) * 8 + (ch0 & 7);
+                *(h4*)ip = dh;
+                *(h4*)(ip + DL_IN_PLANE) = dl;
+                dl_put_sq(u.own + PATCH_OFF[0], 9, ch0, idx, d);
+                if (u.patch) dl_put_sq(u.patch + PATCH_OFF[0], 9, ch0, idx, y);
+            }
+        }
+    }
+}
+
+// the input rows of layer L (L >= 1: the nodes' D squares of map L, radius L + 1) for
+// nodes U[0, g), by LDS-DMA: position-major, a lane's row then its 32 planes
+template <int G>
+__device__ __forceinline__ void dl_fill(_Float16* in, const DlUnit* U, int g, int L, int tid) {
+    const int R = L + 1, S = 2 * R + 1, SS = S * S, off = L == 1 ? PATCH_OFF[1] : (L == 2 ? PATCH_OFF[2] : PATCH_OFF[3]);
+    const DlGeo<G> gi = dl_geo<G>(U, g, R);
+    const int rows = gi.start[G], nb = (rows + 63) >> 6;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int w = wave; w < nb * 8; w += NTS / 64) {  // (64-row block, group of 4 planes)
+        const int blk = w >> 3, p0 = (w & 7) * 4, i = blk * 64 + lane;
+        int h, pr, pc;
+        const bool v = dl_row<G>(gi, i, h, pr, pc);
+        const _Float16* src = (const _Float16*)gz_sib_zero16;
+        int stride = 0;
+        if (v) {
+            const DlUnit& u = U[h];
+            const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+            src = u.own + off + ((pr - cr + R) * S + (pc - cc + R)) * 8 + p0 * SS * 8;
+            stride = SS * 8;
+        }
+        char* dst = (char*)in + ((size_t)p0 * DL_RIN + blk * 64) * 16;
+        if (i < DL_RIN) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                __builtin_amdgcn_global_load_lds((glb_void_t*)(src + k * stride), (lds_void_t*)(dst + k * DL_RIN * 16), 16,
+                                                 0, 0);
+        }
+    }
+}
+
+// list: the root children (tree_children_kernel), list_count entries; scratch: SIB_G
+// patch-sized areas per workgroup (the nodes' D squares)
+__global__ __launch_bounds__(NTS, 1) void pv_delta_kernel(TreeArgs A, _Float16* __restrict__ scratch,
+                                                          const int32_t* __restrict__ list,
+                                                          const int32_t* __restrict__ list_count) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_D];
+    DlUnit* const U = (DlUnit*)(lds + DL_OFF_U);
+    _Float16* const in = (_Float16*)lds;
+    float* const acc = (float*)(lds + DL_OFF_ACC);
+    float* const hpart = (float*)(lds + DL_OFF_HP);
+    const int count = *list_count;
+    const int nx = gridDim.x >= 8 ? 8 : 1;
+    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
+    if (k >= per) return;
+    const int xchunk = (count + nx - 1) / nx;
+    const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+    _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3;
+    const float* W = A.W;
+    int32_t* tiles = A.tiles;
+    SibStamp<16> st;  // phases: 0 units, 1 conv0, 2 exposed fills, 3..6 k-loops, 7 barrier, 8..11 epilogues, 12 record, 13 barrier
+    for (int i = tid; i < DL_ROUT * DL_AS / 4; i += NTS) ((f32x4*)acc)[i] = zero4();
+    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
+        __syncthreads();  // the previous chunk's readers of U are done
+        const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
+        if (wave == 0 && lane < ng) {
+            const int b = list[pos + lane];
+            DlUnit u;
+            const int ci = A.cinfo[b];
+            const int o = (ci >> 8) & 0x3fffff;
+            u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
+            u.pre = A.pres + (size_t)o * 4 * PV_PRE_FLOATS;
+            u.leaf = b;
+            u.cell = ci & 0xff;
+            u.base = A.meta[b];
+            u.own = myscr + (size_t)lane * PATCH_HALVES;
+            const int ps = A.pslot[b];
+            u.patch = ps >= 0 ? A.patches + (size_t)ps * PATCH_HALVES : nullptr;
+            u.pad0 = 0;
+#pragma unroll
+            for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
+            U[lane] = u;
+        }
+        __syncthreads();
+        st(0);
+#ifdef GZ_PVINC_STAMPS
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n[1], (unsigned long long)ng);
+#endif
+        {
+            int t = tid;
+            asm volatile("" : "+v"(t));
+            sib_col((_Float16*)hpart, U, ng, t);
+            __syncthreads();
+            const float* Wp = W;
+            asm volatile("" : "+s"(Wp));
+            dl_conv0(in, (const _Float16*)hpart, U, ng, Wp, np, t & 63);
+            __syncthreads();  // the y1 input rows are in LDS, D(x0) in the squares
+            st(1);
+        }
+        const int nx1 = (ng + 2) / 3, ny2 = (ng + 1) / 2, npass = 1 + nx1 + ny2 + ng;
+        auto pass_of = [&](int p, int& L, int& u0, int& g) {
+            if (p == 0) {
+                L = 0, u0 = 0, g = ng;
+            } else if (p <= nx1) {
+                L = 1, u0 = 3 * (p - 1), g = ng - u0 < 3 ? ng - u0 : 3;
+            } else if (p <= nx1 + ny2) {
+                L = 2, u0 = 2 * (p - 1 - nx1), g = ng - u0 < 2 ? ng - u0 : 2;
+            } else {
+                L = 3, u0 = p - 1 - nx1 - ny2, g = 1;
+            }
+        };
+        auto fill = [&](int L, int u0, int g, int t) {
+            if (L == 1) dl_fill<3>(in, U + u0, g, 1, t);
+            else if (L == 2) dl_fill<2>(in, U + u0, g, 2, t);
+            else if (L == 3) dl_fill<1>(in, U + u0, g, 3, t);
+        };
+        bool filled = true;  // y1's input rows: dl_conv0
+        for (int p = 0; p < npass; p++) {
+            int L, u0, g, L2 = 0, v0 = 0, g2 = 0;
+            pass_of(p, L, u0, g);
+            // the next pass's input rows can be loaded as soon as this pass's k-loop is
+            // done unless this pass's epilogue writes them
+            bool pre = p + 1 < npass;
+            if (pre) {
+                pass_of(p + 1, L2, v0, g2);
+                pre = !(L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2);
+            }
+            const float* Wp = W;
+            int t = tid;
+            asm volatile("" : "+s"(Wp), "+v"(t));
+            if (!filled) {
+                fill(L, u0, g, t);
+                __syncthreads();
+                st(2);
+            }
+            auto mid = [&]() {
+                st(3 + L);
+                __syncthreads();  // every tap is in the accumulator rows; the input rows are free
+                st(7);
+                if (pre) fill(L2, v0, g2, t);
+            };
+            if (L == 0) {
+                dl_pass<0, SIB_G, 10>(in, acc, U, g, Wp, np, t & 63, tiles, hpart, mid);
+            } else if (L == 1) {
+                dl_pass<1, 3, 10>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
+            } else if (L == 2) {
+                dl_pass<2, 2, 11>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
+            } else {
+                float rec[SIB_REC];  // the root's record entries of this thread
+#pragma unroll
+                for (int kk = 0; kk < SIB_REC; kk++) {
+                    const int j = t + kk * NTS;
+                    rec[kk] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
+                }
+                dl_pass<3, 1, 8>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
+                __syncthreads();  // hpart complete
+                st(11);
+                sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
+                st(12);
+            }
+            filled = pre;
+            if (L < 3) st(8 + L);
+            __syncthreads();  // the squares are stored; the accumulator rows are zero again
+            st(13);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" void gz_internal_set_error(const char* msg);
@@ -1996,44 +1805,41 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     return GZ_OK;
 }
 
+// delta != 0: the root children through pv_delta_kernel (d_pres: the roots' pre-BN
+// accumulators), else pv_sib_kernel (bitwise); grandchildren always pv_sib_kernel<true>
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         void* stream) {
-    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
-    // GZ_PVINC_SIB=0: the one-node-per-workgroup kernels (A/B reference for tools/ab.sh)
-    static const int sib = [] {
-        const char* e = getenv("GZ_PVINC_SIB");
-        return e ? atoi(e) : 1;
-    }();
+                                         int delta, const float* d_pres, void* stream) {
+    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles, d_pres};
     hipStream_t s = (hipStream_t)stream;
-    if (sib) {
+    if (delta)
+        pv_delta_kernel<<<grid, NTS, 0, s>>>(A, d_scratch, d_children, d_nchildren);
+    else
         pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_children, d_nchildren);
-        pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
-    } else {
-        pv_child_kernel<<<grid, NTC, 0, s>>>(A, n, d_count);
-        pv_grandchild_kernel<<<grid, NTC, 0, s>>>(A, d_grand, d_ngrand);
-    }
+    pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        gz_internal_set_error((std::string("pv_child_kernel: ") + hipGetErrorString(e)).c_str());
+        gz_internal_set_error((std::string("tree children: ") + hipGetErrorString(e)).c_str());
         return GZ_ERR_HIP;
     }
     return GZ_OK;
 }
 
 #ifdef GZ_PVINC_STAMPS
-// out[0..15] = ticks per phase, out[16] = children of workgroup 0
+// phase stamps of workgroup 0 (-DGZ_PVINC_STAMPS builds, tools/pvinc_bench.py)
 extern "C" int gz_pvinc_stamps_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_pvinc_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(gz_pvinc_stamps_n), sizeof(unsigned long long)) != hipSuccess) return -1;
+    // out[0..31] = ticks per phase (pv_sib_kernel, then pv_delta_kernel), out[32..33] = their nodes
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_pvinc_stamps), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(gz_pvinc_stamps_n), 2 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvinc_stamps), z, sizeof(z)) != hipSuccess) return -1;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvinc_stamps_n), z, sizeof(z[0])) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvinc_stamps_n), z, 2 * sizeof(z[0])) != hipSuccess) return -1;
     }
     return 0;
 }

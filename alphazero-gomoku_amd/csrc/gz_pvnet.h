@@ -55,6 +55,10 @@ constexpr int TOTAL = V1_P + V1_KB * V1_NT * 256;
 // [256 rows][8] then the lo plane -- PV_MAP_HALVES halves per map
 constexpr int PV_MAP_PLANE = CH * 256;
 constexpr int PV_MAP_HALVES = 2 * PV_MAP_PLANE;
+// delta tree forward (gz_pvinc.hip, pv_delta_kernel): a root board's pre-ReLU values
+// of the 4 residual layers (y1, x1, y2, x2: z = BN(conv) [+ skip input]), fp32
+// position-major [256 positions][128 channels] -- PV_PRE_FLOATS floats per layer
+constexpr int PV_PRE_FLOATS = 256 * CH;
 // per-board record of the 1x1 head convs' outputs between the tower and the FC heads
 // (gz_pvnet.hip / gz_pvinc.hip -> pv_heads_kernel): hp [0, 450) channel-major, zero to
 // HP_K; hv [HV_OFF, HV_OFF + 225), zero to HSTRIDE

@@ -159,12 +159,15 @@ __device__ __forceinline__ void f16_load(const ActF16x3& act, f32x4 (&out)[2][NM
 // intermediate maps for the incremental forward of its children (gz_pvinc.hip)
 template <bool SKIP>
 __device__ __forceinline__ void pv_put4(ActF16x3& act, const f32x4& acc, const f32x4& s, const f32x4& t,
-                                        const f32x4& skip, int ch0, int pos, _Float16* __restrict__ g) {
+                                        const f32x4& skip, int ch0, int pos, _Float16* __restrict__ g,
+                                        float* __restrict__ pre) {
     h4 hi, lo;
+    f32x4 z;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         float y = __builtin_fmaf(acc[r], s[r], t[r]);
         if (SKIP) y += skip[r];
+        z[r] = y;
         y = y > 0.f ? y : 0.f;
         const _Float16 h = (_Float16)y;
         hi[r] = h;
@@ -177,12 +180,16 @@ __device__ __forceinline__ void pv_put4(ActF16x3& act, const f32x4& acc, const f
         *(h4*)(g + o) = hi;
         *(h4*)(g + PV_MAP_PLANE + o) = lo;
     }
+    if (pre) *(f32x4*)(pre + pos * CH + ch0) = z;
 }
+
+// pre (root boards of the delta tree forward, else nullptr): the layer's pre-ReLU
+// values z = BN(acc) (+ the skip input), [pos][128] fp32
 
 template <int NM, bool SKIP>
 __device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][NM], const float* __restrict__ S,
                                           const float* __restrict__ T, const f32x4 (&skip)[2][NM], int np, int m0,
-                                          int lane, _Float16* __restrict__ g) {
+                                          int lane, _Float16* __restrict__ g, float* __restrict__ pre) {
     asm volatile("" : "+v"(lane));  // addresses are recomputed per layer, not hoisted (and spilled)
     lane &= 63;
 #pragma unroll
@@ -192,7 +199,7 @@ __device__ __forceinline__ void f16_store(ActF16x3& act, const f32x4 (&acc)[2][N
 #pragma unroll
         for (int m = 0; m < NM; m++) {
             const int pos = (m0 + m) * 16 + (lane & 15);
-            if (pos < POS) pv_put4<SKIP>(act, acc[n][m], s, t, skip[n][m], ch0, pos, g);
+            if (pos < POS) pv_put4<SKIP>(act, acc[n][m], s, t, skip[n][m], ch0, pos, g, pre);
         }
     }
 }
@@ -205,7 +212,7 @@ template <int NM>
 __device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const float* __restrict__ W,
                                                 const float* __restrict__ S, const float* __restrict__ T,
                                                 const f32x4 (&skip)[2][NM], int np, int m0, int lane,
-                                                float* __restrict__ hpart) {
+                                                float* __restrict__ hpart, float* __restrict__ pre) {
     asm volatile("" : "+v"(lane));
     lane &= 63;
     float s0[NM], s1[NM], sv[NM];
@@ -217,6 +224,16 @@ __device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const
         const f32x4 s = *(const f32x4*)(S + ch0), t = *(const f32x4*)(T + ch0);
         const f32x4 w0 = *(const f32x4*)(W + P_W + ch0), w1 = *(const f32x4*)(W + P_W + CH + ch0);
         const f32x4 wv = *(const f32x4*)(W + V_W + ch0);
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = (m0 + m) * 16 + (lane & 15);
+            if (pre && pos < POS) {
+                f32x4 z;
+#pragma unroll
+                for (int r = 0; r < 4; r++) z[r] = __builtin_fmaf(acc[n][m][r], s[r], t[r]) + skip[n][m][r];
+                *(f32x4*)(pre + pos * CH + ch0) = z;
+            }
+        }
 #pragma unroll
         for (int m = 0; m < NM; m++)
 #pragma unroll
@@ -246,10 +263,12 @@ __device__ __forceinline__ void f16_store_heads(const f32x4 (&acc)[2][NM], const
     }
 }
 
-// gmaps: nullptr, or the root's 4 map copies (x0, y1, x1, y2); y1, x1, y2 are stored here
+// gmaps: nullptr, or the root's 4 map copies (x0, y1, x1, y2); y1, x1, y2 are stored here.
+// gpre: nullptr, or the root's 4 pre-ReLU maps (PV_PRE_FLOATS each)
 template <int NM, int m0>
 __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict__ W, int wave, int lane,
-                                          float* __restrict__ hpart, _Float16* __restrict__ gmaps) {
+                                          float* __restrict__ hpart, _Float16* __restrict__ gmaps,
+                                          float* __restrict__ gpre) {
     const int np = wave & 3;
     for (int blk = 0; blk < 2; blk++) {
         f32x4 skip[2][NM];
@@ -269,14 +288,15 @@ __device__ __forceinline__ void f16_tower(ActF16x3& act, const float* __restrict
             __syncthreads();
             PV_WAVE_STAMP(16);
             PV_STAMP(3);
+            float* pre = gpre ? gpre + (size_t)layer * PV_PRE_FLOATS : nullptr;
             if (half == 0)
                 f16_store<NM, false>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane,
-                                     gmaps ? gmaps + (size_t)(1 + layer) * PV_MAP_HALVES : nullptr);
+                                     gmaps ? gmaps + (size_t)(1 + layer) * PV_MAP_HALVES : nullptr, pre);
             else if (blk == 0)
                 f16_store<NM, true>(act, acc, R + RES_S, R + RES_T, skip, np, m0, lane,
-                                    gmaps ? gmaps + (size_t)2 * PV_MAP_HALVES : nullptr);
+                                    gmaps ? gmaps + (size_t)2 * PV_MAP_HALVES : nullptr, pre);
             else
-                f16_store_heads<NM>(acc, W, R + RES_S, R + RES_T, skip, np, m0, lane, hpart);
+                f16_store_heads<NM>(acc, W, R + RES_S, R + RES_T, skip, np, m0, lane, hpart, pre);
             __syncthreads();
             PV_STAMP(4);
         }
@@ -328,7 +348,7 @@ __device__ __forceinline__ void conv0_f16(ActF16x3& act, const float* __restrict
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, a[m], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, a[m], acc, 0, 0, 0);
         const int pos = m * 16 + li;
-        if (pos < POS) pv_put4<false>(act, acc, s, t, none, ch0, pos, g);
+        if (pos < POS) pv_put4<false>(act, acc, s, t, none, ch0, pos, g, nullptr);
     }
 }
 
@@ -603,7 +623,8 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
                                                          const int32_t* __restrict__ list,
                                                          const int32_t* __restrict__ list_count,
                                                          const int32_t* __restrict__ ord,
-                                                         _Float16* __restrict__ maps, int root_cap) {
+                                                         _Float16* __restrict__ maps, int root_cap,
+                                                         float* __restrict__ pres = nullptr) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const Smem sm = smem_layout(lds);
     ActF16x3 act;
@@ -618,9 +639,13 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
     for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
         const int b = LIST ? list[li_] : li_;
         _Float16* gm = nullptr;
+        float* gp = nullptr;
         if (DUMP) {
             const int o = ord[b];
-            if (o >= 0 && o < root_cap) gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
+            if (o >= 0 && o < root_cap) {
+                gm = maps + (size_t)o * 4 * PV_MAP_HALVES;
+                if (pres) gp = pres + (size_t)o * 4 * PV_PRE_FLOATS;
+            }
         }
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
@@ -636,9 +661,9 @@ __global__ __launch_bounds__(NT16, 1) void pv_kernel_f16x3(const float* __restri
         __syncthreads();
         PV_STAMP(1);
         if (wave >> 2)
-            f16_tower<PV_YOUNG_TILES, PV_SPLIT>(act, W, wave, lane, sm.hpart, gm);
+            f16_tower<PV_YOUNG_TILES, PV_SPLIT>(act, W, wave, lane, sm.hpart, gm, gp);
         else
-            f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart, gm);
+            f16_tower<PV_SPLIT, 0>(act, W, wave, lane, sm.hpart, gm, gp);
         int tid_h = threadIdx.x;  // re-read: a pinned tid kept live across the tower is spilled
         asm volatile("" : "+v"(tid_h));
         // the 1x1 head convs' outputs go to HBM; the FC heads run batched over boards
@@ -949,7 +974,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         void* stream);
+                                         int delta, const float* d_pres, void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -960,8 +985,9 @@ struct TreeWs {
     float* hbuf;
     int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *cinfo, *children, *ghead, *ctr;
     _Float16* maps;
+    float* pres;        // the roots' pre-BN accumulators (pv_delta_kernel)
     _Float16* patches;
-    _Float16* scratch;  // pv_sib_kernel: 6 patch-sized areas per workgroup
+    _Float16* scratch;  // pv_sib_kernel / pv_delta_kernel: 6 patch-sized areas per workgroup
 };
 TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
@@ -982,6 +1008,8 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     p += al256((size_t)patch_cap_of(root_cap) * 4);
     t.maps = (_Float16*)p;
     p += (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16);
+    t.pres = (float*)p;
+    p += (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_PRE_FLOATS * sizeof(float);
     t.patches = (_Float16*)p;
     p += (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16);
     t.scratch = (_Float16*)p;
@@ -994,13 +1022,19 @@ extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
     return al256(m * HSTRIDE * sizeof(float)) + 7 * al256(m * 4) + al256((m + m / 64 + 1) * 4) + 256 +
            al256((size_t)patch_cap_of(root_cap) * 4) +
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
+           (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_PRE_FLOATS * sizeof(float) +
            (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16) +
            (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
 }
 
-extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
-                                  const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
-                                  float* d_probs, double* d_prior, void* d_workspace, void* stream) {
+extern "C" int gz_pv_forward_tree_mode(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
+                                       int32_t n, const int32_t* d_count, int32_t root_cap, float* d_logits,
+                                       float* d_value, float* d_probs, double* d_prior, void* d_workspace,
+                                       int32_t mode, void* stream) {
+    if (mode != GZ_TREE_EXACT && mode != GZ_TREE_DELTA) {
+        gz_internal_set_error("gz_pv_forward_tree_mode: unknown mode");
+        return GZ_ERR_ARG;
+    }
     if (n < 0 || root_cap < 0 || (n > 0 && (!d_weights || !d_boards || !d_meta || !d_logits || !d_value || !d_workspace))) {
         gz_internal_set_error("gz_pv_forward_tree: bad arguments");
         return GZ_ERR_ARG;
@@ -1020,13 +1054,14 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     // roots (full forward, maps stored), then every board without a stored root or
     // patch (full forward), then the roots' children and their children (incremental);
     // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed]
+    const bool delta = mode == GZ_TREE_DELTA;
     pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
-                                                     t.ord, t.maps, root_cap);
+                                                     t.ord, t.maps, root_cap, delta ? t.pres : nullptr);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
                                    t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, t.children, t.ctr + 2, grid,
-                                   stream);
+                                   delta ? 1 : 0, t.pres, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
@@ -1038,8 +1073,15 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     return GZ_OK;
 }
 
+extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
+                                  const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
+                                  float* d_probs, double* d_prior, void* d_workspace, void* stream) {
+    return gz_pv_forward_tree_mode(d_weights, d_boards, d_meta, n, d_count, root_cap, d_logits, d_value, d_probs,
+                                   d_prior, d_workspace, GZ_TREE_EXACT, stream);
+}
+
 // the 16-row MFMA tiles of the residual convs the last tree forward's incremental
-// kernels executed: [root children, grandchildren] (0 with GZ_PVINC_SIB=0)
+// kernels executed: [root children, grandchildren]
 extern "C" int gz_pv_tree_exec_tiles(const void* d_workspace, int32_t n, int32_t* d_out2, void* stream) {
     TreeWs t = tree_carve((void*)d_workspace, n, 0);
     if (hipMemcpyAsync(d_out2, t.ctr + 8, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) {

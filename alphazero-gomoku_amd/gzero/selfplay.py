@@ -33,7 +33,9 @@ class SelfPlayEngine:
         pv_mode: "full" = one full forward per node (gz_pv_forward); "tree" = the
         incremental forward (gz_pv_forward_tree: a root's children and grandchildren
         recompute only the windows around their new stone; bit-identical outputs;
-        f16x3 only)."""
+        f16x3 only); "delta" = the incremental forward with the root children as the
+        root's pre-BN accumulators plus the convolution of their input differences
+        (gz_pv_forward_tree_mode GZ_TREE_DELTA: within 1e-4 of the full forward)."""
         self.lib = require_gpu()
         self.n_slots = int(n_slots)
         self.plies_per_step = int(plies_per_step)
@@ -51,11 +53,13 @@ class SelfPlayEngine:
             self.gn_stats(reset=True)
         self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
             else PVWeights(pv_weights)
-        if pv_mode not in ("full", "tree"):
-            raise ValueError(f"pv_mode must be 'full' or 'tree', not {pv_mode!r}")
-        self.tree = pv_mode == "tree" and self.gather
+        if pv_mode not in ("full", "tree", "delta"):
+            raise ValueError(f"pv_mode must be 'full', 'tree' or 'delta', not {pv_mode!r}")
+        self.tree = pv_mode in ("tree", "delta") and self.gather
+        self.tree_mode = _lib.GZ_TREE_DELTA if pv_mode == "delta" else _lib.GZ_TREE_EXACT
+        self.pv_mode = pv_mode if self.gather else "full"
         if self.tree and self.pv_weights.mode != _lib.GZ_PV_F16X3:
-            raise ValueError("pv_mode='tree' needs f16x3 weights")
+            raise ValueError(f"pv_mode={pv_mode!r} needs f16x3 weights")
         S = self.params.num_simulations
         slot_bytes = self.lib.gz_slot_bytes(S)
         self.d_slots = torch.zeros(self.n_slots * slot_bytes, dtype=torch.uint8, device="cuda")
@@ -137,10 +141,11 @@ class SelfPlayEngine:
             return
         d_count = self.d_counters[4:8]  # counters.leaves
         if self.tree:
-            _lib.check(self.lib.gz_pv_forward_tree(ptr(self.pv_weights.tensor), ptr(self.d_leaves), ptr(self.d_meta),
-                                                   self.leaf_cap, ptr(d_count), self.root_cap, ptr(self.d_logits),
-                                                   ptr(self.d_value), ptr(self.d_probs), ptr(self.d_prior),
-                                                   ptr(self.d_tree_ws), stream()), "gz_pv_forward_tree")
+            _lib.check(self.lib.gz_pv_forward_tree_mode(ptr(self.pv_weights.tensor), ptr(self.d_leaves),
+                                                        ptr(self.d_meta), self.leaf_cap, ptr(d_count), self.root_cap,
+                                                        ptr(self.d_logits), ptr(self.d_value), ptr(self.d_probs),
+                                                        ptr(self.d_prior), ptr(self.d_tree_ws), self.tree_mode,
+                                                        stream()), "gz_pv_forward_tree_mode")
             return
         _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
                                           ptr(d_count), ptr(self.d_logits), ptr(self.d_value),

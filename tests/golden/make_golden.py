@@ -964,6 +964,24 @@ def part_planner_mcts():
     dump("planner_mcts", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
 
 
+def part_planner_mcts200():
+    """reference searches at config 4's own settings -- 200
+    simulations, planner_steps 5, medium -- from positions with >= 27 stones (so
+    the sequential UCB phase runs after the parallel one), every planner call
+    recorded.  ~20 min of reference CPU time per search."""
+    import random as pyrandom
+    rng = pyrandom.Random(41)
+    tasks = []
+    for k in range(4):
+        L = rng.randint(27, 44)
+        mv = gen_moves(rng, L, True, True) if k % 2 == 0 else gen_quiet(rng, L)
+        tasks.append((7100 + k, mv, 200, [0.2, 0.0][k // 2], "medium", 5))
+    with Pool(4) as pool:
+        out = pool.map(_planner_mcts_task, tasks, chunksize=1)
+    out.sort(key=lambda r: r["game_id"])
+    dump("planner_mcts200", {"seed": SEED, "gn_seed": GN_SEED, "dqn_seed": DQN_SEED, "cases": out})
+
+
 # ---------------------------------------------------------------------------
 # G9 dataset + SGD (training.py:104-134,277-337,430-454): the dataset's sample
 # order / labels / planes, and two epochs of training.main's optimiser loop
@@ -1163,6 +1181,7 @@ def part_arena():
 PARTS = {"board": part_board, "pattern": part_pattern, "policy": part_policy,
          "rollout": part_rollout, "mcts": part_mcts, "mcts2": part_mcts2, "pvnet": part_pvnet, "prior": part_prior, "pvnet2": part_pvnet2, "augment": part_augment,
          "games": part_games, "gnet": part_gnet, "planner": part_planner, "planner_mcts": part_planner_mcts,
+         "planner_mcts200": part_planner_mcts200,
          "sgd": part_sgd, "arena": part_arena, "arena_plans": part_arena_plans}
 
 if __name__ == "__main__":
