@@ -124,6 +124,55 @@ def test_plan_search_exact_vs_oracle(oracle, gnw, idx):
     assert [float(x) for x in t["value"][:n]] == ot["value"]
 
 
+@pytest.mark.parametrize("idx", range(4))
+def test_plan_search_200_sims_exact_vs_oracle(oracle, gnw, idx):
+    """Config 4's settings at full depth (tests/golden planner_mcts200: 200
+    simulations, planner_steps 5, medium, 32-39 stones -- parallel then sequential
+    phase): the GPU search equals the oracle driven by the GPU's net outputs -- move,
+    draws, predicts and the whole tree, fp64 values bit for bit."""
+    from gzero import device
+    g = golden("planner_mcts200")
+    c = g["cases"][idx]
+    b, st = _state(oracle, c["moves"])
+    cp, ex = DIFF[c["difficulty"]]
+    p = device.search_params(c["sims"], cp, ex, c["beta"], SEED)
+    p.planner_steps = c["planner_steps"]
+    mv, stats, trees, _ = device.plan_search(st, [c["game_id"]], p, _lib.planner_params(c["difficulty"]), gnw,
+                                             want_trees=True)
+    prm = oracle.make_params(c["difficulty"], sims=c["sims"], beta=c["beta"], seed=SEED,
+                             planner_steps=c["planner_steps"], pq=_pq_from_gpu(gnw))
+    om, ot = oracle.get_move(b, b.player, prm, c["game_id"])
+    assert int(mv[0]) == om
+    assert stats[0]["main_draws"] == ot["main_draws"] and stats[0]["sim_draws"] == ot["sim_draws"]
+    assert stats[0]["predicts"] == ot["predicts"]
+    t = trees[0]
+    n = len(ot["parent"])
+    assert [int(x) for x in t["parent"][:n]] == ot["parent"]
+    assert [int(x) for x in t["visits"][:n]] == ot["visits"]
+    assert [float(x) for x in t["value"][:n]] == ot["value"]
+
+
+def test_plan_search_200_sims_vs_reference(oracle, gnw):
+    """The 4 reference searches at 200 simulations / planner_steps 5: same move and
+    root children as the reference, or -- where one differs -- a recorded planner
+    decision inside it that the nets' rounding flips at a near-tie (<= 1e-6)."""
+    from gzero import device
+    g = golden("planner_mcts200")
+    for c in g["cases"]:
+        _, st = _state(oracle, c["moves"])
+        cp, ex = DIFF[c["difficulty"]]
+        p = device.search_params(c["sims"], cp, ex, c["beta"], SEED)
+        p.planner_steps = c["planner_steps"]
+        mv, stats, trees, _ = device.plan_search(st, [c["game_id"]], p, _lib.planner_params(c["difficulty"]), gnw,
+                                                 want_trees=True)
+        t = trees[0]
+        kids = [i for i in range(len(t["move"])) if t["parent"][i] == 0]
+        got = [[int(t["move"][i]), int(t["visits"][i]), float(t["value"][i])] for i in kids]
+        if not (int(mv[0]) == c["move"] and got == c["children"]):
+            gaps = planner_net_flips(c["calls"], gnw, _lib.PLANNER[c["difficulty"]][1])
+            assert gaps and max(gaps) <= 1e-6, (c["game_id"], gaps)
+
+
 def test_plan_search_vs_reference(oracle, gnw):
     """All 20 reference searches: same move / root statistics, or -- for each
     search that differs -- a recorded planner decision inside it that the nets'

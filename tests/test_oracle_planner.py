@@ -146,6 +146,49 @@ def test_planner_search_vs_reference(idx):
         assert kids == c["children"]
 
 
+@pytest.mark.parametrize("idx", range(4))
+def test_planner_search_200_sims_vs_reference(idx):
+    """Config 4's own settings (tests/golden planner_mcts200.json.gz, make_golden.py
+    part_planner_mcts200): reference searches at 200 simulations with 5 planner plies
+    (medium, beta 0.2 and 0.0) from positions with 32-39 stones, so the parallel
+    phase (every root child) is followed by sequential UCB simulations.  With the
+    reference's recorded net outputs injected, in call order, the oracle makes the
+    same ~1,000 planner calls on the same boards and returns the reference's move,
+    draw counts, predict count and every root child's (move, visits, fp64 value)."""
+    g = golden("planner_mcts200")
+    c = g["cases"][idx]
+    calls = c["calls"]
+    pos = [0]
+
+    def pq(board, game_id, sim, step):
+        i = pos[0]
+        assert i < len(calls)
+        call = calls[i]
+        assert call["sim"] == sim and _board_str(board) == call["board"], (i, sim, step)
+        pos[0] += 1
+        p = np.zeros(225, np.float32)
+        q = np.zeros(225, np.float32)
+        p[call["top"]] = _hexf(call["p"])
+        q[call["top"]] = _hexf(call["q"])
+        return p, q
+
+    b = O.new_board(c["moves"])
+    prm = O.make_params(c["difficulty"], sims=c["sims"], beta=c["beta"], seed=g["seed"],
+                        planner_steps=c["planner_steps"], pq=pq)
+    with O.Trace() as tr:
+        mv, tree = O.get_move(b, b.player, prm, c["game_id"])
+    assert pos[0] == len(calls)
+    assert tr.planner_moves == [call["move"] for call in calls]
+    assert mv == c["move"]
+    assert tree["main_draws"] == c["main_draws"] and tree["sim_draws"] == sum(c["sim_draws"])
+    assert tree["predicts"] == c["predicts"]
+    assert tree["visits"][0] == c["root_visits"] and tree["value"][0] == c["root_value"]
+    kids = [[tree["move"][i], tree["visits"][i], tree["value"][i]]
+            for i in range(len(tree["parent"])) if tree["parent"][i] == 0]
+    assert kids == c["children"]
+    assert len(kids) < c["sims"] - 1  # the sequential phase ran
+
+
 def _replay_arena_case(g, c, perturb=None):
     """Replay one arena_plans case in the oracle, every planner call fed the
     reference's recorded net outputs IN ORDER, and check what the games' moves
