@@ -12,13 +12,6 @@
 
 namespace gzc {
 
-// Diagnostic only (tools/Makefile variants, never in the product build): 1 = every
-// k-step reads k-step (ks & 1)'s weight fragments (wrong results, L1-resident weights):
-// an upper bound for what any cut in the weight stream can buy.
-#ifndef F16_WPROBE
-#define F16_WPROBE 0
-#endif
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -118,7 +111,7 @@ __device__ __forceinline__ void f16_conv(const ActF16x3& act, const _Float16* __
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = ((2 * np) * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (F16_WPROBE ? (ks & 1) : ks) * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     h8 b[2][2];
 #pragma unroll

@@ -271,19 +271,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
 // (bg_planner.py:68-78) for HB (32) boards per workgroup as fp32-MFMA GEMMs over
 // the records gn_kernel left (heads_gemm_block, gz_f16conv.h).  DQN fc0 on the one-hot
 // planes = base + the (colour - empty) delta rows of the stones (gz_gnet.h): a GEMM
-// with K = 450 over the record's stone inputs (GN_HSKIP: only the k-blocks holding
-// a stone on one of the workgroup's boards).  Wave w: n-tiles {w, w+4, w+8, w+12}.
-#ifndef GN_HB
-#define GN_HB 32  // boards per workgroup: 32 -> 66 KB of LDS, two workgroups per CU
-#endif
-constexpr int HB = GN_HB;
+// with K = 450 over the record's stone inputs (only the k-blocks holding a stone on
+// one of the workgroup's boards).  Wave w: n-tiles {w, w+4, w+8, w+12}.
+constexpr int HB = 32;  // boards per workgroup: 66 KB of LDS, two workgroups per CU
 constexpr int HMT = HB / 16;  // M tiles (16 boards each)
 constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;   // logits rows
 constexpr int H_STRIDE = 260;    // DQN hidden rows (16 B apart in bank space per row)
-#ifndef GN_HPF
-#define GN_HPF 1  // k-blocks of A/B fragments loaded ahead in heads_gemm (1 or 2)
-#endif
 static_assert(REC_X == 29 * 16 && REC - REC_X == 29 * 16 && REC % 4 == 0 && REC_X % 16 == 0 && H_STRIDE % 4 == 0, "16-B A loads");
 
 // heads_gemm_block's products in its order, with the next k-block's A and B fragments
@@ -304,29 +298,6 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
         for (int q = 0; q < 4; q++)
             b[q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
     };
-#if GN_HPF == 2
-    // two k-blocks in flight: the block after next is loaded while the current one's
-    // MFMAs run (the buffers rotate by value; the unrolled loop renames them)
-    f32x4 a0[HMT], b0[4], a1[HMT], b1[4];
-    load(0, a0, b0);
-    if (KB > 1) load(1, a1, b1);
-#pragma unroll 3
-    for (int kb = 0; kb < KB; kb++) {
-        f32x4 a2[HMT], b2[4];
-        if (kb + 2 < KB) load(kb + 2, a2, b2);
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int m = 0; m < HMT; m++)
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[m][t], b0[q][t], acc[m][q], 0, 0, 0);
-#pragma unroll
-        for (int m = 0; m < HMT; m++) a0[m] = a1[m], a1[m] = a2[m];
-#pragma unroll
-        for (int q = 0; q < 4; q++) b0[q] = b1[q], b1[q] = b2[q];
-    }
-#else
     f32x4 a[2][HMT], b[2][4];
     load(0, a[0], b[0]);
 #pragma unroll 2
@@ -341,17 +312,13 @@ __device__ __forceinline__ void heads_gemm(const float* __restrict__ Wp, int lan
                 for (int q = 0; q < 4; q++)
                     if (q < ntn) acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][m][t], b[cur][q][t], acc[m][q], 0, 0, 0);
     }
-#endif
 }
 
-// GN_HSKIP 1: DQN fc0 over the k-blocks of the one-hot stone inputs that hold a stone
+// DQN fc0 over the k-blocks of the one-hot stone inputs that hold a stone
 // on at least one of the workgroup's boards (mask: bit kb).  A skipped block's
 // products are all zero, and adding them leaves every accumulator bit unchanged (the
 // accumulators start at +0 and never become -0), so the outputs are bitwise those of
 // the dense GEMM
-#ifndef GN_HSKIP
-#define GN_HSKIP 1
-#endif
 template <int NTILES>
 __device__ __forceinline__ void heads_gemm_mask(const float* __restrict__ Wp, int lane, const int (&nt)[4], int ntn,
                                                 f32x4 (&acc)[HMT][4], const float* __restrict__ arow[HMT], uint32_t mask) {
@@ -444,7 +411,6 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
         ntn_p += nt[q] < 15;
     }
     f32x4 acc[HMT][4];
-#if GN_HSKIP
     // the fc0 k-blocks with a stone on any of this workgroup's boards (visible after the
     // barrier that follows the policy FC)
     __shared__ uint32_t kmask;
@@ -467,7 +433,6 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
         }
         if (mk) atomicOr(&kmask, mk);
     }
-#endif
     // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
     heads_gemm<REC_X / 16, 15>(W + GF_P, lane, nt, ntn_p, acc, arow);
     heads_put<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
@@ -506,11 +471,7 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
         const float* ax[HMT];
 #pragma unroll
         for (int m = 0; m < HMT; m++) ax[m] = arow[m] + REC_X;
-#if GN_HSKIP
         heads_gemm_mask<16>(W + D0_P, lane, nt, 4, acc, ax, kmask);
-#else
-        heads_gemm<(REC - REC_X) / 16, 16>(W + D0_P, lane, nt, 4, acc, ax);
-#endif
         heads_put<true>(acc, W + D0_BASE, DQH, nt, 4, lane, rb, H_STRIDE);
     }
     __syncthreads();  // rb complete; ra (logits) no longer read
@@ -561,10 +522,7 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
 // Every output element takes gn_kernel's products in gn_kernel's order (the same
 // k-steps, MFMA operand splits and epilogues), so the records -- and p, q from
 // gn_heads_kernel -- are bitwise those of the full forward.
-#ifndef GN_IG
-#define GN_IG 3  // boards per chunk (1: 4 waves and 2 workgroups per CU)
-#endif
-constexpr int IG = GN_IG;
+constexpr int IG = 3;  // boards per chunk
 constexpr int IMH = IG == 1 ? 1 : 2;      // M parts: waves = 4 n-tiles x IMH
 constexpr int NTI = 256 * IMH;            // wave: n-tile wave & 3, M part wave >> 2
 constexpr int IWG = IG == 1 ? 2 : 1;      // workgroups per CU
@@ -720,17 +678,9 @@ __device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng
     }
 }
 
-#ifndef IG_PROBE
-#define IG_PROBE 0
-#endif
 // tiles per group of the 3x3 k-loop: a group's 3 products interleave over its tiles, so
 // an MFMA's accumulator was last written GT - 1 MFMAs earlier
-#ifndef IG_GT
-#define IG_GT 3  // 6: ±0 (28 spilled VGPRs)
-#endif
-#if IG_PROBE
-#warning "IG_PROBE is a timing probe: the incremental GraphNet's results are wrong in this build"
-#endif
+constexpr int IG_GT = 3;
 
 // compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
 template <class F, int... I>
@@ -753,8 +703,7 @@ __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt * 64 + lane) * 16;
     auto wload = [&](int ks, int lo) -> h8 {
-        // (IG_PROBE 2, timing only: every k-step reads k-step 0 / 1's fragments, L1-resident)
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, (IG_PROBE == 2 ? (ks & 1) : ks) * 4096 + lo * KS * 4096, 0));
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * 4096 + lo * KS * 4096, 0));
     };
     h8 b[4][2];
 #pragma unroll
@@ -782,11 +731,7 @@ __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr
             if (m < NT) {
                 const int o = c8[m] + toff(tap) + CQ * 4 * P * 8;
                 fa[PB][j][0] = *(const h8*)(act + o);
-#if IG_PROBE == 1  // timing probe (wrong results): no lo-plane activation reads (half the LDS reads)
-                fa[PB][j][1] = fa[PB][j][0];
-#else
                 fa[PB][j][1] = *(const h8*)(act + LO + o);
-#endif
             }
         }
     };
@@ -828,18 +773,8 @@ __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr
             __builtin_amdgcn_sched_group_barrier(0x008, 3 * tiles_of(g), 0);  // MFMA
         }, std::make_integer_sequence<int, NK * NG>{});
     };
-#ifndef IG_UNROLL
-#define IG_UNROLL 0  // 1: 2 % slower (same box), 5 minutes of compile
-#endif
-#if IG_UNROLL
-    // fully unrolled: no loop back-edge, where the compiler would wait for every
-    // outstanding weight load (vmcnt(0)) instead of the one it needs
-    ig_sfor([&](auto tp_) { constexpr int tp = decltype(tp_)::value; ksteps(std::integral_constant<int, 4>{}, 4 * tp, 2 * tp); },
-            std::make_integer_sequence<int, 4>{});
-#else
 #pragma unroll 1
     for (int tp = 0; tp < 4; tp++) ksteps(std::integral_constant<int, 4>{}, 4 * tp, 2 * tp);  // taps 2tp, 2tp+1
-#endif
     ksteps(std::integral_constant<int, 2>{}, 16, 8);                                          // tap 8
 #pragma unroll
     for (int m = 0; m < NT; m++) acc[m] = c[m];

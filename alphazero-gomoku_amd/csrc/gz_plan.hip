@@ -648,16 +648,8 @@ __global__ void plan_gn_count_kernel(Workspace w) {
 }
 
 // one planner ply (BGPlannerAI.get_move + make_move) per collected row
-// PLAN_WPE: minimum waves per SIMD for plan_step_kernel (register cap); 0 = the compiler's choice
-#ifndef PLAN_WPE
-#define PLAN_WPE 3  // 3: 178 -> 168 VGPRs, 3 waves per SIMD: config 4 +4.5 % (4: +3 %, 50 spilled VGPRs)
-#endif
-#if PLAN_WPE
-#define PLAN_STEP_ATTR __attribute__((amdgpu_waves_per_eu(PLAN_WPE, 8)))
-#else
-#define PLAN_STEP_ATTR
-#endif
-__global__ __launch_bounds__(WAVE) PLAN_STEP_ATTR void plan_step_kernel(Workspace w, gz_planner_params pp) {
+// (at least 3 waves per SIMD: 178 -> 168 VGPRs, config 4 +4.5 %)
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3, 8))) void plan_step_kernel(Workspace w, gz_planner_params pp) {
     __shared__ PlanShared sh;
     const int row = blockIdx.x;
     if (row >= w.ctr->rows) return;

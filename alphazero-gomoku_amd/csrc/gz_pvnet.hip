@@ -607,12 +607,8 @@ __global__ __launch_bounds__(NT32, 1) void pv_kernel_f32(const float* __restrict
 // (one wave per SIMD with 512 registers and all 15 M tiles per wave measured 37%
 // slower: the compiler serialises the A-fragment reads of a single stream)
 constexpr int NT16 = 512;
-#ifndef PV_SPLIT
-#define PV_SPLIT 8  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
-#endif
-#ifndef PV_YOUNG_TILES
-#define PV_YOUNG_TILES (15 - PV_SPLIT)
-#endif
+constexpr int PV_SPLIT = 8;  // M tiles of the older wave of each SIMD pair (it wins MFMA arbitration)
+constexpr int PV_YOUNG_TILES = 15 - PV_SPLIT;
 // list (optional): the boards to run, list[0 .. *list_count); ord / maps: the
 // root ordinal of every board (-1: none) and the root map area -- a board with
 // 0 <= ord < root_cap also stores its x0, y1, x1, y2 maps (gz_pvinc.hip)
