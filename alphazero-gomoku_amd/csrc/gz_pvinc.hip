@@ -320,9 +320,6 @@ __device__ __forceinline__ void sib_conv_nt(const _Float16* act, const int (&ctr
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
-#ifdef DL_PROBE_W  // timing probe (tools/ variant, wrong results): every weight load reads k-step 0
-        ks = 0;
-#endif
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     h8 b[RING][2][2];
@@ -1249,9 +1246,6 @@ __device__ __forceinline__ void dl_conv_nt(const _Float16* in, float* acc, const
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
-#ifdef DL_PROBE_W  // timing probe (tools/ variant, wrong results): every weight load reads k-step 0
-        ks = 0;
-#endif
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     h8 b[RING][2][2];
@@ -1312,35 +1306,16 @@ __device__ __forceinline__ void dl_conv_nt(const _Float16* in, float* acc, const
                         b[sr][n2][1] = wload(kn, n2, 1);
                     }
                 }
-#ifdef DL_PROBE_NORMW
-                if (false) {
-#else
                 if (cq == 0) {  // this tap's output row and its current sum
-#endif
                     const int r = pr[m] - dy, cc = pc[m] - dx;
                     const bool ok = (unsigned)r < (unsigned)BN && (unsigned)cc < (unsigned)BN;
                     ad[m] = ok ? base[m] - dy * step[m] - dx * DL_AS : DL_TRASH * DL_AS + cl;
-#ifndef DL_ATOMIC
                     old[0][m] = *(const f32x4*)(acc + ad[m]);
                     old[1][m] = *(const f32x4*)(acc + ad[m] + 16);
-#endif
                 }
-#ifdef DL_PROBE_NORMW
-                if (false) {
-#else
                 if (cq == CQ - 1 && m > 0) {  // the previous tile's sum is complete
-#endif
-#ifdef DL_ATOMIC
-#pragma unroll
-                    for (int n = 0; n < 2; n++)
-#pragma unroll
-                        for (int r = 0; r < 4; r++)
-                            __hip_atomic_fetch_add(acc + ad[m - 1] + 16 * n + r, c[n][m - 1][r], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
                     *(f32x4*)(acc + ad[m - 1]) = old[0][m - 1] + c[0][m - 1];
                     *(f32x4*)(acc + ad[m - 1] + 16) = old[1][m - 1] + c[1][m - 1];
-#endif
                 }
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA (tile 0)
@@ -1348,22 +1323,8 @@ __device__ __forceinline__ void dl_conv_nt(const _Float16* in, float* acc, const
 #pragma unroll
             for (int m = 1; m < NT; m++) __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA
         }
-#ifdef DL_PROBE_NORMW
-        f32x4 keep = zero4();
-#pragma unroll
-        for (int m = 0; m < NT; m++) keep += c[0][m] + c[1][m];
-        if (keep[0] == 1234.5f) acc[cl] = keep[1];  // keep the MFMAs alive
-#elif defined(DL_ATOMIC)
-#pragma unroll
-        for (int n = 0; n < 2; n++)
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                __hip_atomic_fetch_add(acc + ad[NT - 1] + 16 * n + r, c[n][NT - 1][r], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
         *(f32x4*)(acc + ad[NT - 1]) = old[0][NT - 1] + c[0][NT - 1];
         *(f32x4*)(acc + ad[NT - 1] + 16) = old[1][NT - 1] + c[1][NT - 1];
-#endif
     }
 }
 

@@ -437,9 +437,10 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--pv-precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="policy-value forward: 3-term fp16 split (f32 accumulate) or exact fp32 MFMA")
-    ap.add_argument("--pv-mode", default="tree", choices=["full", "tree"],
+    ap.add_argument("--pv-mode", default="tree", choices=["full", "tree", "delta"],
                     help="full: one full forward per node; tree: the incremental forward of a root's children "
-                         "(gz_pv_forward_tree, bit-identical outputs)")
+                         "(gz_pv_forward_tree, bit-identical outputs); delta: root children as the root's "
+                         "pre-activations plus a scatter convolution of their input differences (within 2e-5)")
     ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
     ap.add_argument("--elided-plies", type=int, default=20)
     ap.add_argument("--no-elided", action="store_true")
@@ -526,9 +527,11 @@ def main():
                              "forward + masked prior on every non-terminal node the searches create "
                              f"(reference-work mode, {args.pv_precision}"
                              + (", incremental forward of root children and grandchildren: bit-identical outputs"
-                                if eng.tree else "")
+                                if eng.tree and args.pv_mode == "tree" else "")
+                             + (", delta forward of root children (within 2e-5 of the full forward)"
+                                if eng.tree and args.pv_mode == "delta" else "")
                              + ")"),
-                "pv_mode": "tree" if eng.tree else "full",
+                "pv_mode": args.pv_mode if eng.tree else "full",
                 "games_per_gpu": args.slots,
                 "global_games": args.slots * ws,
                 "sims_per_move": args.sims,
@@ -562,7 +565,7 @@ def main():
             "value": round(m4["moves"] / m4["T"], 3), "unit": "moves/s", "steps": args.config4_steps, "warmup": 2,
             "ms_per_step": round(m4["T"] / args.config4_steps * 1e3, 3),
             "pv_boards_per_step": round(float(np.mean(m4["leaves"])), 1),
-            "pv_mode": "tree" if e4.tree else "full",
+            "pv_mode": args.pv_mode if e4.tree else "full",
             "planner_net_rows": {"full_forward": gs["full"], "incremental": gs["incremental"],
                                  "note": "GraphNet rows over the warm-up and timed steps: incremental = boards one "
                                          "stone from kept maps (the search root's, or the rollout's previous "
