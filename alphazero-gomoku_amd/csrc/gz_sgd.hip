@@ -1,0 +1,733 @@
+// gz_sgd.hip -- the policy-value net's residual tower in TRAINING mode (SURVEY §8f
+// row 1: training.py:277-311, the forward/backward of neural_network.py:74-91 and
+// 132-145 with BatchNorm on batch statistics), forward and backward on the device.
+//
+// The tower: a0 = relu(BN0(y0)), then two residual blocks
+//     h = relu(BN1(conv1(a) + b1)),  a' = relu(BN2(conv2(h) + b2) + a)
+// y0 = conv0(x) (3 -> 128 channels) and the heads stay in torch (gzero/sgd.py).
+// Activations are fp32 NHWC [board][225][128].
+//
+// Convolutions (4 forward + 4 input-gradient): one workgroup per (board, half of
+// the output channels), 8 waves; the input plane is staged into LDS as f16 hi/lo
+// (gz_f16conv.h layout) with the producing BatchNorm / ReLU / skip applied on the
+// fly, and gz_f16conv.h's f16x3 implicit GEMM (v_mfma_f32_16x16x32_f16, three
+// products per element, fp32 accumulate) runs the 9 taps x 128 channels.  The
+// input-gradient conv is the same GEMM with the weights transposed and the taps
+// flipped; its operand (the BN input gradient) is scaled by a power of two chosen
+// from a per-channel bound so that its hi/lo halves stay in fp16's normal range.
+// Epilogues write the conv output and each board's per-channel BatchNorm partials
+// (mean, centred sum of squares, max |y|; or sum g, sum g*xhat, max |g|), which a
+// 128-thread kernel combines (Chan's formula, fp64) into the batch statistics,
+// the running-stat update and the backward coefficients.
+// Weight gradients: fp32 MFMA (v_mfma_f32_16x16x4_f32, exact products) over the
+// positions, one workgroup per (tap, group of boards), reading the saved NHWC
+// activations and input gradients directly (a lane's 16 channels are 64
+// contiguous bytes); the groups' partial sums are added by a second kernel.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+
+#include "../../include/gzero.h"
+#include "gz_f16conv.h"
+
+extern "C" void gz_internal_set_error(const char* msg);
+
+namespace {
+using namespace gzc;
+
+constexpr int CH = 128;
+constexpr int NPOS = 225;
+constexpr int LAYERS = 4;   // the residual convs
+constexpr int NBN = 5;      // BN0 + 4
+constexpr int FRAG_HALVES = 36 * 8 * 64 * 8;  // one hi or lo plane of a conv's fragments
+constexpr int CONV_THREADS = 512;
+
+// per-BN coefficient block (floats)
+constexpr int CO_S = 0, CO_T = 128, CO_MEAN = 256, CO_INV = 384, CO_K = 512, CO_MG = 640, CO_MGX = 768,
+              CO_YMAX = 896, CO_SUMXH = 1024, CO_SCALE = 1152, CO_INVSCALE = 1153, CO_FLOATS = 1280;
+constexpr int PART = 3 * CH;  // per board partials
+
+__host__ __device__ constexpr size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+
+// f16x3 A fragments of the four residual convs: [layer][mode][hi, lo][ks 36][n-tile 8][lane 64][8];
+// element (ks, nt, lane, j): output channel n = 16 nt + lane % 16, k = 32 ks + 8 (lane / 16) + j,
+// tap = k / 128, input channel c = k % 128.  mode 0 (forward): w[n][c][tap]; mode 1 (input
+// gradient: conv with taps flipped, channels swapped): w[c][n][8 - tap].
+struct PackArgs {
+    const float* w[LAYERS];
+};
+__global__ void sgd_pack_kernel(PackArgs a, _Float16* __restrict__ frag) {
+    const int per = 2 * FRAG_HALVES;  // elements of one (layer, mode): hi plane index space only
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= LAYERS * 2 * FRAG_HALVES) return;
+    const int lm = e / FRAG_HALVES, i = e - lm * FRAG_HALVES;
+    const int layer = lm >> 1, mode = lm & 1;
+    const int j = i & 7, lane = (i >> 3) & 63, nt = (i >> 9) & 7, ks = i >> 12;
+    const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j, tap = k >> 7, c = k & 127;
+    const float* W = a.w[layer];
+    const float v = mode == 0 ? W[(n * CH + c) * 9 + tap] : W[(c * CH + n) * 9 + (8 - tap)];
+    const _Float16 h = (_Float16)v;
+    _Float16* f = frag + (size_t)lm * per;
+    f[i] = h;
+    f[FRAG_HALVES + i] = (_Float16)(v - (float)h);
+}
+
+// ---------------------------------------------------------------- BN statistics
+// per board: per-channel mean, centred sum of squares and max |y| of y0 (the
+// torch conv0 output; the residual convs produce theirs in their epilogue)
+__global__ __launch_bounds__(256) void sgd_stats_kernel(const float* __restrict__ y, float* __restrict__ part) {
+    __shared__ float red[2][CH];
+    const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
+    const float* yb = y + (size_t)b * NPOS * CH + c;
+    float s = 0.f;
+    for (int p = h; p < NPOS; p += 2) s += yb[(size_t)p * CH];
+    red[h][c] = s;
+    __syncthreads();
+    const float mean = (red[0][c] + red[1][c]) * (1.f / NPOS);
+    __syncthreads();
+    float m2 = 0.f, mx = 0.f;
+    for (int p = h; p < NPOS; p += 2) {
+        const float v = yb[(size_t)p * CH];
+        m2 += (v - mean) * (v - mean);
+        mx = fmaxf(mx, fabsf(v));
+    }
+    red[h][c] = m2;
+    __syncthreads();
+    const float m2t = red[0][c] + red[1][c];
+    __syncthreads();
+    red[h][c] = mx;
+    __syncthreads();
+    if (h == 0) {
+        float* o = part + (size_t)b * PART;
+        o[c] = mean;
+        o[CH + c] = m2t;
+        o[2 * CH + c] = fmaxf(red[0][c], red[1][c]);
+    }
+}
+
+// batch statistics from the boards' partials (equal counts: Chan's combination in
+// fp64), BN scale/shift, the running-stat update (momentum, unbiased variance) --
+// torch BatchNorm2d in training mode
+__global__ __launch_bounds__(128) void sgd_bn_fwd_reduce_kernel(const float* __restrict__ part, int B,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                               float momentum, float eps, float* __restrict__ coef) {
+    const int c = threadIdx.x;
+    double sm = 0.0, mx = 0.0;
+    for (int b = 0; b < B; b++) {
+        sm += part[(size_t)b * PART + c];
+        mx = fmax(mx, (double)part[(size_t)b * PART + 2 * CH + c]);
+    }
+    const double mean = sm / B;
+    double m2 = 0.0, dev = 0.0;
+    for (int b = 0; b < B; b++) {
+        const double d = (double)part[(size_t)b * PART + c] - mean;
+        m2 += part[(size_t)b * PART + CH + c] + (double)NPOS * d * d;
+        dev += (double)NPOS * d;
+    }
+    const double M = (double)NPOS * B;
+    const double var = m2 / M;
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const float s = (float)(gamma[c] * inv);
+    coef[CO_S + c] = s;
+    coef[CO_T + c] = (float)(beta[c] - mean * (double)s);
+    coef[CO_MEAN + c] = (float)mean;
+    coef[CO_INV + c] = (float)inv;
+    coef[CO_YMAX + c] = (float)mx;
+    coef[CO_SUMXH + c] = (float)(dev * inv);
+    if (run_mean) {
+        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
+        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var * (M > 1.0 ? M / (M - 1.0) : 1.0));
+    }
+}
+
+// backward of a BN + ReLU (+ skip) from the boards' partials of g = dL/d(BN output):
+// mean(g), mean(g * xhat), dgamma = sum g xhat, dbeta = sum g, the conv bias gradient
+// (sum of dL/dy over the rows), and the power-of-two scale of dL/dy for the f16x3 GEMM
+__global__ __launch_bounds__(128) void sgd_bn_bwd_reduce_kernel(const float* __restrict__ part, int B,
+                                                               const float* __restrict__ gamma, float* __restrict__ coef,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ dbias) {
+    __shared__ float bmax[2];
+    const int c = threadIdx.x;
+    double sg = 0.0, sgx = 0.0, mg_ = 0.0;
+    for (int b = 0; b < B; b++) {
+        sg += part[(size_t)b * PART + c];
+        sgx += part[(size_t)b * PART + CH + c];
+        mg_ = fmax(mg_, (double)part[(size_t)b * PART + 2 * CH + c]);
+    }
+    const double M = (double)NPOS * B;
+    const double mg = sg / M, mgx = sgx / M;
+    const double inv = coef[CO_INV + c];
+    const double k = (double)gamma[c] * inv;
+    coef[CO_K + c] = (float)k;
+    coef[CO_MG + c] = (float)mg;
+    coef[CO_MGX + c] = (float)mgx;
+    dgamma[c] = (float)sgx;
+    dbeta[c] = (float)sg;
+    // sum over rows of k (g - mg - xhat mgx) = -k mgx sum(xhat)
+    if (dbias) dbias[c] = (float)(-k * mgx * (double)coef[CO_SUMXH + c]);
+    // |dL/dy| <= |k| (max|g| + |mg| + max|xhat| |mgx|), max|xhat| <= (max|y| + |mean|) inv
+    const double xmax = ((double)coef[CO_YMAX + c] + fabs((double)coef[CO_MEAN + c])) * inv;
+    float bound = (float)(fabs(k) * (mg_ + fabs(mg) + xmax * fabs(mgx)));
+    float m = wave_max(bound);
+    if ((c & 63) == 0) bmax[c >> 6] = m;
+    __syncthreads();
+    if (c == 0) {
+        m = fmaxf(bmax[0], bmax[1]);
+        int ex = 0;
+        if (m > 0.f && isfinite(m)) frexpf(m, &ex);  // m < 2^ex
+        int e = 14 - ex;                            // scaled max < 2^14
+        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+        coef[CO_SCALE] = ldexpf(1.f, e);
+        coef[CO_INVSCALE] = ldexpf(1.f, -e);
+    }
+}
+
+// g = dL/da * [a > 0] (the tower output's ReLU) and its BN-backward partials
+__global__ __launch_bounds__(256) void sgd_mask_stats_kernel(const float* __restrict__ da, const float* __restrict__ act,
+                                                            const float* __restrict__ y, const float* __restrict__ coef,
+                                                            float* __restrict__ g, float* __restrict__ part) {
+    __shared__ float red[3][2][CH];
+    const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
+    const float mean = coef[CO_MEAN + c], inv = coef[CO_INV + c];
+    float s = 0.f, sx = 0.f, mx = 0.f;
+    for (int p = h; p < NPOS; p += 2) {
+        const size_t o = ((size_t)b * NPOS + p) * CH + c;
+        const float v = act[o] > 0.f ? da[o] : 0.f;
+        g[o] = v;
+        s += v;
+        sx += v * ((y[o] - mean) * inv);
+        mx = fmaxf(mx, fabsf(v));
+    }
+    red[0][h][c] = s;
+    red[1][h][c] = sx;
+    red[2][h][c] = mx;
+    __syncthreads();
+    if (h == 0) {
+        float* o = part + (size_t)b * PART;
+        o[c] = red[0][0][c] + red[0][1][c];
+        o[CH + c] = red[1][0][c] + red[1][1][c];
+        o[2 * CH + c] = fmaxf(red[2][0][c], red[2][1][c]);
+    }
+}
+
+// dL/dy0 = k (g - mg - xhat mgx) (BN0's input gradient, handed back to torch's conv0)
+__global__ void sgd_bn_dy_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                 const float* __restrict__ coef, float* __restrict__ dy, long long n4) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const int c0 = (int)((i * 4) & 127);
+    const f32x4 gv = ((const f32x4*)g)[i], yv = ((const f32x4*)y)[i];
+    f32x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int c = c0 + r;
+        const float xh = (yv[r] - coef[CO_MEAN + c]) * coef[CO_INV + c];
+        o[r] = coef[CO_K + c] * (gv[r] - coef[CO_MG + c] - xh * coef[CO_MGX + c]);
+    }
+    ((f32x4*)dy)[i] = o;
+}
+
+// the tower output a = relu(y s + t + skip)
+__global__ void sgd_act_kernel(const float* __restrict__ y, const float* __restrict__ coef,
+                               const float* __restrict__ skip, float* __restrict__ out, long long n4) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const int c0 = (int)((i * 4) & 127);
+    const f32x4 yv = ((const f32x4*)y)[i], sv = ((const f32x4*)skip)[i];
+    f32x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const float v = yv[r] * coef[CO_S + c0 + r] + coef[CO_T + c0 + r] + sv[r];
+        o[r] = v > 0.f ? v : 0.f;
+    }
+    ((f32x4*)out)[i] = o;
+}
+
+// ---------------------------------------------------------------- f16x3 convolutions
+struct ConvArgs {
+    // stage: the conv's input plane, computed per element
+    //   forward: x = relu(src s + t (+ skip)), saved to `save` (the activation)
+    //   input gradient: x = k (src - mg - xhat mgx), xhat = (ysrc - mean) inv, saved to
+    //   `save` (dL/dy for the weight gradient) and staged times the scale
+    const float* src;
+    const float* ysrc;
+    const float* skip;
+    const float* coef;
+    float* save;
+    const _Float16* frag;  // the conv's fragments (hi plane, lo plane after it)
+    // forward epilogue: y = acc + bias -> out, BN partials of y -> part
+    const float* bias;
+    // input-gradient epilogue: dx = acc / scale (+ eskip) -> g = dx [eact > 0] -> out,
+    // BN-backward partials of g against the lower BN (ey, ecoef) -> part
+    const float* eskip;
+    const float* eact;
+    const float* ey;
+    const float* ecoef;
+    float* out;
+    float* part;
+};
+
+template <int MODE, int NM>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&acc)[2][NM], int b, int np, int m0,
+                                              int mq, int lane, float (*red)[4][CH], float scale_inv) {
+    const int li = lane & 15, q = lane >> 4;
+    const size_t board = (size_t)b * NPOS;
+    float s[2][4], s2[2][4], mx[2][4];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) s[n][r] = s2[n][r] = mx[n][r] = 0.f;
+    if constexpr (MODE == 0) {
+        f32x4 bias[2];
+#pragma unroll
+        for (int n = 0; n < 2; n++) bias[n] = *(const f32x4*)(a.bias + 16 * (2 * np + n) + 4 * q);
+        f32x4 y[2][NM];
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = 16 * (m0 + m) + li;
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                y[n][m] = acc[n][m] + bias[n];
+                if (pos < NPOS) {
+                    *(f32x4*)(a.out + (board + pos) * CH + 16 * (2 * np + n) + 4 * q) = y[n][m];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) s[n][r] += y[n][m][r];
+                }
+            }
+        }
+        // board mean per channel: lanes li, then the 4 M quarters
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float v = s[n][r];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                v += __shfl_xor(v, 8);
+                if (li == 0) red[0][mq][16 * (2 * np + n) + 4 * q + r] = v;
+            }
+        __syncthreads();
+        float mean[2][4];
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int c = 16 * (2 * np + n) + 4 * q + r;
+                mean[n][r] = (red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]) * (1.f / NPOS);
+            }
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = 16 * (m0 + m) + li;
+            if (pos < NPOS)
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float d = y[n][m][r] - mean[n][r];
+                        s2[n][r] += d * d;
+                        mx[n][r] = fmaxf(mx[n][r], fabsf(y[n][m][r]));
+                    }
+        }
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float v = s2[n][r], w = mx[n][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    v += __shfl_xor(v, o);
+                    w = fmaxf(w, __shfl_xor(w, o));
+                }
+                if (li == 0) {
+                    red[1][mq][16 * (2 * np + n) + 4 * q + r] = v;
+                    red[2][mq][16 * (2 * np + n) + 4 * q + r] = w;
+                }
+            }
+        __syncthreads();
+        if (mq == 0 && li == 0) {
+            float* o = a.part + (size_t)b * PART;
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int c = 16 * (2 * np + n) + 4 * q + r;
+                    o[c] = mean[n][r];
+                    o[CH + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+                    o[2 * CH + c] = fmaxf(fmaxf(red[2][0][c], red[2][1][c]), fmaxf(red[2][2][c], red[2][3][c]));
+                }
+        }
+    } else {
+        f32x4 emean[2], einv[2];
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            emean[n] = *(const f32x4*)(a.ecoef + CO_MEAN + 16 * (2 * np + n) + 4 * q);
+            einv[n] = *(const f32x4*)(a.ecoef + CO_INV + 16 * (2 * np + n) + 4 * q);
+        }
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int pos = 16 * (m0 + m) + li;
+            if (pos >= NPOS) continue;
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const size_t o = (board + pos) * CH + 16 * (2 * np + n) + 4 * q;
+                f32x4 dx = acc[n][m] * scale_inv;
+                if (a.eskip) dx += *(const f32x4*)(a.eskip + o);
+                const f32x4 act = *(const f32x4*)(a.eact + o), yv = *(const f32x4*)(a.ey + o);
+                f32x4 gv;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    gv[r] = act[r] > 0.f ? dx[r] : 0.f;
+                    s[n][r] += gv[r];
+                    s2[n][r] += gv[r] * ((yv[r] - emean[n][r]) * einv[n][r]);
+                    mx[n][r] = fmaxf(mx[n][r], fabsf(gv[r]));
+                }
+                *(f32x4*)(a.out + o) = gv;
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float u = s[n][r], v = s2[n][r], w = mx[n][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    u += __shfl_xor(u, o);
+                    v += __shfl_xor(v, o);
+                    w = fmaxf(w, __shfl_xor(w, o));
+                }
+                if (li == 0) {
+                    const int c = 16 * (2 * np + n) + 4 * q + r;
+                    red[0][mq][c] = u;
+                    red[1][mq][c] = v;
+                    red[2][mq][c] = w;
+                }
+            }
+        __syncthreads();
+        if (mq == 0 && li == 0) {
+            float* o = a.part + (size_t)b * PART;
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int c = 16 * (2 * np + n) + 4 * q + r;
+                    o[c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+                    o[CH + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+                    o[2 * CH + c] = fmaxf(fmaxf(red[2][0][c], red[2][1][c]), fmaxf(red[2][2][c], red[2][3][c]));
+                }
+        }
+    }
+}
+
+// grid (2, boards): workgroup (h, b) computes output channels [64 h, 64 h + 64) of board b;
+// wave w: n-tile pair np = 2 h + (w & 1), M quarter w >> 1 (tiles 4 mq .. 4 mq + 3; 12..14)
+template <int MODE>
+__global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 16 * ROWS16 * 8];
+    __shared__ float red[3][4][CH];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    ActF16x3 act;
+    act.hi = lds;
+    act.lo = lds + 16 * ROWS16 * 8;
+    const size_t board = (size_t)b * NPOS * CH;
+    const bool save = a.save && blockIdx.x == 0;
+    const float scale = MODE == 1 ? a.coef[CO_SCALE] : 1.f;
+    for (int e = tid; e < NPOS * 32; e += CONV_THREADS) {
+        const int p = e >> 5, c0 = (e & 31) * 4;
+        const size_t o = board + (size_t)p * CH + c0;
+        const f32x4 v = *(const f32x4*)(a.src + o);
+        f32x4 x;
+        if constexpr (MODE == 0) {
+            const f32x4 sv = *(const f32x4*)(a.coef + CO_S + c0), tv = *(const f32x4*)(a.coef + CO_T + c0);
+            x = v * sv + tv;
+            if (a.skip) x += *(const f32x4*)(a.skip + o);
+#pragma unroll
+            for (int r = 0; r < 4; r++) x[r] = x[r] > 0.f ? x[r] : 0.f;
+        } else {
+            const f32x4 yv = *(const f32x4*)(a.ysrc + o);
+            const f32x4 mean = *(const f32x4*)(a.coef + CO_MEAN + c0), inv = *(const f32x4*)(a.coef + CO_INV + c0);
+            const f32x4 k = *(const f32x4*)(a.coef + CO_K + c0), mg = *(const f32x4*)(a.coef + CO_MG + c0);
+            const f32x4 mgx = *(const f32x4*)(a.coef + CO_MGX + c0);
+            x = k * (v - mg - (yv - mean) * inv * mgx);
+        }
+        if (save) *(f32x4*)(a.save + o) = x;
+        if constexpr (MODE == 1) x = x * scale;
+        h4 hi, lo;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const _Float16 hh = (_Float16)x[r];
+            hi[r] = hh;
+            lo[r] = (_Float16)(x[r] - (float)hh);
+        }
+        const int lo_off = ActF16x3::off(c0, p);
+        *(h4*)(act.hi + lo_off) = hi;
+        *(h4*)(act.lo + lo_off) = lo;
+    }
+    act.zero_slots(tid, CONV_THREADS, CH);
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63, mq = wave >> 1;
+    const int np = 2 * blockIdx.x + (wave & 1);
+    const float sinv = MODE == 1 ? a.coef[CO_INVSCALE] : 1.f;
+    // quarter 3 has tiles 12..14; its fourth tile (positions 240..255) stays zero and
+    // is skipped by the epilogue (every wave runs the same epilogue and barriers)
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[n][m] = zero4();
+    if (mq < 3) {
+        f16_conv<4, 4, 8, 9>(act, a.frag, np, 4 * mq, lane, acc);
+    } else {
+        f32x4 a3[2][3];
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int m = 0; m < 3; m++) a3[n][m] = zero4();
+        f16_conv<3, 4, 8, 9>(act, a.frag, np, 12, lane, a3);
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int m = 0; m < 3; m++) acc[n][m] = a3[n][m];
+    }
+    conv_epilogue<MODE, 4>(a, acc, b, np, 4 * mq, mq, lane, red, sinv);
+}
+
+// ---------------------------------------------------------------- weight gradient
+// dW[tap][c][n] = sum over boards and positions p of x[p + off(tap)][c] * dy[p][n]
+// (x = the conv's input activation, dy = dL/d(conv output)), fp32 MFMA 16x16x4:
+// M = input channel c, N = output channel n, K = positions.  Workgroup (tap, group of
+// boards), 4 waves (2 x 2) of 64 x 64: lane l reads x / dy at position p0 + l / 16,
+// channels (tile) + l % 16.  16 positions per iteration, the next iteration's 32
+// operands loaded while this one's 64 MFMAs run.  Partial sums per group -> wpart.
+constexpr int WG_THREADS = 256;
+__global__ __launch_bounds__(WG_THREADS, 2) void sgd_wgrad_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ dy, int B, int G, int NG,
+                                                                 float* __restrict__ wpart) {
+    const int tap = blockIdx.x % 9, grp = blockIdx.x / 9;
+    const int b0 = grp * G, b1 = b0 + G < B ? b0 + G : B;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+    const int kq = lane >> 4, cl = lane & 15;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = zero4();
+    const int iters = (b1 - b0) * 15;  // 16 positions per iteration, 15 per board (240 >= 225)
+    float av[2][4][4], bv[2][4][4];    // [buffer][k-step][tile]
+    auto load = [&](int it, float (&A)[4][4], float (&Bv)[4][4]) {
+        const int b = b0 + it / 15, p0 = (it % 15) * 16;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const int p = p0 + 4 * s + kq;
+            const int r = p / 15 + dr, c = p % 15 + dc;
+            const bool okx = p < NPOS && r >= 0 && r < 15 && c >= 0 && c < 15;
+            const bool oky = p < NPOS;
+            const float* xr = x + ((size_t)b * NPOS + (okx ? r * 15 + c : 0)) * CH + 64 * wm + cl;
+            const float* yr = dy + ((size_t)b * NPOS + (oky ? p : 0)) * CH + 64 * wn + cl;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                A[s][t] = okx ? xr[16 * t] : 0.f;
+                Bv[s][t] = oky ? yr[16 * t] : 0.f;
+            }
+        }
+    };
+    if (iters > 0) load(0, av[0], bv[0]);
+    for (int it = 0; it < iters; it += 2) {
+        if (it + 1 < iters) load(it + 1, av[1], bv[1]);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0][s][i], bv[0][s][j], acc[i][j], 0, 0, 0);
+        if (it + 1 >= iters) break;
+        if (it + 2 < iters) load(it + 2, av[0], bv[0]);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1][s][i], bv[1][s][j], acc[i][j], 0, 0, 0);
+    }
+    // D[row = c: 4 (l / 16) + r][col = n: l % 16]
+    float* o = wpart + ((size_t)tap * NG + grp) * CH * CH;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                o[(size_t)(64 * wm + 16 * i + 4 * kq + r) * CH + 64 * wn + 16 * j + cl] = acc[i][j][r];
+}
+
+// dW (torch layout [n][c][kh][kw]) = sum of the groups' partials
+__global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, float* __restrict__ dw) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (tap, c, n), n fastest
+    if (e >= 9 * CH * CH) return;
+    const int tap = e / (CH * CH), rem = e - tap * CH * CH, c = rem >> 7, n = rem & 127;
+    const float* p = wpart + (size_t)tap * NG * CH * CH + rem;
+    float s = 0.f;
+    for (int g = 0; g < NG; g++) s += p[(size_t)g * CH * CH];
+    dw[((size_t)n * CH + c) * 9 + tap] = s;
+}
+
+// ---------------------------------------------------------------- host side
+struct Ws {
+    _Float16* frag;
+    float* y[NBN];    // y[0] is the caller's
+    float* act[4];    // a0, h1, a1, h2 (inputs of conv 1..4)
+    float* g[NBN];    // dL/d(BN output) of BN 0..4
+    float* dy;        // dL/dy of the current conv (weight gradient operand)
+    float* coef;      // [NBN][CO_FLOATS]
+    float* fpart;     // [NBN][B][PART]
+    float* bpart;     // [NBN][B][PART]
+    float* wpart;     // [9][NG][CH][CH]
+    int NG, G;
+};
+
+size_t ws_layout(int B, Ws* w, char* base) {
+    const size_t R = (size_t)B * NPOS * CH * sizeof(float);
+    const int NG = B < 32 ? B : 32, G = (B + NG - 1) / NG;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    Ws t;
+    t.frag = (_Float16*)take((size_t)LAYERS * 2 * 2 * FRAG_HALVES * sizeof(_Float16));
+    t.y[0] = nullptr;
+    for (int i = 1; i < NBN; i++) t.y[i] = (float*)take(R);
+    for (int i = 0; i < 4; i++) t.act[i] = (float*)take(R);
+    for (int i = 0; i < NBN; i++) t.g[i] = (float*)take(R);
+    t.dy = (float*)take(R);
+    t.coef = (float*)take((size_t)NBN * CO_FLOATS * sizeof(float));
+    t.fpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
+    t.bpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
+    t.wpart = (float*)take((size_t)9 * NG * CH * CH * sizeof(float));
+    t.NG = NG;
+    t.G = G;
+    if (w) *w = t;
+    return off;
+}
+
+int sgd_fail(int code, const std::string& msg) {
+    gz_internal_set_error(msg.c_str());
+    return code;
+}
+
+int sgd_check(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return sgd_fail(GZ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return GZ_OK;
+}
+
+int check_net(const gz_sgd_net* net, int B, const void* ws) {
+    if (!net || B < 1 || B > GZ_SGD_MAX_BOARDS || !ws) return sgd_fail(GZ_ERR_ARG, "gz_sgd: bad arguments");
+    for (int i = 0; i < NBN; i++)
+        if (!net->bn_weight[i] || !net->bn_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd: BatchNorm parameters are NULL");
+    for (int i = 0; i < LAYERS; i++)
+        if (!net->conv_weight[i] || !net->conv_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd: conv parameters are NULL");
+    if (!(net->eps > 0.f) || !(net->momentum >= 0.f && net->momentum <= 1.f))
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd: eps must be > 0 and momentum in [0, 1]");
+    return GZ_OK;
+}
+
+}  // namespace
+
+extern "C" size_t gz_sgd_workspace_bytes(int32_t boards) {
+    return boards < 1 ? 0 : ws_layout(boards, nullptr, nullptr);
+}
+
+extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y0, float* d_out, void* d_ws,
+                              void* stream) {
+    int rc;
+    if ((rc = check_net(net, B, d_ws))) return rc;
+    if (!d_y0 || !d_out) return sgd_fail(GZ_ERR_ARG, "gz_sgd_forward: y0 / out are NULL");
+    hipStream_t s = (hipStream_t)stream;
+    Ws w;
+    ws_layout(B, &w, (char*)d_ws);
+    w.y[0] = (float*)d_y0;
+    const long long n4 = (long long)B * NPOS * CH / 4;
+    PackArgs pa;
+    for (int i = 0; i < LAYERS; i++) pa.w[i] = net->conv_weight[i];
+    sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.frag);
+    sgd_stats_kernel<<<B, 256, 0, s>>>(d_y0, w.fpart);
+    sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0], net->bn_running_mean[0],
+                                             net->bn_running_var[0], net->momentum, net->eps, w.coef);
+    if ((rc = sgd_check("gz_sgd_forward: BN0"))) return rc;
+    // conv L (1..4): input = relu(BN_{L-1}(y_{L-1}) (+ skip)), skip a0 for conv 3's input a1
+    for (int L = 1; L <= LAYERS; L++) {
+        ConvArgs a{};
+        a.src = w.y[L - 1];
+        a.coef = w.coef + (size_t)(L - 1) * CO_FLOATS;
+        a.skip = L == 3 ? w.act[0] : nullptr;
+        a.save = w.act[L - 1];
+        a.frag = w.frag + (size_t)((L - 1) * 2 + 0) * 2 * FRAG_HALVES;
+        a.bias = net->conv_bias[L - 1];
+        a.out = w.y[L];
+        a.part = w.fpart + (size_t)L * B * PART;
+        sgd_conv_kernel<0><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
+        sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(a.part, B, net->bn_weight[L], net->bn_bias[L],
+                                                 net->bn_running_mean[L], net->bn_running_var[L], net->momentum,
+                                                 net->eps, w.coef + (size_t)L * CO_FLOATS);
+        if ((rc = sgd_check("gz_sgd_forward: conv"))) return rc;
+    }
+    // a2 = relu(BN4(y4) + a1)
+    sgd_act_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(w.y[4], w.coef + 4 * CO_FLOATS, w.act[2], d_out, n4);
+    return sgd_check("gz_sgd_forward: output");
+}
+
+extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_y0, const float* d_out,
+                               const float* d_dout, float* d_dy0, const gz_sgd_grads* gr, void* d_ws, void* stream) {
+    int rc;
+    if ((rc = check_net(net, B, d_ws))) return rc;
+    if (!d_y0 || !d_out || !d_dout || !d_dy0 || !gr) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL argument");
+    for (int i = 0; i < NBN; i++)
+        if (!gr->bn_weight[i] || !gr->bn_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL gradient");
+    for (int i = 0; i < LAYERS; i++)
+        if (!gr->conv_weight[i] || !gr->conv_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL gradient");
+    hipStream_t s = (hipStream_t)stream;
+    Ws w;
+    ws_layout(B, &w, (char*)d_ws);
+    w.y[0] = (float*)d_y0;
+    const long long n4 = (long long)B * NPOS * CH / 4;
+    // g4 = dL/d(BN4 output) = dout [out > 0]; also the skip gradient into a1
+    sgd_mask_stats_kernel<<<B, 256, 0, s>>>(d_dout, d_out, w.y[4], w.coef + 4 * CO_FLOATS, w.g[4],
+                                            w.bpart + (size_t)4 * B * PART);
+    for (int L = LAYERS; L >= 1; L--) {
+        float* coefL = w.coef + (size_t)L * CO_FLOATS;
+        sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart + (size_t)L * B * PART, B, net->bn_weight[L], coefL,
+                                                 gr->bn_weight[L], gr->bn_bias[L], gr->conv_bias[L - 1]);
+        // input gradient of conv L: dy_L = k (g_L - mg - xhat mgx) staged (and saved for the
+        // weight gradient); its output is dL/d(input of conv L) -> masked by that
+        // activation's ReLU (+ the skip gradient: g4 into a1, g2 into a0)
+        ConvArgs a{};
+        a.src = w.g[L];
+        a.ysrc = w.y[L];
+        a.coef = coefL;
+        a.save = w.dy;
+        a.frag = w.frag + (size_t)((L - 1) * 2 + 1) * 2 * FRAG_HALVES;
+        a.eskip = L == 3 ? w.g[4] : (L == 1 ? w.g[2] : nullptr);
+        a.eact = w.act[L - 1];
+        a.ey = w.y[L - 1];
+        a.ecoef = w.coef + (size_t)(L - 1) * CO_FLOATS;
+        a.out = w.g[L - 1];
+        a.part = w.bpart + (size_t)(L - 1) * B * PART;
+        sgd_conv_kernel<1><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
+        sgd_wgrad_kernel<<<9 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, B, w.G, w.NG, w.wpart);
+        sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, gr->conv_weight[L - 1]);
+        if ((rc = sgd_check("gz_sgd_backward: conv"))) return rc;
+    }
+    sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0], gr->bn_bias[0],
+                                             nullptr);
+    sgd_bn_dy_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(w.g[0], d_y0, w.coef, d_dy0, n4);
+    return sgd_check("gz_sgd_backward: BN0");
+}

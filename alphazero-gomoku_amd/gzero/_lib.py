@@ -77,6 +77,20 @@ class SelfplayCounters(ctypes.Structure):
 assert ctypes.sizeof(BoardState) == 80 and ctypes.sizeof(Record) == 80
 assert ctypes.sizeof(SearchStats) == 24 and ctypes.sizeof(SelfplayCounters) == 40
 
+class SgdNet(ctypes.Structure):  # gz_sgd_net
+    _fields_ = [("bn_weight", ctypes.c_void_p * 5), ("bn_bias", ctypes.c_void_p * 5),
+                ("bn_running_mean", ctypes.c_void_p * 5), ("bn_running_var", ctypes.c_void_p * 5),
+                ("conv_weight", ctypes.c_void_p * 4), ("conv_bias", ctypes.c_void_p * 4),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float)]
+
+
+class SgdGrads(ctypes.Structure):  # gz_sgd_grads
+    _fields_ = [("bn_weight", ctypes.c_void_p * 5), ("bn_bias", ctypes.c_void_p * 5),
+                ("conv_weight", ctypes.c_void_p * 4), ("conv_bias", ctypes.c_void_p * 4)]
+
+
+GZ_SGD_MAX_BOARDS = 65535
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -122,6 +136,10 @@ SIGNATURES = {
     "gz_knowledge_scores": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
     "gz_dataset_build": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P]),
     "gz_dataset_gather": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _I64, _I32, _P, _P, _P, _P]),
+    "gz_sgd_workspace_bytes": (_SZ, [_I32]),
+    "gz_sgd_forward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P]),
+    "gz_sgd_backward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P, ctypes.POINTER(SgdGrads), _P,
+                                       _P]),
 }
 
 _lib = None

@@ -152,10 +152,15 @@ def _world(group):
 
 
 class DeviceTrainer:
-    """Adam + StepLR policy-value SGD of training.main (training.py:379-388) on the device."""
+    """Adam + StepLR policy-value SGD of training.main (training.py:379-388) on the device.
+
+    On a GPU the training forward/backward of the residual tower runs on the HIP
+    kernels of csrc/gz_sgd.hip (``gzero.sgd.train_forward``; ``native=False``: torch's
+    own convolutions, kept for comparison); on the CPU (gloo rehearsals of the
+    data-parallel loop) it is torch's."""
 
     def __init__(self, model, lr=8e-4, weight_decay=1e-5, grad_clip=0.8, step_size=2, gamma=0.85, group=None,
-                 device="cuda"):
+                 device="cuda", native=None):
         self.gm = model
         self.net = model.model if hasattr(model, "model") else model
         self.device = torch.device(device)
@@ -163,6 +168,12 @@ class DeviceTrainer:
         if hasattr(model, "device"):
             model.device = self.device
         self.grad_clip = grad_clip
+        self.native = (self.device.type == "cuda") if native is None else bool(native)
+        if self.native:
+            from . import sgd
+            self._forward = lambda x: sgd.train_forward(self.net, x)
+        else:
+            self._forward = self.net
         self.group = group
         self.world, self.rank = _world(group)
         self.params = [p for p in self.net.parameters()]
@@ -224,7 +235,7 @@ class DeviceTrainer:
             self.optimizer.zero_grad(set_to_none=False)
             if local > 0:
                 x, y, v = _gather(ds, mine)
-                logits, val = self.net(x)
+                logits, val = self._forward(x)
                 loss = self.ce(logits, y) + self.mse(val, v)
                 (loss * (local / gcount) if self.world > 1 else loss).backward()
                 lval = loss.detach()

@@ -1,0 +1,132 @@
+"""The training step's device tower (csrc/gz_sgd.hip via gzero.sgd.train_forward)
+against torch autograd of the same PolicyValueNet in float64 on the CPU (the
+reference's training.py:277-311 step: forward in train mode, CE + MSE loss,
+backward), on identical weights and boards.
+
+Tolerances, stated here: logits / value within 2e-5 (absolute, |logits| ~ 1),
+the loss within 1e-6 relative, every parameter gradient within 2e-4 of the
+float64 gradient's norm (relative Frobenius error; torch's own fp32 GPU path,
+MIOpen, measured alongside for scale) and every BatchNorm running statistic
+within 1e-5.  The biases of the convs that feed a BatchNorm have a zero gradient
+(the batch mean cancels them); theirs must stay below 1e-6 of the largest
+gradient norm.  The training-loop tests (test_gpu_train.py) run the same kernels
+through DeviceTrainer against the reference's recorded losses (3e-3).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(seed=3, scale=1.0):
+    from gzero import weights
+    net = weights.PolicyValueNet()
+    sd = weights.init_state_dict(seed)
+    if scale != 1.0:
+        for k in sd:
+            if "conv" in k and k.endswith("weight"):
+                sd[k] = sd[k] * scale
+    net.load_state_dict(sd)
+    return net
+
+
+def _batch(B, seed):
+    rng = np.random.default_rng(seed)
+    cells = rng.choice(np.array([0, 0, 0, 1, 2], np.int8), size=(B, 225))
+    x = np.stack([cells == 1, cells == 2, cells == 0], 1).reshape(B, 3, 15, 15).astype(np.float32)
+    y = rng.integers(0, 225, B)
+    v = rng.uniform(-1, 1, (B, 1)).astype(np.float32)
+    return torch.from_numpy(x), torch.from_numpy(y), torch.from_numpy(v)
+
+
+def _step(net, fwd, x, y, v, loss_scale=1.0):
+    net.train()
+    net.zero_grad(set_to_none=True)
+    lg, val = fwd(x)
+    loss = nn.CrossEntropyLoss()(lg, y) + nn.MSELoss()(val, v.to(val.dtype))
+    (loss * loss_scale).backward()
+    grads = {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()}
+    bufs = {k: b.detach().double().cpu() for k, b in net.named_buffers()}
+    return lg.detach().double().cpu(), val.detach().double().cpu(), float(loss), grads, bufs
+
+
+def _compare(B, seed, scale=1.0, loss_scale=1.0, gtol=2e-4):
+    from gzero import sgd
+    net = _net(seed, scale)
+    x, y, v = _batch(B, seed + 100)
+    ref_net = copy.deepcopy(net).double()
+    ref = _step(ref_net, ref_net, x.double(), y, v.double(), loss_scale)
+    dev_net = copy.deepcopy(net).cuda()
+    got = _step(dev_net, lambda t: sgd.train_forward(dev_net, t), x.cuda(), y.cuda(), v.cuda(), loss_scale)
+    mio_net = copy.deepcopy(net).cuda()
+    mio = _step(mio_net, mio_net, x.cuda(), y.cuda(), v.cuda(), loss_scale)
+    assert (got[0] - ref[0]).abs().max() < 2e-5 * max(1.0, float(ref[0].abs().max()))
+    assert (got[1] - ref[1]).abs().max() < 2e-5
+    assert abs(got[2] - ref[2]) <= 1e-6 * abs(ref[2])
+    worst, worst_mio = {}, {}
+    top = max(float(g.norm()) for g in ref[3].values())
+    for k, g in ref[3].items():
+        if float(g.norm()) < 1e-9 * top:  # a bias in front of a BatchNorm
+            assert float(got[3][k].norm()) < 1e-6 * top, k
+            continue
+        den = float(g.norm())
+        worst[k] = float((got[3][k] - g).norm()) / den
+        worst_mio[k] = float((mio[3][k] - g).norm()) / den
+    for k, b in ref[4].items():
+        assert torch.allclose(got[4][k], b, rtol=1e-5, atol=1e-6), k
+    bad = {k: e for k, e in worst.items() if e > gtol}
+    print("max rel grad error: native %.2e (%s), MIOpen fp32 %.2e" %
+          (max(worst.values()), max(worst, key=worst.get), max(worst_mio.values())))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("B", [128, 7, 1])
+def test_sgd_tower_vs_float64(B):
+    """Batch 128 (a training step), a 7-board remainder batch and a single board."""
+    _compare(B, SEED + B)
+
+
+def test_sgd_tower_loss_scaled():
+    """Gradients 1e-6 and 1e4 times larger: the input-gradient GEMM's power-of-two
+    operand scaling keeps the same relative accuracy."""
+    _compare(32, SEED + 5, loss_scale=1e-6)
+    _compare(32, SEED + 6, loss_scale=1e4)
+
+
+@pytest.mark.parametrize("scale", [0.1, 3.0])
+def test_sgd_tower_scaled_weights(scale):
+    """Conv weights x0.1 / x3 (BatchNorm renormalises; gradients through it grow / shrink)."""
+    _compare(24, SEED + 9, scale=scale)
+
+
+def test_sgd_tower_two_steps_match_torch_trainer():
+    """Three Adam steps of DeviceTrainer (native tower) vs the same trainer on torch's
+    GPU convolutions (native=False): the losses (each after the previous steps'
+    updates) within 1e-4 and the BatchNorm running statistics within 1e-5.
+    (Parameters are not compared element-wise: Adam's first steps move weights whose
+    gradient is rounding noise by +-lr either way.)"""
+    from gzero.train import DeviceTrainer
+    nets = [_net(SEED), _net(SEED)]
+    x, y, v = _batch(128, SEED + 1)
+    losses = []
+    for native, net in zip((True, False), nets):
+        tr = DeviceTrainer(net, native=native)
+        ls = []
+        for _ in range(3):
+            tr.optimizer.zero_grad()
+            lg, val = tr._forward(x.cuda())
+            loss = nn.CrossEntropyLoss()(lg, y.cuda()) + nn.MSELoss()(val, v.cuda())
+            loss.backward()
+            nn.utils.clip_grad_norm_(tr.params, 0.8)
+            tr.optimizer.step()
+            ls.append(float(loss))
+        losses.append(ls)
+    np.testing.assert_allclose(losses[0], losses[1], rtol=1e-4)
+    for (k, a), (_, b) in zip(nets[0].named_buffers(), nets[1].named_buffers()):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-5, atol=1e-5), k

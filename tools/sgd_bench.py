@@ -11,7 +11,7 @@ import torch.nn as nn  # noqa: E402
 from gzero import weights  # noqa: E402
 
 
-def run(tag, steps=60, bs=128, channels_last=False):
+def run(tag, steps=60, bs=128, channels_last=False, native=False):
     torch.manual_seed(0)
     net = weights.PolicyValueNet().cuda()
     if channels_last:
@@ -25,9 +25,12 @@ def run(tag, steps=60, bs=128, channels_last=False):
     v = torch.rand((bs, 1), device="cuda")
     net.train()
 
+    from gzero import sgd
+    fwd = (lambda t: sgd.train_forward(net, t)) if native else net
+
     def step():
         opt.zero_grad()
-        lg, val = net(x)
+        lg, val = fwd(x)
         loss = ce(lg, y) + mse(val, v)
         loss.backward()
         nn.utils.clip_grad_norm_(net.parameters(), 0.8)
@@ -44,6 +47,7 @@ def run(tag, steps=60, bs=128, channels_last=False):
     print(f"{tag}: {dt * 1e3:.2f} ms/step, {bs * 3 * 267.38e6 / dt / 1e12:.1f} TFLOP/s", flush=True)
 
 
+run("native", native=True)
 run("default")
 torch.backends.cudnn.benchmark = True
 run("benchmark")
@@ -76,5 +80,6 @@ def trainer_run(tag, n_records=4000, **kw):
 
 
 torch.backends.cudnn.benchmark = False
-trainer_run("default")
-trainer_run("default-2nd")
+trainer_run("native", native=True)
+trainer_run("native-2nd", native=True)
+trainer_run("miopen", native=False)
