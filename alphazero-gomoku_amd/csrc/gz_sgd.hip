@@ -19,10 +19,11 @@
 // (mean, centred sum of squares, max |y|; or sum g, sum g*xhat, max |g|), which a
 // 128-thread kernel combines (Chan's formula, fp64) into the batch statistics,
 // the running-stat update and the backward coefficients.
-// Weight gradients: fp32 MFMA (v_mfma_f32_16x16x4_f32, exact products) over the
-// positions, one workgroup per (tap, group of boards), reading the saved NHWC
-// activations and input gradients directly (a lane's 16 channels are 64
-// contiguous bytes); the groups' partial sums are added by a second kernel.
+// Weight gradients: the same f16x3 MFMA with K = positions, one workgroup per
+// (quarter of the 128 x 128 channel pairs, group of boards), all 9 taps; the saved
+// NHWC activations and input gradients are staged into LDS as [position][channel]
+// rows and read transposed (ds_read_b64_tr_b16); the groups' partial sums are added
+// by a second kernel.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -498,84 +499,137 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
 
 // ---------------------------------------------------------------- weight gradient
 // dW[tap][c][n] = sum over boards and positions p of x[p + off(tap)][c] * dy[p][n]
-// (x = the conv's input activation, dy = dL/d(conv output)), fp32 MFMA 16x16x4:
-// M = input channel c, N = output channel n, K = positions.  Workgroup (tap, group of
-// boards), 4 waves (2 x 2) of 64 x 64: lane l reads x / dy at position p0 + l / 16,
-// channels (tile) + l % 16.  16 positions per iteration, the next iteration's 32
-// operands loaded while this one's 64 MFMAs run.  Partial sums per group -> wpart.
+// (x = the conv's input activation, dy = dL/d(conv output)): M = input channel c,
+// N = output channel n, K = positions.  Partial sums per group of boards -> wpart
+// [tap][group][c][n] (times S), added by sgd_wreduce_kernel.
 constexpr int WG_THREADS = 256;
-__global__ __launch_bounds__(WG_THREADS, 2) void sgd_wgrad_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ dy, int B, int G, int NG,
-                                                                 float* __restrict__ wpart) {
-    const int tap = blockIdx.x % 9, grp = blockIdx.x / 9;
+// f16x3 MFMA (v_mfma_f32_16x16x32_f16, K = 32 positions per MFMA): workgroup (c half, n half, group of boards), 4 waves; wave w takes input
+// channels [16 w, 16 w + 16) of the half and all 64 output channels of its n half,
+// all 9 taps (9 x 4 accumulator tiles).  A board's x (the conv input, 64 channels)
+// and dy (64 output channels, times the BN-backward scale S) are staged as f16 hi/lo
+// in LDS as [position][channel] rows of 128 B (225 positions + a zero row); the
+// MFMA operands, 8 consecutive positions of one channel per lane, come from
+// ds_read_b64_tr_b16 (4 positions x 16 channels per 16-lane group, delivered
+// transposed).  A row's four 32-B channel tiles are stored XOR-swizzled by
+// s(row) = bit 1 | bit 3 << 1 of the row so that the 8 rows of a half-wave's read
+// (p0 + {0..3, 8..11}) hit 8 different 32-B bank slots.  Taps shift the A rows:
+// x at position p + off(tap), the zero row off the board and past position 224.
+constexpr int W16_ROWS = NPOS + 1;            // + the zero row
+constexpr int W16_PLANE = W16_ROWS * 128;     // bytes per hi / lo plane (64 channels)
+__device__ __forceinline__ int w16_off(int row, int ch) {  // byte offset of channel ch (0..63) of a row
+    const int s = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    return row * 128 + 32 * ((ch >> 4) ^ s) + 2 * (ch & 15);
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h4 w16_tr(const char* lds, int byte) {
+    return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                      (__attribute__((address_space(3))) s16x4*)(lds + byte)));
+}
+__device__ __forceinline__ h8 w16_cat(h4 a, h4 b) {
+    h8 r;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        r[j] = a[j];
+        r[4 + j] = b[j];
+    }
+    return r;
+}
+__global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ dy,
+                                                                   const float* __restrict__ coef, int B, int G,
+                                                                   int NG, float* __restrict__ wpart) {
+    __shared__ __attribute__((aligned(16))) char lds[4 * W16_PLANE];  // x hi, x lo, dy hi, dy lo
+    const int cq = blockIdx.x & 1, nq = (blockIdx.x >> 1) & 1, grp = blockIdx.x >> 2;
     const int b0 = grp * G, b1 = b0 + G < B ? b0 + G : B;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
-    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-    const int kq = lane >> 4, cl = lane & 15;
-    f32x4 acc[4][4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pc = lane & 3;
+    const float S = coef[CO_SCALE];
+    f32x4 acc[9][4];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int t = 0; t < 9; t++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = zero4();
-    const int iters = (b1 - b0) * 15;  // 16 positions per iteration, 15 per board (240 >= 225)
-    float av[2][4][4], bv[2][4][4];    // [buffer][k-step][tile]
-    auto load = [&](int it, float (&A)[4][4], float (&Bv)[4][4]) {
-        const int b = b0 + it / 15, p0 = (it % 15) * 16;
+        for (int j = 0; j < 4; j++) acc[t][j] = zero4();
+    // zero rows (both tensors, both planes), never overwritten by the staging
+    if (tid < 4 * 16) *(uint64_t*)(lds + (tid >> 4) * W16_PLANE + NPOS * 128 + 8 * (tid & 15)) = 0ull;
+    for (int b = b0; b < b1; b++) {
+        __syncthreads();  // the previous board's reads are done
+        for (int e = tid; e < 2 * NPOS * 16; e += WG_THREADS) {
+            const int t = e >= NPOS * 16, r = e - t * NPOS * 16, p = r >> 4, c4 = (r & 15) * 4;
+            const float* src = t ? dy + ((size_t)b * NPOS + p) * CH + 64 * nq + c4
+                                 : x + ((size_t)b * NPOS + p) * CH + 64 * cq + c4;
+            f32x4 v = *(const f32x4*)src;
+            if (t) v = v * S;
+            h4 hi, lo;
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const int p = p0 + 4 * s + kq;
-            const int r = p / 15 + dr, c = p % 15 + dc;
-            const bool okx = p < NPOS && r >= 0 && r < 15 && c >= 0 && c < 15;
-            const bool oky = p < NPOS;
-            const float* xr = x + ((size_t)b * NPOS + (okx ? r * 15 + c : 0)) * CH + 64 * wm + cl;
-            const float* yr = dy + ((size_t)b * NPOS + (oky ? p : 0)) * CH + 64 * wn + cl;
+            for (int k = 0; k < 4; k++) {
+                const _Float16 h = (_Float16)v[k];
+                hi[k] = h;
+                lo[k] = (_Float16)(v[k] - (float)h);
+            }
+            char* base = lds + 2 * t * W16_PLANE + w16_off(p, c4);
+            *(h4*)base = hi;
+            *(h4*)(base + W16_PLANE) = lo;
+        }
+        __syncthreads();
+        const char* xh = lds;
+        const char* dh = lds + 2 * W16_PLANE;
+        for (int s = 0; s < 8; s++) {
+            // the lane's two rows: positions p_a (elements 0..3) and p_a + 4 (4..7)
+            const int pa = 32 * s + 8 * g + q, pb = pa + 4;
+            h8 bh[4], bl[4];
+            {
+                const int ra = pa < NPOS ? pa : NPOS, rb = pb < NPOS ? pb : NPOS;
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                A[s][t] = okx ? xr[16 * t] : 0.f;
-                Bv[s][t] = oky ? yr[16 * t] : 0.f;
+                for (int j = 0; j < 4; j++) {
+                    const int ch = 16 * j + 4 * pc;
+                    const h4 a0 = w16_tr(dh, w16_off(ra, ch)), a1 = w16_tr(dh, w16_off(rb, ch));
+                    const h4 c0 = w16_tr(dh + W16_PLANE, w16_off(ra, ch)), c1 = w16_tr(dh + W16_PLANE, w16_off(rb, ch));
+                    bh[j] = w16_cat(a0, a1);
+                    bl[j] = w16_cat(c0, c1);
+                }
+            }
+            const int ya = pa / 15, xa = pa - 15 * ya, yb = pb / 15, xb = pb - 15 * yb;
+#pragma unroll
+            for (int tap = 0; tap < 9; tap++) {
+                const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+                const int r1 = ya + dr, c1 = xa + dc, r2 = yb + dr, c2 = xb + dc;
+                const int ra = pa < NPOS && (unsigned)r1 < 15u && (unsigned)c1 < 15u ? r1 * 15 + c1 : NPOS;
+                const int rb = pb < NPOS && (unsigned)r2 < 15u && (unsigned)c2 < 15u ? r2 * 15 + c2 : NPOS;
+                const int ch = 16 * wave + 4 * pc;
+                const h8 ah = w16_cat(w16_tr(xh, w16_off(ra, ch)), w16_tr(xh, w16_off(rb, ch)));
+                const h8 al = w16_cat(w16_tr(xh + W16_PLANE, w16_off(ra, ch)), w16_tr(xh + W16_PLANE, w16_off(rb, ch)));
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[tap][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[tap][j], 0, 0, 0);
+                    acc[tap][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[tap][j], 0, 0, 0);
+                    acc[tap][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[tap][j], 0, 0, 0);
+                }
             }
         }
-    };
-    if (iters > 0) load(0, av[0], bv[0]);
-    for (int it = 0; it < iters; it += 2) {
-        if (it + 1 < iters) load(it + 1, av[1], bv[1]);
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0][s][i], bv[0][s][j], acc[i][j], 0, 0, 0);
-        if (it + 1 >= iters) break;
-        if (it + 2 < iters) load(it + 2, av[0], bv[0]);
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1][s][i], bv[1][s][j], acc[i][j], 0, 0, 0);
     }
-    // D[row = c: 4 (l / 16) + r][col = n: l % 16]
-    float* o = wpart + ((size_t)tap * NG + grp) * CH * CH;
+    // D[row = c: 4 g + r][col = n: lane % 16] of tile (tap, j), scaled by S
+    const int i = lane & 15;
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int tap = 0; tap < 9; tap++) {
+        float* o = wpart + ((size_t)tap * NG + grp) * CH * CH;
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                o[(size_t)(64 * wm + 16 * i + 4 * kq + r) * CH + 64 * wn + 16 * j + cl] = acc[i][j][r];
+                o[(size_t)(64 * cq + 16 * wave + 4 * g + r) * CH + 64 * nq + 16 * j + i] = acc[tap][j][r];
+    }
 }
 
 // dW (torch layout [n][c][kh][kw]) = sum of the groups' partials
-__global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, float* __restrict__ dw) {
+__global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, const float* __restrict__ coef,
+                                   float* __restrict__ dw) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (tap, c, n), n fastest
     if (e >= 9 * CH * CH) return;
     const int tap = e / (CH * CH), rem = e - tap * CH * CH, c = rem >> 7, n = rem & 127;
     const float* p = wpart + (size_t)tap * NG * CH * CH + rem;
     float s = 0.f;
     for (int g = 0; g < NG; g++) s += p[(size_t)g * CH * CH];
-    dw[((size_t)n * CH + c) * 9 + tap] = s;
+    dw[((size_t)n * CH + c) * 9 + tap] = s * coef[CO_INVSCALE];
 }
 
 // ---------------------------------------------------------------- host side
@@ -594,7 +648,7 @@ struct Ws {
 
 size_t ws_layout(int B, Ws* w, char* base) {
     const size_t R = (size_t)B * NPOS * CH * sizeof(float);
-    const int NG = B < 32 ? B : 32, G = (B + NG - 1) / NG;
+    const int NG = B < 64 ? B : 64, G = (B + NG - 1) / NG;  // 4 NG weight-gradient workgroups
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char* p = base ? base + off : nullptr;
@@ -722,8 +776,8 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         a.out = w.g[L - 1];
         a.part = w.bpart + (size_t)(L - 1) * B * PART;
         sgd_conv_kernel<1><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
-        sgd_wgrad_kernel<<<9 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, B, w.G, w.NG, w.wpart);
-        sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, gr->conv_weight[L - 1]);
+        sgd_wgrad16_kernel<<<4 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, coefL, B, w.G, w.NG, w.wpart);
+        sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, coefL, gr->conv_weight[L - 1]);
         if ((rc = sgd_check("gz_sgd_backward: conv"))) return rc;
     }
     sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0], gr->bn_bias[0],

@@ -340,7 +340,12 @@ def config5(games, sims, seed, iterations=2):
         r["iteration_s"] = time.perf_counter() - t0
         its.append(r)
     last = its[-1]
+    per1024 = last["iteration_s"] * 1024.0 / games
     return {"value": round(3600.0 / last["iteration_s"], 2), "unit": "iterations/h",
+            "games_per_iteration": games,
+            "per_1024_games": {"iteration_s": round(per1024, 2), "iterations_per_h": round(3600.0 / per1024, 2),
+                               "note": "the same iteration scaled linearly to 1,024 games (self-play, dataset and "
+                                       "SGD all grow with the record count), for comparison with round 2"},
             "iteration_s": round(last["iteration_s"], 2), "selfplay_s": round(last["selfplay_s"], 2),
             "sgd_s": round(last.get("sgd_s", 0.0), 2), "records": last["records"],
             "samples": last.get("samples"), "moves_played": last["moves_played"],
@@ -348,7 +353,9 @@ def config5(games, sims, seed, iterations=2):
             "workload": (f"BASELINE config 5 on 1 GPU: training.run_iteration with {games} self-play games per "
                          f"iteration ({sims} sims, medium, beta 0.2, planner_steps 5, tree PV forward on every node, "
                          "records through gzero.dist.RecordExchange), 35 % augmentation, 2 epochs of SGD "
-                         "(batch 128, Adam 8e-4, clip 0.8, torch/MIOpen fp32), StepLR; value from the last of "
+                         "(batch 128, Adam 8e-4, clip 0.8; residual tower on gz_sgd_forward/backward, f16x3 MFMA; conv0 and the "
+                         "heads torch), StepLR; games per iteration fixed by the builder (BASELINE names none); "
+                         "value from the last of "
                          f"{iterations} iterations")}
 
 
