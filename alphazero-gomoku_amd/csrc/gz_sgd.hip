@@ -437,7 +437,8 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
     const size_t board = (size_t)b * NPOS * CH;
     const bool save = a.save && blockIdx.x == 0;
     const float scale = MODE == 1 ? a.coef[CO_SCALE] : 1.f;
-    for (int e = tid; e < NPOS * 32; e += CONV_THREADS) {
+#pragma unroll 4
+    for (int e = tid; e < NPOS * 32; e += CONV_THREADS) {  // (unrolled: 4 rows' loads in flight)
         const int p = e >> 5, c0 = (e & 31) * 4;
         const size_t o = board + (size_t)p * CH + c0;
         const f32x4 v = *(const f32x4*)(a.src + o);
@@ -553,6 +554,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float*
     if (tid < 4 * 16) *(uint64_t*)(lds + (tid >> 4) * W16_PLANE + NPOS * 128 + 8 * (tid & 15)) = 0ull;
     for (int b = b0; b < b1; b++) {
         __syncthreads();  // the previous board's reads are done
+#pragma unroll 4
         for (int e = tid; e < 2 * NPOS * 16; e += WG_THREADS) {
             const int t = e >= NPOS * 16, r = e - t * NPOS * 16, p = r >> 4, c4 = (r & 15) * 4;
             const float* src = t ? dy + ((size_t)b * NPOS + p) * CH + 64 * nq + c4
