@@ -80,6 +80,7 @@ def trainer_run(tag, n_records=4000, **kw):
 
 
 torch.backends.cudnn.benchmark = False
-trainer_run("native", native=True)
-trainer_run("native-2nd", native=True)
+trainer_run("native+graph", native=True)
+trainer_run("native+graph-2nd", native=True)
+trainer_run("native, no graph", native=True, graphs=False)
 trainer_run("miopen", native=False)
