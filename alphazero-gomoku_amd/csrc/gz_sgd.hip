@@ -46,7 +46,18 @@ constexpr int CONV_THREADS = 512;
 
 // per-BN coefficient block (floats)
 constexpr int CO_S = 0, CO_T = 128, CO_MEAN = 256, CO_INV = 384, CO_K = 512, CO_MG = 640, CO_MGX = 768,
-              CO_YMAX = 896, CO_SUMXH = 1024, CO_SCALE = 1152, CO_INVSCALE = 1153, CO_FLOATS = 1280;
+              CO_YMAX = 896, CO_SUMXH = 1024, CO_SCALE = 1152, CO_INVSCALE = 1153, CO_ABOUND = 1154,
+              CO_XSCALE = 1155, CO_XINV = 1156, CO_FLOATS = 1280;
+// f16x3 operands are scaled by powers of two so that their largest value is just below
+// 2^14: the lo halves of small values then stay out of fp16's subnormal range, where
+// they would lose bits (a float64 emulation of this step put the gradient error at
+// ~1e-3 without the scaling, ~1e-7 with it).  Scale = 2^(14 - e) for max < 2^e.
+__device__ __forceinline__ int f16_scale_exp(float m) {
+    int ex = 0;
+    if (m > 0.f && isfinite(m)) frexpf(m, &ex);
+    const int e = 14 - ex;
+    return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
 constexpr int PART = 3 * CH;  // per board partials
 
 __host__ __device__ constexpr size_t align256(size_t x) { return (x + 255) / 256 * 256; }
@@ -58,7 +69,16 @@ __host__ __device__ constexpr size_t align256(size_t x) { return (x + 255) / 256
 struct PackArgs {
     const float* w[LAYERS];
 };
-__global__ void sgd_pack_kernel(PackArgs a, _Float16* __restrict__ frag) {
+// max |w| of each conv (float bits of non-negative values order as unsigned integers)
+__global__ __launch_bounds__(256) void sgd_wmax_kernel(PackArgs a, unsigned* __restrict__ wmax) {
+    const float* W = a.w[blockIdx.y];
+    float m = 0.f;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < CH * CH * 9; i += gridDim.x * 256) m = fmaxf(m, fabsf(W[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(wmax + blockIdx.y, __float_as_uint(m));
+}
+// wsc: [0, 4) max |w| bits (sgd_wmax_kernel), [4, 8) 1 / the weight scale of each conv
+__global__ void sgd_pack_kernel(PackArgs a, float* __restrict__ wsc, _Float16* __restrict__ frag) {
     const int per = 2 * FRAG_HALVES;  // elements of one (layer, mode): hi plane index space only
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= LAYERS * 2 * FRAG_HALVES) return;
@@ -67,7 +87,9 @@ __global__ void sgd_pack_kernel(PackArgs a, _Float16* __restrict__ frag) {
     const int j = i & 7, lane = (i >> 3) & 63, nt = (i >> 9) & 7, ks = i >> 12;
     const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j, tap = k >> 7, c = k & 127;
     const float* W = a.w[layer];
-    const float v = mode == 0 ? W[(n * CH + c) * 9 + tap] : W[(c * CH + n) * 9 + (8 - tap)];
+    const int se = f16_scale_exp(__uint_as_float(((const unsigned*)wsc)[layer]));
+    if (i == 0 && mode == 0) wsc[4 + layer] = ldexpf(1.f, -se);
+    const float v = ldexpf(mode == 0 ? W[(n * CH + c) * 9 + tap] : W[(c * CH + n) * 9 + (8 - tap)], se);
     const _Float16 h = (_Float16)v;
     _Float16* f = frag + (size_t)lm * per;
     f[i] = h;
@@ -110,11 +132,15 @@ __global__ __launch_bounds__(256) void sgd_stats_kernel(const float* __restrict_
 // batch statistics from the boards' partials (equal counts: Chan's combination in
 // fp64), BN scale/shift, the running-stat update (momentum, unbiased variance) --
 // torch BatchNorm2d in training mode
+// Also the bound of the activation relu(y s + t (+ skip)) it feeds to the next conv,
+// max_c |s| max|y| + |t| (+ the skip's bound, skip_coef), and that activation's f16x3 scale.
 __global__ __launch_bounds__(128) void sgd_bn_fwd_reduce_kernel(const float* __restrict__ part, int B,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta,
                                                                float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                               float momentum, float eps, float* __restrict__ coef) {
+                                                               float momentum, float eps, float* __restrict__ coef,
+                                                               const float* __restrict__ skip_coef) {
+    __shared__ float amax[2];
     const int c = threadIdx.x;
     double sm = 0.0, mx = 0.0;
     for (int b = 0; b < B; b++) {
@@ -138,6 +164,16 @@ __global__ __launch_bounds__(128) void sgd_bn_fwd_reduce_kernel(const float* __r
     coef[CO_INV + c] = (float)inv;
     coef[CO_YMAX + c] = (float)mx;
     coef[CO_SUMXH + c] = (float)(dev * inv);
+    const float ab = wave_max(fabsf(s) * (float)mx + fabsf(coef[CO_T + c]));
+    if ((c & 63) == 0) amax[c >> 6] = ab;
+    __syncthreads();
+    if (c == 0) {
+        const float A = fmaxf(amax[0], amax[1]) + (skip_coef ? skip_coef[CO_ABOUND] : 0.f);
+        const int e = f16_scale_exp(A);
+        coef[CO_ABOUND] = A;
+        coef[CO_XSCALE] = ldexpf(1.f, e);
+        coef[CO_XINV] = ldexpf(1.f, -e);
+    }
     if (run_mean) {
         run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
         run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var * (M > 1.0 ? M / (M - 1.0) : 1.0));
@@ -177,11 +213,7 @@ __global__ __launch_bounds__(128) void sgd_bn_bwd_reduce_kernel(const float* __r
     if ((c & 63) == 0) bmax[c >> 6] = m;
     __syncthreads();
     if (c == 0) {
-        m = fmaxf(bmax[0], bmax[1]);
-        int ex = 0;
-        if (m > 0.f && isfinite(m)) frexpf(m, &ex);  // m < 2^ex
-        int e = 14 - ex;                            // scaled max < 2^14
-        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+        const int e = f16_scale_exp(fmaxf(bmax[0], bmax[1]));
         coef[CO_SCALE] = ldexpf(1.f, e);
         coef[CO_INVSCALE] = ldexpf(1.f, -e);
     }
@@ -259,7 +291,8 @@ struct ConvArgs {
     const float* skip;
     const float* coef;
     float* save;
-    const _Float16* frag;  // the conv's fragments (hi plane, lo plane after it)
+    const _Float16* frag;  // the conv's fragments (hi plane, lo plane after it), weights x 2^k
+    const float* winv;     // 2^-k
     // forward epilogue: y = acc + bias -> out, BN partials of y -> part
     const float* bias;
     // input-gradient epilogue: dx = acc / scale (+ eskip) -> g = dx [eact > 0] -> out,
@@ -292,7 +325,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
             const int pos = 16 * (m0 + m) + li;
 #pragma unroll
             for (int n = 0; n < 2; n++) {
-                y[n][m] = acc[n][m] + bias[n];
+                y[n][m] = acc[n][m] * scale_inv + bias[n];
                 if (pos < NPOS) {
                     *(f32x4*)(a.out + (board + pos) * CH + 16 * (2 * np + n) + 4 * q) = y[n][m];
 #pragma unroll
@@ -436,7 +469,7 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
     act.lo = lds + 16 * ROWS16 * 8;
     const size_t board = (size_t)b * NPOS * CH;
     const bool save = a.save && blockIdx.x == 0;
-    const float scale = MODE == 1 ? a.coef[CO_SCALE] : 1.f;
+    const float scale = MODE == 1 ? a.coef[CO_SCALE] : a.coef[CO_XSCALE];
 #pragma unroll 4
     for (int e = tid; e < NPOS * 32; e += CONV_THREADS) {  // (unrolled: 4 rows' loads in flight)
         const int p = e >> 5, c0 = (e & 31) * 4;
@@ -457,7 +490,7 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
             x = k * (v - mg - (yv - mean) * inv * mgx);
         }
         if (save) *(f32x4*)(a.save + o) = x;
-        if constexpr (MODE == 1) x = x * scale;
+        x = x * scale;
         h4 hi, lo;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -473,7 +506,7 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63, mq = wave >> 1;
     const int np = 2 * blockIdx.x + (wave & 1);
-    const float sinv = MODE == 1 ? a.coef[CO_INVSCALE] : 1.f;
+    const float sinv = (MODE == 1 ? a.coef[CO_INVSCALE] : a.coef[CO_XINV]) * *a.winv;
     // quarter 3 has tiles 12..14; its fourth tile (positions 240..255) stays zero and
     // is skipped by the epilogue (every wave runs the same epilogue and barriers)
     f32x4 acc[2][4];
@@ -537,14 +570,15 @@ __device__ __forceinline__ h8 w16_cat(h4 a, h4 b) {
 }
 __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float* __restrict__ x,
                                                                    const float* __restrict__ dy,
-                                                                   const float* __restrict__ coef, int B, int G,
+                                                                   const float* __restrict__ coef,
+                                                                   const float* __restrict__ xcoef, int B, int G,
                                                                    int NG, float* __restrict__ wpart) {
     __shared__ __attribute__((aligned(16))) char lds[4 * W16_PLANE];  // x hi, x lo, dy hi, dy lo
     const int cq = blockIdx.x & 1, nq = (blockIdx.x >> 1) & 1, grp = blockIdx.x >> 2;
     const int b0 = grp * G, b1 = b0 + G < B ? b0 + G : B;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, q = (lane >> 2) & 3, pc = lane & 3;
-    const float S = coef[CO_SCALE];
+    const float S = coef[CO_SCALE], SX = xcoef[CO_XSCALE], unscale = coef[CO_INVSCALE] * xcoef[CO_XINV];
     f32x4 acc[9][4];
 #pragma unroll
     for (int t = 0; t < 9; t++)
@@ -560,7 +594,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float*
             const float* src = t ? dy + ((size_t)b * NPOS + p) * CH + 64 * nq + c4
                                  : x + ((size_t)b * NPOS + p) * CH + 64 * cq + c4;
             f32x4 v = *(const f32x4*)src;
-            if (t) v = v * S;
+            v = v * (t ? S : SX);
             h4 hi, lo;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -609,7 +643,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float*
             }
         }
     }
-    // D[row = c: 4 g + r][col = n: lane % 16] of tile (tap, j), scaled by S
+    // D[row = c: 4 g + r][col = n: lane % 16] of tile (tap, j), unscaled
     const int i = lane & 15;
 #pragma unroll
     for (int tap = 0; tap < 9; tap++) {
@@ -618,20 +652,19 @@ __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float*
         for (int j = 0; j < 4; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                o[(size_t)(64 * cq + 16 * wave + 4 * g + r) * CH + 64 * nq + 16 * j + i] = acc[tap][j][r];
+                o[(size_t)(64 * cq + 16 * wave + 4 * g + r) * CH + 64 * nq + 16 * j + i] = acc[tap][j][r] * unscale;
     }
 }
 
 // dW (torch layout [n][c][kh][kw]) = sum of the groups' partials
-__global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, const float* __restrict__ coef,
-                                   float* __restrict__ dw) {
+__global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, float* __restrict__ dw) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (tap, c, n), n fastest
     if (e >= 9 * CH * CH) return;
     const int tap = e / (CH * CH), rem = e - tap * CH * CH, c = rem >> 7, n = rem & 127;
     const float* p = wpart + (size_t)tap * NG * CH * CH + rem;
     float s = 0.f;
     for (int g = 0; g < NG; g++) s += p[(size_t)g * CH * CH];
-    dw[((size_t)n * CH + c) * 9 + tap] = s * coef[CO_INVSCALE];
+    dw[((size_t)n * CH + c) * 9 + tap] = s;
 }
 
 // ---------------------------------------------------------------- host side
@@ -642,6 +675,7 @@ struct Ws {
     float* g[NBN];    // dL/d(BN output) of BN 0..4
     float* dy;        // dL/dy of the current conv (weight gradient operand)
     float* coef;      // [NBN][CO_FLOATS]
+    float* wsc;       // weight scales (sgd_pack_kernel)
     float* fpart;     // [NBN][B][PART]
     float* bpart;     // [NBN][B][PART]
     float* wpart;     // [9][NG][CH][CH]
@@ -665,6 +699,7 @@ size_t ws_layout(int B, Ws* w, char* base) {
     for (int i = 0; i < NBN; i++) t.g[i] = (float*)take(R);
     t.dy = (float*)take(R);
     t.coef = (float*)take((size_t)NBN * CO_FLOATS * sizeof(float));
+    t.wsc = (float*)take(8 * sizeof(float));
     t.fpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.bpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.wpart = (float*)take((size_t)9 * NG * CH * CH * sizeof(float));
@@ -714,10 +749,13 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
     const long long n4 = (long long)B * NPOS * CH / 4;
     PackArgs pa;
     for (int i = 0; i < LAYERS; i++) pa.w[i] = net->conv_weight[i];
-    sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.frag);
+    if (hipMemsetAsync(w.wsc, 0, 8 * sizeof(float), s) != hipSuccess)
+        return sgd_fail(GZ_ERR_HIP, "gz_sgd_forward: memset");
+    sgd_wmax_kernel<<<dim3(32, LAYERS), 256, 0, s>>>(pa, (unsigned*)w.wsc);
+    sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.wsc, w.frag);
     sgd_stats_kernel<<<B, 256, 0, s>>>(d_y0, w.fpart);
     sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0], net->bn_running_mean[0],
-                                             net->bn_running_var[0], net->momentum, net->eps, w.coef);
+                                             net->bn_running_var[0], net->momentum, net->eps, w.coef, nullptr);
     if ((rc = sgd_check("gz_sgd_forward: BN0"))) return rc;
     // conv L (1..4): input = relu(BN_{L-1}(y_{L-1}) (+ skip)), skip a0 for conv 3's input a1
     for (int L = 1; L <= LAYERS; L++) {
@@ -727,13 +765,15 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
         a.skip = L == 3 ? w.act[0] : nullptr;
         a.save = w.act[L - 1];
         a.frag = w.frag + (size_t)((L - 1) * 2 + 0) * 2 * FRAG_HALVES;
+        a.winv = w.wsc + 4 + (L - 1);
         a.bias = net->conv_bias[L - 1];
         a.out = w.y[L];
         a.part = w.fpart + (size_t)L * B * PART;
         sgd_conv_kernel<0><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
         sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(a.part, B, net->bn_weight[L], net->bn_bias[L],
                                                  net->bn_running_mean[L], net->bn_running_var[L], net->momentum,
-                                                 net->eps, w.coef + (size_t)L * CO_FLOATS);
+                                                 net->eps, w.coef + (size_t)L * CO_FLOATS,
+                                                 L == 2 ? w.coef : nullptr);  // BN2's output adds the skip a0
         if ((rc = sgd_check("gz_sgd_forward: conv"))) return rc;
     }
     // a2 = relu(BN4(y4) + a1)
@@ -771,6 +811,7 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         a.coef = coefL;
         a.save = w.dy;
         a.frag = w.frag + (size_t)((L - 1) * 2 + 1) * 2 * FRAG_HALVES;
+        a.winv = w.wsc + 4 + (L - 1);
         a.eskip = L == 3 ? w.g[4] : (L == 1 ? w.g[2] : nullptr);
         a.eact = w.act[L - 1];
         a.ey = w.y[L - 1];
@@ -778,8 +819,9 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         a.out = w.g[L - 1];
         a.part = w.bpart + (size_t)(L - 1) * B * PART;
         sgd_conv_kernel<1><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
-        sgd_wgrad16_kernel<<<4 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, coefL, B, w.G, w.NG, w.wpart);
-        sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, coefL, gr->conv_weight[L - 1]);
+        sgd_wgrad16_kernel<<<4 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, coefL, a.ecoef, B, w.G, w.NG,
+                                                           w.wpart);
+        sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, gr->conv_weight[L - 1]);
         if ((rc = sgd_check("gz_sgd_backward: conv"))) return rc;
     }
     sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0], gr->bn_bias[0],
