@@ -46,12 +46,13 @@ constexpr int CONV_THREADS = 512;
 
 // per-BN coefficient block (floats)
 constexpr int CO_S = 0, CO_T = 128, CO_MEAN = 256, CO_INV = 384, CO_K = 512, CO_MG = 640, CO_MGX = 768,
-              CO_YMAX = 896, CO_SUMXH = 1024, CO_SCALE = 1152, CO_INVSCALE = 1153, CO_ABOUND = 1154,
-              CO_XSCALE = 1155, CO_XINV = 1156, CO_FLOATS = 1280;
+              CO_YMAX = 896, CO_SUMXH = 1024, CO_FLOATS = 1152;
 // f16x3 operands are scaled by powers of two so that their largest value is just below
 // 2^14: the lo halves of small values then stay out of fp16's subnormal range, where
 // they would lose bits (a float64 emulation of this step put the gradient error at
-// ~1e-3 without the scaling, ~1e-7 with it).  Scale = 2^(14 - e) for max < 2^e.
+// ~1e-3 without the scaling, ~1e-7 with it).  Scale = 2^(14 - e) for max < 2^e; the
+// max is exact: per board for the convolutions (whose sums stay within a board), per
+// group of boards for the weight gradient, per conv for the weights.
 __device__ __forceinline__ int f16_scale_exp(float m) {
     int ex = 0;
     if (m > 0.f && isfinite(m)) frexpf(m, &ex);
@@ -104,12 +105,14 @@ __global__ __launch_bounds__(256) void sgd_stats_kernel(const float* __restrict_
     const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
     const float* yb = y + (size_t)b * NPOS * CH + c;
     float s = 0.f;
+#pragma unroll 8
     for (int p = h; p < NPOS; p += 2) s += yb[(size_t)p * CH];
     red[h][c] = s;
     __syncthreads();
     const float mean = (red[0][c] + red[1][c]) * (1.f / NPOS);
     __syncthreads();
     float m2 = 0.f, mx = 0.f;
+#pragma unroll 8
     for (int p = h; p < NPOS; p += 2) {
         const float v = yb[(size_t)p * CH];
         m2 += (v - mean) * (v - mean);
@@ -131,49 +134,63 @@ __global__ __launch_bounds__(256) void sgd_stats_kernel(const float* __restrict_
 
 // batch statistics from the boards' partials (equal counts: Chan's combination in
 // fp64), BN scale/shift, the running-stat update (momentum, unbiased variance) --
-// torch BatchNorm2d in training mode
-// Also the bound of the activation relu(y s + t (+ skip)) it feeds to the next conv,
-// max_c |s| max|y| + |t| (+ the skip's bound, skip_coef), and that activation's f16x3 scale.
-__global__ __launch_bounds__(128) void sgd_bn_fwd_reduce_kernel(const float* __restrict__ part, int B,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta,
-                                                               float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                               float momentum, float eps, float* __restrict__ coef,
-                                                               const float* __restrict__ skip_coef) {
-    __shared__ float amax[2];
-    const int c = threadIdx.x;
+// torch BatchNorm2d in training mode.  1024 threads: channel c = tid % 128 over the
+// boards b = tid / 128 (mod 8), combined in LDS.
+constexpr int RED_THREADS = 1024, RED_PARTS = RED_THREADS / CH;
+__device__ __forceinline__ double red_sum(double v, double* sh, int c, int h) {
+    __syncthreads();
+    sh[h * CH + c] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < RED_PARTS; k++) t += sh[k * CH + c];
+    return t;
+}
+__device__ __forceinline__ double red_max(double v, double* sh, int c, int h) {
+    __syncthreads();
+    sh[h * CH + c] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < RED_PARTS; k++) t = fmax(t, sh[k * CH + c]);
+    return t;
+}
+__global__ __launch_bounds__(RED_THREADS) void sgd_bn_fwd_reduce_kernel(const float* __restrict__ part, int B,
+                                                                       const float* __restrict__ gamma,
+                                                                       const float* __restrict__ beta,
+                                                                       float* __restrict__ run_mean,
+                                                                       float* __restrict__ run_var, float momentum,
+                                                                       float eps, float* __restrict__ coef) {
+    __shared__ double sh[RED_THREADS];
+    const int c = threadIdx.x & (CH - 1), h = threadIdx.x / CH;
     double sm = 0.0, mx = 0.0;
-    for (int b = 0; b < B; b++) {
+#pragma unroll 4
+    for (int b = h; b < B; b += RED_PARTS) {
         sm += part[(size_t)b * PART + c];
         mx = fmax(mx, (double)part[(size_t)b * PART + 2 * CH + c]);
     }
-    const double mean = sm / B;
+    const double mean = red_sum(sm, sh, c, h) / B;
+    mx = red_max(mx, sh, c, h);
     double m2 = 0.0, dev = 0.0;
-    for (int b = 0; b < B; b++) {
+#pragma unroll 4
+    for (int b = h; b < B; b += RED_PARTS) {
         const double d = (double)part[(size_t)b * PART + c] - mean;
         m2 += part[(size_t)b * PART + CH + c] + (double)NPOS * d * d;
         dev += (double)NPOS * d;
     }
+    m2 = red_sum(m2, sh, c, h);
+    dev = red_sum(dev, sh, c, h);
+    if (h) return;
     const double M = (double)NPOS * B;
     const double var = m2 / M;
     const double inv = 1.0 / sqrt(var + (double)eps);
-    const float s = (float)(gamma[c] * inv);
-    coef[CO_S + c] = s;
-    coef[CO_T + c] = (float)(beta[c] - mean * (double)s);
+    const float sc = (float)(gamma[c] * inv);
+    coef[CO_S + c] = sc;
+    coef[CO_T + c] = (float)(beta[c] - mean * (double)sc);
     coef[CO_MEAN + c] = (float)mean;
     coef[CO_INV + c] = (float)inv;
     coef[CO_YMAX + c] = (float)mx;
     coef[CO_SUMXH + c] = (float)(dev * inv);
-    const float ab = wave_max(fabsf(s) * (float)mx + fabsf(coef[CO_T + c]));
-    if ((c & 63) == 0) amax[c >> 6] = ab;
-    __syncthreads();
-    if (c == 0) {
-        const float A = fmaxf(amax[0], amax[1]) + (skip_coef ? skip_coef[CO_ABOUND] : 0.f);
-        const int e = f16_scale_exp(A);
-        coef[CO_ABOUND] = A;
-        coef[CO_XSCALE] = ldexpf(1.f, e);
-        coef[CO_XINV] = ldexpf(1.f, -e);
-    }
     if (run_mean) {
         run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
         run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var * (M > 1.0 ? M / (M - 1.0) : 1.0));
@@ -181,20 +198,25 @@ __global__ __launch_bounds__(128) void sgd_bn_fwd_reduce_kernel(const float* __r
 }
 
 // backward of a BN + ReLU (+ skip) from the boards' partials of g = dL/d(BN output):
-// mean(g), mean(g * xhat), dgamma = sum g xhat, dbeta = sum g, the conv bias gradient
-// (sum of dL/dy over the rows), and the power-of-two scale of dL/dy for the f16x3 GEMM
-__global__ __launch_bounds__(128) void sgd_bn_bwd_reduce_kernel(const float* __restrict__ part, int B,
-                                                               const float* __restrict__ gamma, float* __restrict__ coef,
-                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                               float* __restrict__ dbias) {
-    __shared__ float bmax[2];
-    const int c = threadIdx.x;
-    double sg = 0.0, sgx = 0.0, mg_ = 0.0;
-    for (int b = 0; b < B; b++) {
+// mean(g), mean(g * xhat), dgamma = sum g xhat, dbeta = sum g and the conv bias gradient
+// (sum of dL/dy over the rows)
+__global__ __launch_bounds__(RED_THREADS) void sgd_bn_bwd_reduce_kernel(const float* __restrict__ part, int B,
+                                                                       const float* __restrict__ gamma,
+                                                                       float* __restrict__ coef,
+                                                                       float* __restrict__ dgamma,
+                                                                       float* __restrict__ dbeta,
+                                                                       float* __restrict__ dbias) {
+    __shared__ double sh[RED_THREADS];
+    const int c = threadIdx.x & (CH - 1), h = threadIdx.x / CH;
+    double sg = 0.0, sgx = 0.0;
+#pragma unroll 4
+    for (int b = h; b < B; b += RED_PARTS) {
         sg += part[(size_t)b * PART + c];
         sgx += part[(size_t)b * PART + CH + c];
-        mg_ = fmax(mg_, (double)part[(size_t)b * PART + 2 * CH + c]);
     }
+    sg = red_sum(sg, sh, c, h);
+    sgx = red_sum(sgx, sh, c, h);
+    if (h) return;
     const double M = (double)NPOS * B;
     const double mg = sg / M, mgx = sgx / M;
     const double inv = coef[CO_INV + c];
@@ -206,17 +228,6 @@ __global__ __launch_bounds__(128) void sgd_bn_bwd_reduce_kernel(const float* __r
     dbeta[c] = (float)sg;
     // sum over rows of k (g - mg - xhat mgx) = -k mgx sum(xhat)
     if (dbias) dbias[c] = (float)(-k * mgx * (double)coef[CO_SUMXH + c]);
-    // |dL/dy| <= |k| (max|g| + |mg| + max|xhat| |mgx|), max|xhat| <= (max|y| + |mean|) inv
-    const double xmax = ((double)coef[CO_YMAX + c] + fabs((double)coef[CO_MEAN + c])) * inv;
-    float bound = (float)(fabs(k) * (mg_ + fabs(mg) + xmax * fabs(mgx)));
-    float m = wave_max(bound);
-    if ((c & 63) == 0) bmax[c >> 6] = m;
-    __syncthreads();
-    if (c == 0) {
-        const int e = f16_scale_exp(fmaxf(bmax[0], bmax[1]));
-        coef[CO_SCALE] = ldexpf(1.f, e);
-        coef[CO_INVSCALE] = ldexpf(1.f, -e);
-    }
 }
 
 // g = dL/da * [a > 0] (the tower output's ReLU) and its BN-backward partials
@@ -227,6 +238,7 @@ __global__ __launch_bounds__(256) void sgd_mask_stats_kernel(const float* __rest
     const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
     const float mean = coef[CO_MEAN + c], inv = coef[CO_INV + c];
     float s = 0.f, sx = 0.f, mx = 0.f;
+#pragma unroll 8
     for (int p = h; p < NPOS; p += 2) {
         const size_t o = ((size_t)b * NPOS + p) * CH + c;
         const float v = act[o] > 0.f ? da[o] : 0.f;
@@ -293,6 +305,7 @@ struct ConvArgs {
     float* save;
     const _Float16* frag;  // the conv's fragments (hi plane, lo plane after it), weights x 2^k
     const float* winv;     // 2^-k
+    float* bmax;           // per board: max |staged input| (written by the workgroup saving it)
     // forward epilogue: y = acc + bias -> out, BN partials of y -> part
     const float* bias;
     // input-gradient epilogue: dx = acc / scale (+ eskip) -> g = dx [eact > 0] -> out,
@@ -469,9 +482,15 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
     act.lo = lds + 16 * ROWS16 * 8;
     const size_t board = (size_t)b * NPOS * CH;
     const bool save = a.save && blockIdx.x == 0;
-    const float scale = MODE == 1 ? a.coef[CO_SCALE] : a.coef[CO_XSCALE];
-#pragma unroll 4
-    for (int e = tid; e < NPOS * 32; e += CONV_THREADS) {  // (unrolled: 4 rows' loads in flight)
+    // the board's input plane: every value computed into registers first (STG per thread),
+    // the board's max |x| -> the power-of-two scale, then the scaled hi / lo into LDS
+    constexpr int STG = (NPOS * 32 + CONV_THREADS - 1) / CONV_THREADS;
+    f32x4 xs[STG];
+    float xmax = 0.f;
+#pragma unroll
+    for (int k = 0; k < STG; k++) {
+        const int e = tid + k * CONV_THREADS;
+        if (e >= NPOS * 32) continue;
         const int p = e >> 5, c0 = (e & 31) * 4;
         const size_t o = board + (size_t)p * CH + c0;
         const f32x4 v = *(const f32x4*)(a.src + o);
@@ -490,7 +509,24 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
             x = k * (v - mg - (yv - mean) * inv * mgx);
         }
         if (save) *(f32x4*)(a.save + o) = x;
-        x = x * scale;
+        xs[k] = x;
+        xmax = fmaxf(xmax, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+    }
+    xmax = wave_max(xmax);
+    if ((tid & 63) == 0) red[0][0][tid >> 6] = xmax;
+    __syncthreads();
+    xmax = red[0][0][0];
+#pragma unroll
+    for (int w8 = 1; w8 < CONV_THREADS / 64; w8++) xmax = fmaxf(xmax, red[0][0][w8]);
+    const int se = f16_scale_exp(xmax);
+    const float scale = ldexpf(1.f, se);
+    if (save && tid == 0) a.bmax[b] = xmax;  // the weight gradient's group scale
+#pragma unroll
+    for (int k = 0; k < STG; k++) {
+        const int e = tid + k * CONV_THREADS;
+        if (e >= NPOS * 32) continue;
+        const int p = e >> 5, c0 = (e & 31) * 4;
+        const f32x4 x = xs[k] * scale;
         h4 hi, lo;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -503,10 +539,10 @@ __global__ __launch_bounds__(CONV_THREADS, 1) void sgd_conv_kernel(ConvArgs a) {
         *(h4*)(act.lo + lo_off) = lo;
     }
     act.zero_slots(tid, CONV_THREADS, CH);
-    __syncthreads();
+    __syncthreads();  // (also: every wave has read red[0][0] before the epilogue reuses it)
     const int wave = tid >> 6, lane = tid & 63, mq = wave >> 1;
     const int np = 2 * blockIdx.x + (wave & 1);
-    const float sinv = (MODE == 1 ? a.coef[CO_INVSCALE] : a.coef[CO_XINV]) * *a.winv;
+    const float sinv = ldexpf(1.f, -se) * *a.winv;
     // quarter 3 has tiles 12..14; its fourth tile (positions 240..255) stays zero and
     // is skipped by the epilogue (every wave runs the same epilogue and barriers)
     f32x4 acc[2][4];
@@ -570,15 +606,22 @@ __device__ __forceinline__ h8 w16_cat(h4 a, h4 b) {
 }
 __global__ __launch_bounds__(WG_THREADS, 1) void sgd_wgrad16_kernel(const float* __restrict__ x,
                                                                    const float* __restrict__ dy,
-                                                                   const float* __restrict__ coef,
-                                                                   const float* __restrict__ xcoef, int B, int G,
+                                                                   const float* __restrict__ xmax,
+                                                                   const float* __restrict__ dymax, int B, int G,
                                                                    int NG, float* __restrict__ wpart) {
     __shared__ __attribute__((aligned(16))) char lds[4 * W16_PLANE];  // x hi, x lo, dy hi, dy lo
     const int cq = blockIdx.x & 1, nq = (blockIdx.x >> 1) & 1, grp = blockIdx.x >> 2;
     const int b0 = grp * G, b1 = b0 + G < B ? b0 + G : B;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, q = (lane >> 2) & 3, pc = lane & 3;
-    const float S = coef[CO_SCALE], SX = xcoef[CO_XSCALE], unscale = coef[CO_INVSCALE] * xcoef[CO_XINV];
+    // the group's scales from its boards' max |x|, max |dy| (the convolutions' staging)
+    float mx = 0.f, md = 0.f;
+    for (int b = b0; b < b1; b++) {
+        mx = fmaxf(mx, xmax[b]);
+        md = fmaxf(md, dymax[b]);
+    }
+    const int ex = f16_scale_exp(mx), ed = f16_scale_exp(md);
+    const float S = ldexpf(1.f, ed), SX = ldexpf(1.f, ex), unscale = ldexpf(1.f, -ed - ex);
     f32x4 acc[9][4];
 #pragma unroll
     for (int t = 0; t < 9; t++)
@@ -663,6 +706,7 @@ __global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, floa
     const int tap = e / (CH * CH), rem = e - tap * CH * CH, c = rem >> 7, n = rem & 127;
     const float* p = wpart + (size_t)tap * NG * CH * CH + rem;
     float s = 0.f;
+#pragma unroll 8
     for (int g = 0; g < NG; g++) s += p[(size_t)g * CH * CH];
     dw[((size_t)n * CH + c) * 9 + tap] = s;
 }
@@ -676,6 +720,8 @@ struct Ws {
     float* dy;        // dL/dy of the current conv (weight gradient operand)
     float* coef;      // [NBN][CO_FLOATS]
     float* wsc;       // weight scales (sgd_pack_kernel)
+    float* xmax;      // [4][B] max |conv input| per board (forward staging)
+    float* dymax;     // [4][B] max |dL/dy| per board (input-gradient staging)
     float* fpart;     // [NBN][B][PART]
     float* bpart;     // [NBN][B][PART]
     float* wpart;     // [9][NG][CH][CH]
@@ -700,6 +746,8 @@ size_t ws_layout(int B, Ws* w, char* base) {
     t.dy = (float*)take(R);
     t.coef = (float*)take((size_t)NBN * CO_FLOATS * sizeof(float));
     t.wsc = (float*)take(8 * sizeof(float));
+    t.xmax = (float*)take((size_t)4 * B * sizeof(float));
+    t.dymax = (float*)take((size_t)4 * B * sizeof(float));
     t.fpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.bpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.wpart = (float*)take((size_t)9 * NG * CH * CH * sizeof(float));
@@ -754,8 +802,9 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
     sgd_wmax_kernel<<<dim3(32, LAYERS), 256, 0, s>>>(pa, (unsigned*)w.wsc);
     sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.wsc, w.frag);
     sgd_stats_kernel<<<B, 256, 0, s>>>(d_y0, w.fpart);
-    sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0], net->bn_running_mean[0],
-                                             net->bn_running_var[0], net->momentum, net->eps, w.coef, nullptr);
+    sgd_bn_fwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0],
+                                                      net->bn_running_mean[0], net->bn_running_var[0], net->momentum,
+                                                      net->eps, w.coef);
     if ((rc = sgd_check("gz_sgd_forward: BN0"))) return rc;
     // conv L (1..4): input = relu(BN_{L-1}(y_{L-1}) (+ skip)), skip a0 for conv 3's input a1
     for (int L = 1; L <= LAYERS; L++) {
@@ -766,14 +815,14 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
         a.save = w.act[L - 1];
         a.frag = w.frag + (size_t)((L - 1) * 2 + 0) * 2 * FRAG_HALVES;
         a.winv = w.wsc + 4 + (L - 1);
+        a.bmax = w.xmax + (size_t)(L - 1) * B;
         a.bias = net->conv_bias[L - 1];
         a.out = w.y[L];
         a.part = w.fpart + (size_t)L * B * PART;
         sgd_conv_kernel<0><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
-        sgd_bn_fwd_reduce_kernel<<<1, CH, 0, s>>>(a.part, B, net->bn_weight[L], net->bn_bias[L],
-                                                 net->bn_running_mean[L], net->bn_running_var[L], net->momentum,
-                                                 net->eps, w.coef + (size_t)L * CO_FLOATS,
-                                                 L == 2 ? w.coef : nullptr);  // BN2's output adds the skip a0
+        sgd_bn_fwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(a.part, B, net->bn_weight[L], net->bn_bias[L],
+                                                          net->bn_running_mean[L], net->bn_running_var[L],
+                                                          net->momentum, net->eps, w.coef + (size_t)L * CO_FLOATS);
         if ((rc = sgd_check("gz_sgd_forward: conv"))) return rc;
     }
     // a2 = relu(BN4(y4) + a1)
@@ -800,8 +849,8 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
                                             w.bpart + (size_t)4 * B * PART);
     for (int L = LAYERS; L >= 1; L--) {
         float* coefL = w.coef + (size_t)L * CO_FLOATS;
-        sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart + (size_t)L * B * PART, B, net->bn_weight[L], coefL,
-                                                 gr->bn_weight[L], gr->bn_bias[L], gr->conv_bias[L - 1]);
+        sgd_bn_bwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.bpart + (size_t)L * B * PART, B, net->bn_weight[L],
+                                                          coefL, gr->bn_weight[L], gr->bn_bias[L], gr->conv_bias[L - 1]);
         // input gradient of conv L: dy_L = k (g_L - mg - xhat mgx) staged (and saved for the
         // weight gradient); its output is dL/d(input of conv L) -> masked by that
         // activation's ReLU (+ the skip gradient: g4 into a1, g2 into a0)
@@ -812,6 +861,7 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         a.save = w.dy;
         a.frag = w.frag + (size_t)((L - 1) * 2 + 1) * 2 * FRAG_HALVES;
         a.winv = w.wsc + 4 + (L - 1);
+        a.bmax = w.dymax + (size_t)(L - 1) * B;
         a.eskip = L == 3 ? w.g[4] : (L == 1 ? w.g[2] : nullptr);
         a.eact = w.act[L - 1];
         a.ey = w.y[L - 1];
@@ -819,13 +869,13 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         a.out = w.g[L - 1];
         a.part = w.bpart + (size_t)(L - 1) * B * PART;
         sgd_conv_kernel<1><<<dim3(2, B), CONV_THREADS, 0, s>>>(a);
-        sgd_wgrad16_kernel<<<4 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, coefL, a.ecoef, B, w.G, w.NG,
-                                                           w.wpart);
+        sgd_wgrad16_kernel<<<4 * w.NG, WG_THREADS, 0, s>>>(w.act[L - 1], w.dy, w.xmax + (size_t)(L - 1) * B,
+                                                           w.dymax + (size_t)(L - 1) * B, B, w.G, w.NG, w.wpart);
         sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, gr->conv_weight[L - 1]);
         if ((rc = sgd_check("gz_sgd_backward: conv"))) return rc;
     }
-    sgd_bn_bwd_reduce_kernel<<<1, CH, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0], gr->bn_bias[0],
-                                             nullptr);
+    sgd_bn_bwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0],
+                                                      gr->bn_bias[0], nullptr);
     sgd_bn_dy_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(w.g[0], d_y0, w.coef, d_dy0, n4);
     return sgd_check("gz_sgd_backward: BN0");
 }

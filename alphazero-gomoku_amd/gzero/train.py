@@ -157,10 +157,10 @@ class DeviceTrainer:
     On a GPU the training forward/backward of the residual tower runs on the HIP
     kernels of csrc/gz_sgd.hip (``gzero.sgd.train_forward``; ``native=False``: torch's
     own convolutions, kept for comparison); on the CPU (gloo rehearsals of the
-    data-parallel loop) it is torch's.  On one GPU a full batch's step (zero_grad,
-    forward, loss, backward, clip, Adam) is captured once into a HIP graph and
-    replayed with each batch gathered into its static inputs (``graphs``): about a
-    hundred kernel launches per step become one replay.  The graph is re-captured when
+    data-parallel loop) it is torch's.  ``graphs=True`` (one GPU): a full batch's step
+    (zero_grad, forward, loss, backward, clip, Adam) is captured once into a HIP graph
+    and replayed with each batch gathered into its static inputs: about a hundred
+    kernel launches per step become one replay.  The graph is re-captured when
     the learning rate changes (StepLR); the first full batch of a trainer runs eagerly
     (it creates Adam's state), as do remainder batches."""
 
@@ -183,7 +183,7 @@ class DeviceTrainer:
         self.world, self.rank = _world(group)
         self._warm = False
         self.params = [p for p in self.net.parameters()]
-        self.graphs = (self.native and self.world == 1) if graphs is None else bool(graphs)
+        self.graphs = False if graphs is None else bool(graphs)
         self._graph = None
         # capturable: Adam's step count and bias corrections stay on the device (graph replay)
         self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay, capturable=self.graphs)
@@ -252,6 +252,7 @@ class DeviceTrainer:
                 loss = self.ce(logits, y) + self.mse(val, v)
                 (loss * (local / gcount) if self.world > 1 else loss).backward()
                 lval = loss.detach()
+                del logits, val, loss  # no autograd graph outlives the step (graph capture)
             else:
                 lval = torch.zeros((), device=self.device)
             if self.world > 1:

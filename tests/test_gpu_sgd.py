@@ -130,3 +130,32 @@ def test_sgd_tower_two_steps_match_torch_trainer():
     np.testing.assert_allclose(losses[0], losses[1], rtol=1e-4)
     for (k, a), (_, b) in zip(nets[0].named_buffers(), nets[1].named_buffers()):
         assert torch.allclose(a.float(), b.float(), rtol=1e-5, atol=1e-5), k
+
+
+def test_trainer_graph_replay_matches_eager():
+    """DeviceTrainer(graphs=True): two epochs whose full batches replay one captured
+    HIP graph (re-captured after the StepLR change) give the eager trainer's losses
+    within 1e-5 and the same running statistics."""
+    import random
+    from gzero import boards
+    from gzero.train import DeviceDataset, DeviceTrainer
+    rng = np.random.default_rng(SEED)
+    cells = rng.choice(np.array([0, 0, 0, 1, 2], np.int8), size=(300, 225))
+    rec = np.zeros(300, boards.RECORD_DTYPE)
+    rec["black"], rec["white"] = boards.cells_to_words(cells)
+    rec["move"] = rng.integers(0, 225, 300)
+    rec["z"] = rng.integers(-1, 2, 300)
+    out = []
+    for graphs in (False, True):
+        ds = DeviceDataset(rec, augment_ratio=0.35, rng=random.Random(0))
+        net = _net(SEED).cuda()
+        tr = DeviceTrainer(net, graphs=graphs, step_size=1)
+        torch.manual_seed(5)
+        losses = []
+        for _ in range(2):
+            losses.append(tr.train_epoch(ds, 128))
+            tr.step_scheduler()
+        out.append((losses, {k: b.detach().clone() for k, b in net.named_buffers()}))
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-5)
+    for k, b in out[0][1].items():
+        assert torch.allclose(out[1][1][k].float(), b.float(), rtol=1e-5, atol=1e-6), k

@@ -47,11 +47,13 @@ def run(tag, steps=60, bs=128, channels_last=False, native=False):
     print(f"{tag}: {dt * 1e3:.2f} ms/step, {bs * 3 * 267.38e6 / dt / 1e12:.1f} TFLOP/s", flush=True)
 
 
+ONLY = sys.argv[1] if len(sys.argv) > 1 else None  # "native": just the device-tower runs (profiling)
 run("native", native=True)
-run("default")
-torch.backends.cudnn.benchmark = True
-run("benchmark")
-run("benchmark+channels_last", channels_last=True)
+if ONLY != "native":
+    run("default")
+    torch.backends.cudnn.benchmark = True
+    run("benchmark")
+    run("benchmark+channels_last", channels_last=True)
 
 
 def trainer_run(tag, n_records=4000, **kw):
@@ -80,7 +82,9 @@ def trainer_run(tag, n_records=4000, **kw):
 
 
 torch.backends.cudnn.benchmark = False
-trainer_run("native+graph", native=True)
-trainer_run("native+graph-2nd", native=True)
-trainer_run("native, no graph", native=True, graphs=False)
-trainer_run("miopen", native=False)
+trainer_run("native", native=True)
+trainer_run("native-2nd", native=True)
+if ONLY != "native":
+    trainer_run("miopen", native=False)
+if ONLY == "graphs":
+    trainer_run("native+graph", native=True, graphs=True)
