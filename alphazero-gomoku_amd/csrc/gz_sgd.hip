@@ -781,6 +781,20 @@ int check_net(const gz_sgd_net* net, int B, const void* ws) {
 
 }  // namespace
 
+// a copy of what gz_sgd_forward saved (checkers): which 0..3 = the inputs of conv 1..4
+// (a0, h1, a1, h2), 4..7 = the conv outputs y1..y4; fp32 NHWC [boards][225][128]
+extern "C" int gz_sgd_saved(const void* d_ws, int32_t B, int32_t which, float* d_out, void* stream) {
+    if (!d_ws || !d_out || B < 1 || B > GZ_SGD_MAX_BOARDS || which < 0 || which > 7)
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd_saved: bad arguments");
+    Ws w;
+    ws_layout(B, &w, (char*)d_ws);
+    const float* src = which < 4 ? w.act[which] : w.y[which - 3];
+    if (hipMemcpyAsync(d_out, src, (size_t)B * NPOS * CH * sizeof(float), hipMemcpyDeviceToDevice,
+                       (hipStream_t)stream) != hipSuccess)
+        return sgd_fail(GZ_ERR_HIP, "gz_sgd_saved: copy");
+    return GZ_OK;
+}
+
 extern "C" size_t gz_sgd_workspace_bytes(int32_t boards) {
     return boards < 1 ? 0 : ws_layout(boards, nullptr, nullptr);
 }

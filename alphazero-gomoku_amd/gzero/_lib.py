@@ -140,6 +140,7 @@ SIGNATURES = {
     "gz_sgd_forward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P]),
     "gz_sgd_backward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P, ctypes.POINTER(SgdGrads), _P,
                                        _P]),
+    "gz_sgd_saved": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
 }
 
 _lib = None

@@ -185,8 +185,10 @@ class DeviceTrainer:
         self.params = [p for p in self.net.parameters()]
         self.graphs = False if graphs is None else bool(graphs)
         self._graph = None
-        # capturable: Adam's step count and bias corrections stay on the device (graph replay)
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay, capturable=self.graphs)
+        # capturable (on the GPU): Adam's step count and bias corrections stay on the device,
+        # so eager steps and graph replays run the same arithmetic
+        self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay,
+                                          capturable=self.device.type == "cuda")
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=step_size, gamma=gamma)
         self.ce, self.mse = nn.CrossEntropyLoss(), nn.MSELoss()
         if self.world > 1:
@@ -294,7 +296,7 @@ class DeviceTrainer:
                 if self.grad_clip is not None and self.grad_clip > 0:
                     nn.utils.clip_grad_norm_(self.params, self.grad_clip)
                 self.optimizer.step()
-            g.update(graph=graph, lr=lr, loss=loss)
+            g.update(graph=graph, lr=lr, loss=loss.detach())  # (no autograd graph kept alive)
         g["graph"].replay()
         return g["loss"]
 

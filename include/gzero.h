@@ -350,6 +350,10 @@ int gz_sgd_forward(const gz_sgd_net* net, int32_t boards, const float* d_y0, flo
  * are the forward's, the workspace the one that forward used */
 int gz_sgd_backward(const gz_sgd_net* net, int32_t boards, const float* d_y0, const float* d_out,
                     const float* d_dout, float* d_dy0, const gz_sgd_grads* grads, void* d_workspace, void* stream);
+/* checkers: a copy of a saved tensor of the last gz_sgd_forward on this workspace:
+ * which 0..3 = the inputs of the four residual convs (a0, h1, a1, h2), 4..7 = their
+ * outputs y1..y4 (fp32 NHWC) */
+int gz_sgd_saved(const void* d_workspace, int32_t boards, int32_t which, float* d_out, void* stream);
 
 #ifdef __cplusplus
 }
