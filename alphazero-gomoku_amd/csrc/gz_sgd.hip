@@ -98,37 +98,51 @@ __global__ void sgd_pack_kernel(PackArgs a, float* __restrict__ wsc, _Float16* _
 }
 
 // ---------------------------------------------------------------- BN statistics
-// per board: per-channel mean, centred sum of squares and max |y| of y0 (the
-// torch conv0 output; the residual convs produce theirs in their epilogue)
-__global__ __launch_bounds__(256) void sgd_stats_kernel(const float* __restrict__ y, float* __restrict__ part) {
-    __shared__ float red[2][CH];
-    const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
-    const float* yb = y + (size_t)b * NPOS * CH + c;
-    float s = 0.f;
-#pragma unroll 8
-    for (int p = h; p < NPOS; p += 2) s += yb[(size_t)p * CH];
-    red[h][c] = s;
+// Per-board kernels: 256 threads = 32 channel quads (float4) x 8 position strides; the
+// board's 225 x 128 values are read once into registers (29 float4 per thread), then
+// reduced over the 8 strides in LDS.
+constexpr int PB_THREADS = 256, PB_STRIDES = PB_THREADS / 32, PB_ITEMS = (NPOS + PB_STRIDES - 1) / PB_STRIDES;
+__device__ __forceinline__ f32x4 pb_reduce(f32x4 v, f32x4* sh, int q, int h, bool mx) {
     __syncthreads();
-    const float mean = (red[0][c] + red[1][c]) * (1.f / NPOS);
+    sh[h * 32 + q] = v;
     __syncthreads();
-    float m2 = 0.f, mx = 0.f;
-#pragma unroll 8
-    for (int p = h; p < NPOS; p += 2) {
-        const float v = yb[(size_t)p * CH];
-        m2 += (v - mean) * (v - mean);
-        mx = fmaxf(mx, fabsf(v));
+    f32x4 t = sh[q];
+#pragma unroll
+    for (int k = 1; k < PB_STRIDES; k++) {
+        const f32x4 u = sh[k * 32 + q];
+#pragma unroll
+        for (int r = 0; r < 4; r++) t[r] = mx ? fmaxf(t[r], u[r]) : t[r] + u[r];
     }
-    red[h][c] = m2;
-    __syncthreads();
-    const float m2t = red[0][c] + red[1][c];
-    __syncthreads();
-    red[h][c] = mx;
-    __syncthreads();
+    return t;
+}
+
+// per board: per-channel mean, centred sum of squares and max |y| of y0 (the torch
+// conv0 output; the residual convs produce theirs in their epilogue)
+__global__ __launch_bounds__(PB_THREADS) void sgd_stats_kernel(const float* __restrict__ y, float* __restrict__ part) {
+    __shared__ f32x4 sh[PB_THREADS];
+    const int b = blockIdx.x, q = threadIdx.x & 31, h = threadIdx.x >> 5;
+    const f32x4* yb = (const f32x4*)(y + (size_t)b * NPOS * CH) + q;
+    f32x4 v[PB_ITEMS], s = zero4(), mx = zero4();
+#pragma unroll
+    for (int k = 0; k < PB_ITEMS; k++) {
+        const int p = h + k * PB_STRIDES;
+        v[k] = p < NPOS ? yb[(size_t)p * 32] : zero4();
+        s += v[k];
+#pragma unroll
+        for (int r = 0; r < 4; r++) mx[r] = fmaxf(mx[r], fabsf(v[k][r]));
+    }
+    const f32x4 mean = pb_reduce(s, sh, q, h, false) * (1.f / NPOS);
+    f32x4 m2 = zero4();
+#pragma unroll
+    for (int k = 0; k < PB_ITEMS; k++)
+        if (h + k * PB_STRIDES < NPOS) m2 += (v[k] - mean) * (v[k] - mean);
+    m2 = pb_reduce(m2, sh, q, h, false);
+    mx = pb_reduce(mx, sh, q, h, true);
     if (h == 0) {
-        float* o = part + (size_t)b * PART;
-        o[c] = mean;
-        o[CH + c] = m2t;
-        o[2 * CH + c] = fmaxf(red[0][c], red[1][c]);
+        float* o = part + (size_t)b * PART + 4 * q;
+        *(f32x4*)o = mean;
+        *(f32x4*)(o + CH) = m2;
+        *(f32x4*)(o + 2 * CH) = mx;
     }
 }
 
@@ -231,31 +245,38 @@ __global__ __launch_bounds__(RED_THREADS) void sgd_bn_bwd_reduce_kernel(const fl
 }
 
 // g = dL/da * [a > 0] (the tower output's ReLU) and its BN-backward partials
-__global__ __launch_bounds__(256) void sgd_mask_stats_kernel(const float* __restrict__ da, const float* __restrict__ act,
-                                                            const float* __restrict__ y, const float* __restrict__ coef,
-                                                            float* __restrict__ g, float* __restrict__ part) {
-    __shared__ float red[3][2][CH];
-    const int b = blockIdx.x, c = threadIdx.x & 127, h = threadIdx.x >> 7;
-    const float mean = coef[CO_MEAN + c], inv = coef[CO_INV + c];
-    float s = 0.f, sx = 0.f, mx = 0.f;
+__global__ __launch_bounds__(PB_THREADS) void sgd_mask_stats_kernel(const float* __restrict__ da,
+                                                                   const float* __restrict__ act,
+                                                                   const float* __restrict__ y,
+                                                                   const float* __restrict__ coef,
+                                                                   float* __restrict__ g, float* __restrict__ part) {
+    __shared__ f32x4 sh[PB_THREADS];
+    const int b = blockIdx.x, q = threadIdx.x & 31, h = threadIdx.x >> 5;
+    const f32x4 mean = *(const f32x4*)(coef + CO_MEAN + 4 * q), inv = *(const f32x4*)(coef + CO_INV + 4 * q);
+    const size_t base = (size_t)b * NPOS * 32 + q;
+    f32x4 s = zero4(), sx = zero4(), mx = zero4();
 #pragma unroll 8
-    for (int p = h; p < NPOS; p += 2) {
-        const size_t o = ((size_t)b * NPOS + p) * CH + c;
-        const float v = act[o] > 0.f ? da[o] : 0.f;
-        g[o] = v;
+    for (int p = h; p < NPOS; p += PB_STRIDES) {
+        const size_t o = base + (size_t)p * 32;
+        const f32x4 d = ((const f32x4*)da)[o], a = ((const f32x4*)act)[o], yv = ((const f32x4*)y)[o];
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            v[r] = a[r] > 0.f ? d[r] : 0.f;
+            mx[r] = fmaxf(mx[r], fabsf(v[r]));
+        }
+        ((f32x4*)g)[o] = v;
         s += v;
-        sx += v * ((y[o] - mean) * inv);
-        mx = fmaxf(mx, fabsf(v));
+        sx += v * ((yv - mean) * inv);
     }
-    red[0][h][c] = s;
-    red[1][h][c] = sx;
-    red[2][h][c] = mx;
-    __syncthreads();
+    s = pb_reduce(s, sh, q, h, false);
+    sx = pb_reduce(sx, sh, q, h, false);
+    mx = pb_reduce(mx, sh, q, h, true);
     if (h == 0) {
-        float* o = part + (size_t)b * PART;
-        o[c] = red[0][0][c] + red[0][1][c];
-        o[CH + c] = red[1][0][c] + red[1][1][c];
-        o[2 * CH + c] = fmaxf(red[2][0][c], red[2][1][c]);
+        float* o = part + (size_t)b * PART + 4 * q;
+        *(f32x4*)o = s;
+        *(f32x4*)(o + CH) = sx;
+        *(f32x4*)(o + 2 * CH) = mx;
     }
 }
 
@@ -815,7 +836,7 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
         return sgd_fail(GZ_ERR_HIP, "gz_sgd_forward: memset");
     sgd_wmax_kernel<<<dim3(32, LAYERS), 256, 0, s>>>(pa, (unsigned*)w.wsc);
     sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.wsc, w.frag);
-    sgd_stats_kernel<<<B, 256, 0, s>>>(d_y0, w.fpart);
+    sgd_stats_kernel<<<B, PB_THREADS, 0, s>>>(d_y0, w.fpart);
     sgd_bn_fwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0],
                                                       net->bn_running_mean[0], net->bn_running_var[0], net->momentum,
                                                       net->eps, w.coef);
@@ -859,7 +880,7 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
     w.y[0] = (float*)d_y0;
     const long long n4 = (long long)B * NPOS * CH / 4;
     // g4 = dL/d(BN4 output) = dout [out > 0]; also the skip gradient into a1
-    sgd_mask_stats_kernel<<<B, 256, 0, s>>>(d_dout, d_out, w.y[4], w.coef + 4 * CO_FLOATS, w.g[4],
+    sgd_mask_stats_kernel<<<B, PB_THREADS, 0, s>>>(d_dout, d_out, w.y[4], w.coef + 4 * CO_FLOATS, w.g[4],
                                             w.bpart + (size_t)4 * B * PART);
     for (int L = LAYERS; L >= 1; L--) {
         float* coefL = w.coef + (size_t)L * CO_FLOATS;

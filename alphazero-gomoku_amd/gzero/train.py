@@ -157,15 +157,11 @@ class DeviceTrainer:
     On a GPU the training forward/backward of the residual tower runs on the HIP
     kernels of csrc/gz_sgd.hip (``gzero.sgd.train_forward``; ``native=False``: torch's
     own convolutions, kept for comparison); on the CPU (gloo rehearsals of the
-    data-parallel loop) it is torch's.  ``graphs=True`` (one GPU): a full batch's step
-    (zero_grad, forward, loss, backward, clip, Adam) is captured once into a HIP graph
-    and replayed with each batch gathered into its static inputs: about a hundred
-    kernel launches per step become one replay.  The graph is re-captured when
-    the learning rate changes (StepLR); the first full batch of a trainer runs eagerly
-    (it creates Adam's state), as do remainder batches."""
+    data-parallel loop) it is torch's.  On the GPU Adam is torch's fused
+    implementation (one kernel per step instead of a dozen multi-tensor passes)."""
 
     def __init__(self, model, lr=8e-4, weight_decay=1e-5, grad_clip=0.8, step_size=2, gamma=0.85, group=None,
-                 device="cuda", native=None, graphs=None):
+                 device="cuda", native=None):
         self.gm = model
         self.net = model.model if hasattr(model, "model") else model
         self.device = torch.device(device)
@@ -181,14 +177,9 @@ class DeviceTrainer:
             self._forward = self.net
         self.group = group
         self.world, self.rank = _world(group)
-        self._warm = False
         self.params = [p for p in self.net.parameters()]
-        self.graphs = False if graphs is None else bool(graphs)
-        self._graph = None
-        # capturable (on the GPU): Adam's step count and bias corrections stay on the device,
-        # so eager steps and graph replays run the same arithmetic
         self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay,
-                                          capturable=self.device.type == "cuda")
+                                          fused=True if self.device.type == "cuda" else None)
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=step_size, gamma=gamma)
         self.ce, self.mse = nn.CrossEntropyLoss(), nn.MSELoss()
         if self.world > 1:
@@ -243,10 +234,6 @@ class DeviceTrainer:
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         batches = 0
         for mine, local, gcount in self._slices(ids_all, batch_size):
-            if self.graphs and local == batch_size and self.world == 1 and self._warm:
-                total += self._graph_step(ds, mine, batch_size).double()
-                batches += 1
-                continue
             self.optimizer.zero_grad(set_to_none=False)
             if local > 0:
                 x, y, v = _gather(ds, mine)
@@ -254,7 +241,6 @@ class DeviceTrainer:
                 loss = self.ce(logits, y) + self.mse(val, v)
                 (loss * (local / gcount) if self.world > 1 else loss).backward()
                 lval = loss.detach()
-                del logits, val, loss  # no autograd graph outlives the step (graph capture)
             else:
                 lval = torch.zeros((), device=self.device)
             if self.world > 1:
@@ -267,38 +253,10 @@ class DeviceTrainer:
             self.optimizer.step()
             total += lval.double()
             batches += 1
-            self._warm = self._warm or local == batch_size
         if self.world > 1:
             for t in self.net.buffers():  # BatchNorm running stats: rank 0's, as DDP's broadcast_buffers
                 dist.broadcast(t, 0, group=self.group)
         return float(total.item()) / max(1, batches)
-
-    def _graph_step(self, ds, ids, B):
-        """One full-batch step by graph replay (captured on first use and after a
-        learning-rate change); returns the batch loss (a device scalar)."""
-        lr = tuple(float(pg["lr"]) for pg in self.optimizer.param_groups)
-        g = self._graph
-        if g is None or g["B"] != B:
-            g = self._graph = {"B": B, "lr": None, "graph": None,
-                               "in": (torch.empty((B,) + SAMPLE_SHAPE, dtype=torch.float32, device=self.device),
-                                      torch.empty(B, dtype=torch.int64, device=self.device),
-                                      torch.empty((B, 1), dtype=torch.float32, device=self.device))}
-        x, y, v = g["in"]
-        ds.gather(ids, out=(x, y, v), check=False) if isinstance(ds, DeviceDataset) else \
-            [t.copy_(u) for t, u in zip((x, y, v), ds.gather(ids))]
-        if g["graph"] is None or g["lr"] != lr:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                self.optimizer.zero_grad(set_to_none=False)
-                logits, val = self._forward(x)
-                loss = self.ce(logits, y) + self.mse(val, v)
-                loss.backward()
-                if self.grad_clip is not None and self.grad_clip > 0:
-                    nn.utils.clip_grad_norm_(self.params, self.grad_clip)
-                self.optimizer.step()
-            g.update(graph=graph, lr=lr, loss=loss.detach())  # (no autograd graph kept alive)
-        g["graph"].replay()
-        return g["loss"]
 
     @torch.no_grad()
     def validate_epoch(self, ds, batch_size=128, indices=None):

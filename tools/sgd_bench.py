@@ -16,7 +16,7 @@ def run(tag, steps=60, bs=128, channels_last=False, native=False):
     net = weights.PolicyValueNet().cuda()
     if channels_last:
         net = net.to(memory_format=torch.channels_last)
-    opt = torch.optim.Adam(net.parameters(), lr=8e-4, weight_decay=1e-5)
+    opt = torch.optim.Adam(net.parameters(), lr=8e-4, weight_decay=1e-5, fused=native)
     ce, mse = nn.CrossEntropyLoss(), nn.MSELoss()
     x = (torch.rand((bs, 3, 15, 15), device="cuda") < 0.3).float()
     if channels_last:
@@ -86,5 +86,4 @@ trainer_run("native", native=True)
 trainer_run("native-2nd", native=True)
 if ONLY != "native":
     trainer_run("miopen", native=False)
-if ONLY == "graphs":
-    trainer_run("native+graph", native=True, graphs=True)
+
