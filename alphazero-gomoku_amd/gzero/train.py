@@ -234,7 +234,9 @@ class DeviceTrainer:
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         batches = 0
         for mine, local, gcount in self._slices(ids_all, batch_size):
-            self.optimizer.zero_grad(set_to_none=False)
+            # (torch's default, as training.py:292: fresh gradients are assigned, not added
+            # into zero-filled ones -- about 60 fewer kernels per step)
+            self.optimizer.zero_grad(set_to_none=True)
             if local > 0:
                 x, y, v = _gather(ds, mine)
                 logits, val = self._forward(x)

@@ -272,7 +272,7 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
         steps += 1
         # the step's one host synchronisation: moves, finished games and every loss counter
         c = torch.cat([eng.d_counters.view(torch.int64)[2:3], col.games, ex.overflow, col.dropped,
-                       eng.d_counters[0:4].view(torch.int32)[2:3].to(torch.int64)]).cpu().tolist()
+                       eng.d_counters[0:16].view(torch.int32)[2:3].to(torch.int64)]).cpu().tolist()
         moves += int(c[0])
         if c[2] or c[3] or c[4]:
             raise RuntimeError(f"selfplay_device: records lost (exchange overflow {c[2]}, collector {c[3]}, "
