@@ -34,7 +34,18 @@ for k in sys.argv[2:]:
             n += 1
     after[k] = {"gaps": n, "total_ms": round(tot / 1e6, 3), "mean_us": round(tot / max(1, n) / 1e3, 2)}
 big = [g for g, _ in gaps if g > 20000]
+# the kernels on either side of the gaps over 20 us
+pairs = {}
+for (s0, e0, n0), (s1, e1, n1) in zip(rows, rows[1:]):
+    if s1 - e0 > 20000:
+        k = (n0.split("(")[0][-40:], n1.split("(")[0][-40:])
+        c = pairs.setdefault(k, [0, 0])
+        c[0] += 1
+        c[1] += s1 - e0
+top_pairs = sorted(pairs.items(), key=lambda kv: -kv[1][1])[:8]
 print(json.dumps({"kernels": len(rows), "span_ms": round(span / 1e6, 3), "busy_ms": round(busy / 1e6, 3),
                   "idle_ms": round((span - busy) / 1e6, 3), "gaps": len(gaps),
                   "gaps_over_20us": len(big), "gaps_over_20us_ms": round(sum(big) / 1e6, 3),
-                  "after": after}, indent=1))
+                  "after": after,
+                  "big_gaps_between": [{"before": k[0], "after": k[1], "count": v[0], "total_ms": round(v[1] / 1e6, 3)}
+                                       for k, v in top_pairs]}, indent=1))
