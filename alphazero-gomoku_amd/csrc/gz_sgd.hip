@@ -116,17 +116,47 @@ __device__ __forceinline__ f32x4 pb_reduce(f32x4 v, f32x4* sh, int q, int h, boo
     return t;
 }
 
-// per board: per-channel mean, centred sum of squares and max |y| of y0 (the torch
-// conv0 output; the residual convs produce theirs in their epilogue)
-__global__ __launch_bounds__(PB_THREADS) void sgd_stats_kernel(const float* __restrict__ y, float* __restrict__ part) {
+// conv0 (3 -> 128 channels, 3x3, fp32 FMA) of a board's planes [3][15][15] into y0
+// (NHWC), and the per-channel mean, centred sum of squares and max |y| of the board
+// (the residual convs produce theirs in their epilogue).  The planes (zero-padded to
+// 17 x 17) and the weights, transposed to [ci*9 + tap][co], sit in LDS.
+constexpr int C0K = 27;
+__device__ __forceinline__ void c0_stage(const float* __restrict__ x, int b, float* xs, int tid) {
+    for (int i = tid; i < 3 * 17 * 17; i += PB_THREADS) {
+        const int ci = i / 289, r = (i % 289) / 17 - 1, c = i % 17 - 1;
+        xs[i] = (r >= 0 && r < 15 && c >= 0 && c < 15) ? x[((size_t)b * 3 + ci) * NPOS + r * 15 + c] : 0.f;
+    }
+}
+__global__ __launch_bounds__(PB_THREADS) void sgd_conv0_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ w0,
+                                                              const float* __restrict__ b0, float* __restrict__ y,
+                                                              float* __restrict__ part) {
     __shared__ f32x4 sh[PB_THREADS];
-    const int b = blockIdx.x, q = threadIdx.x & 31, h = threadIdx.x >> 5;
-    const f32x4* yb = (const f32x4*)(y + (size_t)b * NPOS * CH) + q;
+    __shared__ float xs[3 * 17 * 17];
+    __shared__ __attribute__((aligned(16))) float ws[C0K * CH];
+    const int b = blockIdx.x, tid = threadIdx.x, q = tid & 31, h = tid >> 5;
+    c0_stage(x, b, xs, tid);
+    for (int i = tid; i < C0K * CH; i += PB_THREADS) ws[(i % C0K) * CH + i / C0K] = w0[i];  // w0[co][ci][kh][kw]
+    __syncthreads();
+    const f32x4 bias = *(const f32x4*)(b0 + 4 * q);
+    f32x4* yb = (f32x4*)(y + (size_t)b * NPOS * CH) + q;
     f32x4 v[PB_ITEMS], s = zero4(), mx = zero4();
 #pragma unroll
     for (int k = 0; k < PB_ITEMS; k++) {
         const int p = h + k * PB_STRIDES;
-        v[k] = p < NPOS ? yb[(size_t)p * 32] : zero4();
+        v[k] = zero4();
+        if (p < NPOS) {
+            const int r = p / 15, c = p - (p / 15) * 15;
+            f32x4 acc = bias;
+#pragma unroll
+            for (int kk = 0; kk < C0K; kk++) {
+                const int ci = kk / 9, tap = kk % 9;
+                const float xv = xs[ci * 289 + (r + tap / 3) * 17 + c + tap % 3];
+                acc += xv * *(const f32x4*)(ws + kk * CH + 4 * q);
+            }
+            v[k] = acc;
+            yb[(size_t)p * 32] = acc;
+        }
         s += v[k];
 #pragma unroll
         for (int r = 0; r < 4; r++) mx[r] = fmaxf(mx[r], fabsf(v[k][r]));
@@ -150,7 +180,7 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_stats_kernel(const float* __re
 // fp64), BN scale/shift, the running-stat update (momentum, unbiased variance) --
 // torch BatchNorm2d in training mode.  1024 threads: channel c = tid % 128 over the
 // boards b = tid / 128 (mod 8), combined in LDS.
-constexpr int RED_THREADS = 1024, RED_PARTS = RED_THREADS / CH;
+constexpr int RED_THREADS = 1024, RED_PARTS = RED_THREADS / CH, RED_THREADS_H = 512;
 __device__ __forceinline__ double red_sum(double v, double* sh, int c, int h) {
     __syncthreads();
     sh[h * CH + c] = v;
@@ -244,73 +274,197 @@ __global__ __launch_bounds__(RED_THREADS) void sgd_bn_bwd_reduce_kernel(const fl
     if (dbias) dbias[c] = (float)(-k * mgx * (double)coef[CO_SUMXH + c]);
 }
 
-// g = dL/da * [a > 0] (the tower output's ReLU) and its BN-backward partials
-__global__ __launch_bounds__(PB_THREADS) void sgd_mask_stats_kernel(const float* __restrict__ da,
-                                                                   const float* __restrict__ act,
-                                                                   const float* __restrict__ y,
-                                                                   const float* __restrict__ coef,
-                                                                   float* __restrict__ g, float* __restrict__ part) {
+// The heads' 1x1 convs backward and the tower output's ReLU: dL/da2[p][c] =
+// dpin[0][p] wp[0][c] + dpin[1][p] wp[1][c] + dvin[p] wv[c]; g4 = that [a2 > 0] and
+// its BN-backward partials (sum g, sum g xhat, max |g|); the board's partial weight
+// gradients of policy_conv / value_conv (sum_p dpin[k][p] a2[p][c], sum_p dvin[p] a2[p][c]).
+__global__ __launch_bounds__(PB_THREADS) void sgd_heads_bwd_kernel(const float* __restrict__ dpin,
+                                                                  const float* __restrict__ dvin,
+                                                                  const float* __restrict__ act,
+                                                                  const float* __restrict__ y,
+                                                                  const float* __restrict__ coef,
+                                                                  const float* __restrict__ wp,
+                                                                  const float* __restrict__ wv,
+                                                                  float* __restrict__ g, float* __restrict__ part,
+                                                                  float* __restrict__ hpart) {
     __shared__ f32x4 sh[PB_THREADS];
     const int b = blockIdx.x, q = threadIdx.x & 31, h = threadIdx.x >> 5;
     const f32x4 mean = *(const f32x4*)(coef + CO_MEAN + 4 * q), inv = *(const f32x4*)(coef + CO_INV + 4 * q);
+    const f32x4 w0 = *(const f32x4*)(wp + 4 * q), w1 = *(const f32x4*)(wp + CH + 4 * q), w2 = *(const f32x4*)(wv + 4 * q);
     const size_t base = (size_t)b * NPOS * 32 + q;
-    f32x4 s = zero4(), sx = zero4(), mx = zero4();
-#pragma unroll 8
+    const float* dp = dpin + (size_t)b * 2 * NPOS;
+    const float* dv = dvin + (size_t)b * NPOS;
+    f32x4 s = zero4(), sx = zero4(), mx = zero4(), h0 = zero4(), h1 = zero4(), h2 = zero4();
+#pragma unroll 4
     for (int p = h; p < NPOS; p += PB_STRIDES) {
         const size_t o = base + (size_t)p * 32;
-        const f32x4 d = ((const f32x4*)da)[o], a = ((const f32x4*)act)[o], yv = ((const f32x4*)y)[o];
+        const float d0 = dp[p], d1 = dp[NPOS + p], d2 = dv[p];
+        const f32x4 a = ((const f32x4*)act)[o], yv = ((const f32x4*)y)[o];
+        const f32x4 da = d0 * w0 + d1 * w1 + d2 * w2;
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            v[r] = a[r] > 0.f ? d[r] : 0.f;
+            v[r] = a[r] > 0.f ? da[r] : 0.f;
             mx[r] = fmaxf(mx[r], fabsf(v[r]));
         }
         ((f32x4*)g)[o] = v;
         s += v;
         sx += v * ((yv - mean) * inv);
+        h0 += d0 * a;
+        h1 += d1 * a;
+        h2 += d2 * a;
     }
     s = pb_reduce(s, sh, q, h, false);
     sx = pb_reduce(sx, sh, q, h, false);
     mx = pb_reduce(mx, sh, q, h, true);
+    h0 = pb_reduce(h0, sh, q, h, false);
+    h1 = pb_reduce(h1, sh, q, h, false);
+    h2 = pb_reduce(h2, sh, q, h, false);
     if (h == 0) {
         float* o = part + (size_t)b * PART + 4 * q;
         *(f32x4*)o = s;
         *(f32x4*)(o + CH) = sx;
         *(f32x4*)(o + 2 * CH) = mx;
+        float* oh = hpart + (size_t)b * 3 * CH + 4 * q;
+        *(f32x4*)oh = h0;
+        *(f32x4*)(oh + CH) = h1;
+        *(f32x4*)(oh + 2 * CH) = h2;
     }
 }
 
-// dL/dy0 = k (g - mg - xhat mgx) (BN0's input gradient, handed back to torch's conv0)
-__global__ void sgd_bn_dy_kernel(const float* __restrict__ g, const float* __restrict__ y,
-                                 const float* __restrict__ coef, float* __restrict__ dy, long long n4) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n4) return;
-    const int c0 = (int)((i * 4) & 127);
-    const f32x4 gv = ((const f32x4*)g)[i], yv = ((const f32x4*)y)[i];
-    f32x4 o;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int c = c0 + r;
-        const float xh = (yv[r] - coef[CO_MEAN + c]) * coef[CO_INV + c];
-        o[r] = coef[CO_K + c] * (gv[r] - coef[CO_MG + c] - xh * coef[CO_MGX + c]);
+// the heads' weight and bias gradients: sums of the boards' partials (weights) and of
+// dpin / dvin (biases)
+__global__ __launch_bounds__(RED_THREADS_H) void sgd_heads_reduce_kernel(const float* __restrict__ hpart,
+                                                                        const float* __restrict__ dpin,
+                                                                        const float* __restrict__ dvin, int B,
+                                                                        float* __restrict__ dwp, float* __restrict__ dbp,
+                                                                        float* __restrict__ dwv, float* __restrict__ dbv) {
+    __shared__ float sh[3][RED_THREADS_H];
+    const int t = threadIdx.x;
+    if (t < 3 * CH) {
+        float a = 0.f;
+        for (int b = 0; b < B; b++) a += hpart[(size_t)b * 3 * CH + t];
+        if (t < 2 * CH) dwp[t] = a; else dwv[t - 2 * CH] = a;
     }
-    ((f32x4*)dy)[i] = o;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int i = t; i < B * NPOS; i += RED_THREADS_H) {
+        const int b = i / NPOS, p = i - b * NPOS;
+        s0 += dpin[(size_t)b * 2 * NPOS + p];
+        s1 += dpin[(size_t)b * 2 * NPOS + NPOS + p];
+        s2 += dvin[i];
+    }
+    sh[0][t] = s0;
+    sh[1][t] = s1;
+    sh[2][t] = s2;
+    __syncthreads();
+    for (int w = RED_THREADS_H / 2; w > 0; w >>= 1) {
+        if (t < w)
+            for (int k = 0; k < 3; k++) sh[k][t] += sh[k][t + w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        dbp[0] = sh[0][0];
+        dbp[1] = sh[1][0];
+        dbv[0] = sh[2][0];
+    }
 }
 
-// the tower output a = relu(y s + t + skip)
-__global__ void sgd_act_kernel(const float* __restrict__ y, const float* __restrict__ coef,
-                               const float* __restrict__ skip, float* __restrict__ out, long long n4) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n4) return;
-    const int c0 = (int)((i * 4) & 127);
-    const f32x4 yv = ((const f32x4*)y)[i], sv = ((const f32x4*)skip)[i];
-    f32x4 o;
+// conv0's weight / bias gradient partials of a board: dy0 = k (g0 - mg - xhat mgx)
+// (BN0's input gradient, never stored) times the board's planes at each tap:
+// wpart0[b][co][ci*9 + tap], [27] = sum_p dy0[p][co]
+__global__ __launch_bounds__(PB_THREADS) void sgd_conv0_wgrad_kernel(const float* __restrict__ g,
+                                                                    const float* __restrict__ y,
+                                                                    const float* __restrict__ coef,
+                                                                    const float* __restrict__ x,
+                                                                    float* __restrict__ wpart) {
+    __shared__ f32x4 sh[PB_THREADS];
+    __shared__ float xs[3 * 17 * 17];
+    const int b = blockIdx.x, tid = threadIdx.x, q = tid & 31, h = tid >> 5;
+    c0_stage(x, b, xs, tid);
+    __syncthreads();
+    const f32x4 mean = *(const f32x4*)(coef + CO_MEAN + 4 * q), inv = *(const f32x4*)(coef + CO_INV + 4 * q);
+    const f32x4 k = *(const f32x4*)(coef + CO_K + 4 * q), mg = *(const f32x4*)(coef + CO_MG + 4 * q);
+    const f32x4 mgx = *(const f32x4*)(coef + CO_MGX + 4 * q);
+    const size_t base = (size_t)b * NPOS * 32 + q;
+    f32x4 acc[C0K + 1];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const float v = yv[r] * coef[CO_S + c0 + r] + coef[CO_T + c0 + r] + sv[r];
-        o[r] = v > 0.f ? v : 0.f;
+    for (int kk = 0; kk <= C0K; kk++) acc[kk] = zero4();
+    for (int p = h; p < NPOS; p += PB_STRIDES) {
+        const size_t o = base + (size_t)p * 32;
+        const f32x4 gv = ((const f32x4*)g)[o], yv = ((const f32x4*)y)[o];
+        const f32x4 dy = k * (gv - mg - (yv - mean) * inv * mgx);
+        const int r = p / 15, c = p - (p / 15) * 15;
+#pragma unroll
+        for (int kk = 0; kk < C0K; kk++) {
+            const int ci = kk / 9, tap = kk % 9;
+            acc[kk] += xs[ci * 289 + (r + tap / 3) * 17 + c + tap % 3] * dy;
+        }
+        acc[C0K] += dy;
     }
-    ((f32x4*)out)[i] = o;
+    float* o = wpart + (size_t)b * CH * (C0K + 1);
+#pragma unroll
+    for (int kk = 0; kk <= C0K; kk++) {
+        const f32x4 t = pb_reduce(acc[kk], sh, q, h, false);
+        if (h == 0)
+#pragma unroll
+            for (int r = 0; r < 4; r++) o[(4 * q + r) * (C0K + 1) + kk] = t[r];
+    }
+}
+
+// conv0's weight ([128][3][3][3]) and bias gradients: sums of the boards' partials
+__global__ void sgd_conv0_reduce_kernel(const float* __restrict__ wpart, int B, float* __restrict__ dw,
+                                        float* __restrict__ db) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // co * 28 + kk
+    if (e >= CH * (C0K + 1)) return;
+    float a = 0.f;
+#pragma unroll 4
+    for (int b = 0; b < B; b++) a += wpart[(size_t)b * CH * (C0K + 1) + e];
+    const int co = e / (C0K + 1), kk = e - co * (C0K + 1);
+    if (kk < C0K) dw[co * C0K + kk] = a; else db[co] = a;
+}
+
+// the tower output a2 = relu(y4 s + t + a1) (saved) and the heads' 1x1 convs on it:
+// pin[b][k*225 + p] = bp[k] + sum_c a2[p][c] wp[k][c] (policy_conv, 2 channels, in
+// torch's flatten order), vin[b][p] = bv + sum_c a2[p][c] wv[c] (value_conv); one row
+// (board position) per thread
+__global__ __launch_bounds__(256) void sgd_out_heads_kernel(const float* __restrict__ y,
+                                                           const float* __restrict__ coef,
+                                                           const float* __restrict__ skip,
+                                                           const float* __restrict__ wp,
+                                                           const float* __restrict__ bp,
+                                                           const float* __restrict__ wv,
+                                                           const float* __restrict__ bv, float* __restrict__ out,
+                                                           float* __restrict__ pin, float* __restrict__ vin, int rows) {
+    __shared__ __attribute__((aligned(16))) float cs[5 * CH];  // s, t, wp0, wp1, wv
+    for (int i = threadIdx.x; i < CH; i += 256) {
+        cs[i] = coef[CO_S + i];
+        cs[CH + i] = coef[CO_T + i];
+        cs[2 * CH + i] = wp[i];
+        cs[3 * CH + i] = wp[CH + i];
+        cs[4 * CH + i] = wv[i];
+    }
+    __syncthreads();
+    const int row = blockIdx.x * 256 + threadIdx.x;
+    if (row >= rows) return;
+    const f32x4* yr = (const f32x4*)(y + (size_t)row * CH);
+    const f32x4* sr = (const f32x4*)(skip + (size_t)row * CH);
+    f32x4* orow = (f32x4*)(out + (size_t)row * CH);
+    f32x4 d0 = zero4(), d1 = zero4(), d2 = zero4();
+#pragma unroll 8
+    for (int c4 = 0; c4 < 32; c4++) {
+        const f32x4 sv = *(const f32x4*)(cs + 4 * c4), tv = *(const f32x4*)(cs + CH + 4 * c4);
+        f32x4 a = yr[c4] * sv + tv + sr[c4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) a[r] = a[r] > 0.f ? a[r] : 0.f;
+        orow[c4] = a;
+        d0 += a * *(const f32x4*)(cs + 2 * CH + 4 * c4);
+        d1 += a * *(const f32x4*)(cs + 3 * CH + 4 * c4);
+        d2 += a * *(const f32x4*)(cs + 4 * CH + 4 * c4);
+    }
+    const int b = row / NPOS, p = row - b * NPOS;
+    pin[(size_t)b * 2 * NPOS + p] = bp[0] + (d0[0] + d0[1] + d0[2] + d0[3]);
+    pin[(size_t)b * 2 * NPOS + NPOS + p] = bp[1] + (d1[0] + d1[1] + d1[2] + d1[3]);
+    vin[row] = bv[0] + (d2[0] + d2[1] + d2[2] + d2[3]);
 }
 
 // ---------------------------------------------------------------- f16x3 convolutions
@@ -735,8 +889,9 @@ __global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, floa
 // ---------------------------------------------------------------- host side
 struct Ws {
     _Float16* frag;
-    float* y[NBN];    // y[0] is the caller's
+    float* y[NBN];    // y0 (conv0's output), y1..y4
     float* act[4];    // a0, h1, a1, h2 (inputs of conv 1..4)
+    float* out;       // a2, the tower output (the heads' input)
     float* g[NBN];    // dL/d(BN output) of BN 0..4
     float* dy;        // dL/dy of the current conv (weight gradient operand)
     float* coef;      // [NBN][CO_FLOATS]
@@ -746,6 +901,8 @@ struct Ws {
     float* fpart;     // [NBN][B][PART]
     float* bpart;     // [NBN][B][PART]
     float* wpart;     // [9][NG][CH][CH]
+    float* hpart;     // [B][3][CH] heads' weight-gradient partials
+    float* c0part;    // [B][CH][28] conv0's weight / bias gradient partials
     int NG, G;
 };
 
@@ -760,9 +917,9 @@ size_t ws_layout(int B, Ws* w, char* base) {
     };
     Ws t;
     t.frag = (_Float16*)take((size_t)LAYERS * 2 * 2 * FRAG_HALVES * sizeof(_Float16));
-    t.y[0] = nullptr;
-    for (int i = 1; i < NBN; i++) t.y[i] = (float*)take(R);
+    for (int i = 0; i < NBN; i++) t.y[i] = (float*)take(R);
     for (int i = 0; i < 4; i++) t.act[i] = (float*)take(R);
+    t.out = (float*)take(R);
     for (int i = 0; i < NBN; i++) t.g[i] = (float*)take(R);
     t.dy = (float*)take(R);
     t.coef = (float*)take((size_t)NBN * CO_FLOATS * sizeof(float));
@@ -772,6 +929,8 @@ size_t ws_layout(int B, Ws* w, char* base) {
     t.fpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.bpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.wpart = (float*)take((size_t)9 * NG * CH * CH * sizeof(float));
+    t.hpart = (float*)take((size_t)B * 3 * CH * sizeof(float));
+    t.c0part = (float*)take((size_t)B * CH * (C0K + 1) * sizeof(float));
     t.NG = NG;
     t.G = G;
     if (w) *w = t;
@@ -795,6 +954,9 @@ int check_net(const gz_sgd_net* net, int B, const void* ws) {
         if (!net->bn_weight[i] || !net->bn_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd: BatchNorm parameters are NULL");
     for (int i = 0; i < LAYERS; i++)
         if (!net->conv_weight[i] || !net->conv_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd: conv parameters are NULL");
+    if (!net->conv0_weight || !net->conv0_bias || !net->policy_weight || !net->policy_bias || !net->value_weight ||
+        !net->value_bias)
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd: conv0 / head conv parameters are NULL");
     if (!(net->eps > 0.f) || !(net->momentum >= 0.f && net->momentum <= 1.f))
         return sgd_fail(GZ_ERR_ARG, "gz_sgd: eps must be > 0 and momentum in [0, 1]");
     return GZ_OK;
@@ -803,13 +965,14 @@ int check_net(const gz_sgd_net* net, int B, const void* ws) {
 }  // namespace
 
 // a copy of what gz_sgd_forward saved (checkers): which 0..3 = the inputs of conv 1..4
-// (a0, h1, a1, h2), 4..7 = the conv outputs y1..y4; fp32 NHWC [boards][225][128]
+// (a0, h1, a1, h2), 4..7 = the conv outputs y1..y4, 8 = the tower output a2, 9 = y0
+// (conv0's output); fp32 NHWC [boards][225][128]
 extern "C" int gz_sgd_saved(const void* d_ws, int32_t B, int32_t which, float* d_out, void* stream) {
-    if (!d_ws || !d_out || B < 1 || B > GZ_SGD_MAX_BOARDS || which < 0 || which > 7)
+    if (!d_ws || !d_out || B < 1 || B > GZ_SGD_MAX_BOARDS || which < 0 || which > 9)
         return sgd_fail(GZ_ERR_ARG, "gz_sgd_saved: bad arguments");
     Ws w;
     ws_layout(B, &w, (char*)d_ws);
-    const float* src = which < 4 ? w.act[which] : w.y[which - 3];
+    const float* src = which < 4 ? w.act[which] : which < 8 ? w.y[which - 3] : which == 8 ? w.out : w.y[0];
     if (hipMemcpyAsync(d_out, src, (size_t)B * NPOS * CH * sizeof(float), hipMemcpyDeviceToDevice,
                        (hipStream_t)stream) != hipSuccess)
         return sgd_fail(GZ_ERR_HIP, "gz_sgd_saved: copy");
@@ -820,27 +983,26 @@ extern "C" size_t gz_sgd_workspace_bytes(int32_t boards) {
     return boards < 1 ? 0 : ws_layout(boards, nullptr, nullptr);
 }
 
-extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y0, float* d_out, void* d_ws,
-                              void* stream) {
+extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_x, float* d_pin, float* d_vin,
+                              void* d_ws, void* stream) {
     int rc;
     if ((rc = check_net(net, B, d_ws))) return rc;
-    if (!d_y0 || !d_out) return sgd_fail(GZ_ERR_ARG, "gz_sgd_forward: y0 / out are NULL");
+    if (!d_x || !d_pin || !d_vin) return sgd_fail(GZ_ERR_ARG, "gz_sgd_forward: x / outputs are NULL");
     hipStream_t s = (hipStream_t)stream;
     Ws w;
     ws_layout(B, &w, (char*)d_ws);
-    w.y[0] = (float*)d_y0;
-    const long long n4 = (long long)B * NPOS * CH / 4;
     PackArgs pa;
     for (int i = 0; i < LAYERS; i++) pa.w[i] = net->conv_weight[i];
     if (hipMemsetAsync(w.wsc, 0, 8 * sizeof(float), s) != hipSuccess)
         return sgd_fail(GZ_ERR_HIP, "gz_sgd_forward: memset");
     sgd_wmax_kernel<<<dim3(32, LAYERS), 256, 0, s>>>(pa, (unsigned*)w.wsc);
     sgd_pack_kernel<<<(LAYERS * 2 * FRAG_HALVES + 255) / 256, 256, 0, s>>>(pa, w.wsc, w.frag);
-    sgd_stats_kernel<<<B, PB_THREADS, 0, s>>>(d_y0, w.fpart);
+    // y0 = conv0(x) and its BN0 partials
+    sgd_conv0_kernel<<<B, PB_THREADS, 0, s>>>(d_x, net->conv0_weight, net->conv0_bias, w.y[0], w.fpart);
     sgd_bn_fwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.fpart, B, net->bn_weight[0], net->bn_bias[0],
                                                       net->bn_running_mean[0], net->bn_running_var[0], net->momentum,
                                                       net->eps, w.coef);
-    if ((rc = sgd_check("gz_sgd_forward: BN0"))) return rc;
+    if ((rc = sgd_check("gz_sgd_forward: conv0"))) return rc;
     // conv L (1..4): input = relu(BN_{L-1}(y_{L-1}) (+ skip)), skip a0 for conv 3's input a1
     for (int L = 1; L <= LAYERS; L++) {
         ConvArgs a{};
@@ -860,28 +1022,35 @@ extern "C" int gz_sgd_forward(const gz_sgd_net* net, int32_t B, const float* d_y
                                                           net->momentum, net->eps, w.coef + (size_t)L * CO_FLOATS);
         if ((rc = sgd_check("gz_sgd_forward: conv"))) return rc;
     }
-    // a2 = relu(BN4(y4) + a1)
-    sgd_act_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(w.y[4], w.coef + 4 * CO_FLOATS, w.act[2], d_out, n4);
+    // a2 = relu(BN4(y4) + a1), then the heads' 1x1 convs
+    const int rows = B * NPOS;
+    sgd_out_heads_kernel<<<(rows + 255) / 256, 256, 0, s>>>(w.y[4], w.coef + 4 * CO_FLOATS, w.act[2],
+                                                            net->policy_weight, net->policy_bias, net->value_weight,
+                                                            net->value_bias, w.out, d_pin, d_vin, rows);
     return sgd_check("gz_sgd_forward: output");
 }
 
-extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_y0, const float* d_out,
-                               const float* d_dout, float* d_dy0, const gz_sgd_grads* gr, void* d_ws, void* stream) {
+extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_x, const float* d_dpin,
+                               const float* d_dvin, const gz_sgd_grads* gr, void* d_ws, void* stream) {
     int rc;
     if ((rc = check_net(net, B, d_ws))) return rc;
-    if (!d_y0 || !d_out || !d_dout || !d_dy0 || !gr) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL argument");
+    if (!d_x || !d_dpin || !d_dvin || !gr) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL argument");
     for (int i = 0; i < NBN; i++)
         if (!gr->bn_weight[i] || !gr->bn_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL gradient");
     for (int i = 0; i < LAYERS; i++)
         if (!gr->conv_weight[i] || !gr->conv_bias[i]) return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL gradient");
+    if (!gr->conv0_weight || !gr->conv0_bias || !gr->policy_weight || !gr->policy_bias || !gr->value_weight ||
+        !gr->value_bias)
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd_backward: NULL gradient");
     hipStream_t s = (hipStream_t)stream;
     Ws w;
     ws_layout(B, &w, (char*)d_ws);
-    w.y[0] = (float*)d_y0;
-    const long long n4 = (long long)B * NPOS * CH / 4;
-    // g4 = dL/d(BN4 output) = dout [out > 0]; also the skip gradient into a1
-    sgd_mask_stats_kernel<<<B, PB_THREADS, 0, s>>>(d_dout, d_out, w.y[4], w.coef + 4 * CO_FLOATS, w.g[4],
-                                            w.bpart + (size_t)4 * B * PART);
+    // the heads' 1x1 convs backward -> g4 = dL/d(BN4 output) (also the skip gradient into a1)
+    sgd_heads_bwd_kernel<<<B, PB_THREADS, 0, s>>>(d_dpin, d_dvin, w.out, w.y[4], w.coef + 4 * CO_FLOATS,
+                                                  net->policy_weight, net->value_weight, w.g[4],
+                                                  w.bpart + (size_t)4 * B * PART, w.hpart);
+    sgd_heads_reduce_kernel<<<1, RED_THREADS_H, 0, s>>>(w.hpart, d_dpin, d_dvin, B, gr->policy_weight,
+                                                        gr->policy_bias, gr->value_weight, gr->value_bias);
     for (int L = LAYERS; L >= 1; L--) {
         float* coefL = w.coef + (size_t)L * CO_FLOATS;
         sgd_bn_bwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.bpart + (size_t)L * B * PART, B, net->bn_weight[L],
@@ -909,8 +1078,11 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
         sgd_wreduce_kernel<<<(9 * CH * CH + 255) / 256, 256, 0, s>>>(w.wpart, w.NG, gr->conv_weight[L - 1]);
         if ((rc = sgd_check("gz_sgd_backward: conv"))) return rc;
     }
+    // BN0, then conv0's weight and bias gradients (its input gradient is not needed)
     sgd_bn_bwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.bpart, B, net->bn_weight[0], w.coef, gr->bn_weight[0],
                                                       gr->bn_bias[0], nullptr);
-    sgd_bn_dy_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(w.g[0], d_y0, w.coef, d_dy0, n4);
-    return sgd_check("gz_sgd_backward: BN0");
+    sgd_conv0_wgrad_kernel<<<B, PB_THREADS, 0, s>>>(w.g[0], w.y[0], w.coef, d_x, w.c0part);
+    sgd_conv0_reduce_kernel<<<(CH * (C0K + 1) + 255) / 256, 256, 0, s>>>(w.c0part, B, gr->conv0_weight,
+                                                                         gr->conv0_bias);
+    return sgd_check("gz_sgd_backward: conv0");
 }

@@ -81,12 +81,18 @@ class SgdNet(ctypes.Structure):  # gz_sgd_net
     _fields_ = [("bn_weight", ctypes.c_void_p * 5), ("bn_bias", ctypes.c_void_p * 5),
                 ("bn_running_mean", ctypes.c_void_p * 5), ("bn_running_var", ctypes.c_void_p * 5),
                 ("conv_weight", ctypes.c_void_p * 4), ("conv_bias", ctypes.c_void_p * 4),
-                ("momentum", ctypes.c_float), ("eps", ctypes.c_float)]
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float),
+                ("conv0_weight", ctypes.c_void_p), ("conv0_bias", ctypes.c_void_p),
+                ("policy_weight", ctypes.c_void_p), ("policy_bias", ctypes.c_void_p),
+                ("value_weight", ctypes.c_void_p), ("value_bias", ctypes.c_void_p)]
 
 
 class SgdGrads(ctypes.Structure):  # gz_sgd_grads
     _fields_ = [("bn_weight", ctypes.c_void_p * 5), ("bn_bias", ctypes.c_void_p * 5),
-                ("conv_weight", ctypes.c_void_p * 4), ("conv_bias", ctypes.c_void_p * 4)]
+                ("conv_weight", ctypes.c_void_p * 4), ("conv_bias", ctypes.c_void_p * 4),
+                ("conv0_weight", ctypes.c_void_p), ("conv0_bias", ctypes.c_void_p),
+                ("policy_weight", ctypes.c_void_p), ("policy_bias", ctypes.c_void_p),
+                ("value_weight", ctypes.c_void_p), ("value_bias", ctypes.c_void_p)]
 
 
 GZ_SGD_MAX_BOARDS = 65535
@@ -137,9 +143,8 @@ SIGNATURES = {
     "gz_dataset_build": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P]),
     "gz_dataset_gather": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _I64, _I32, _P, _P, _P, _P]),
     "gz_sgd_workspace_bytes": (_SZ, [_I32]),
-    "gz_sgd_forward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P]),
-    "gz_sgd_backward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P, ctypes.POINTER(SgdGrads), _P,
-                                       _P]),
+    "gz_sgd_forward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P, _P]),
+    "gz_sgd_backward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, ctypes.POINTER(SgdGrads), _P, _P]),
     "gz_sgd_saved": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
 }
 

@@ -1,15 +1,16 @@
-"""Training-mode forward/backward of the policy-value net's residual tower on the
-device (csrc/gz_sgd.hip, include/gzero.h gz_sgd_*), as a torch autograd Function.
+"""Training-mode forward/backward of the policy-value net's convolutional part on
+the device (csrc/gz_sgd.hip, include/gzero.h gz_sgd_*), as a torch autograd Function.
 
 ``train_forward(net, x)`` is ``PolicyValueNet.forward`` (neural_network.py:132-159)
-in training mode with the tower -- BN0 + ReLU and the two residual blocks
-(neural_network.py:74-91), BatchNorm on batch statistics -- replaced by the HIP
-kernels: f16x3 MFMA implicit-GEMM convolutions (forward and input gradient), fp32
-MFMA weight gradients, BatchNorm statistics and backward in the conv epilogues.
-conv0 (3 -> 128 channels) and the policy / value heads stay torch ops; the loss,
-``clip_grad_norm_`` and Adam of ``training.train_epoch`` (training.py:277-311) are
-unchanged.  The BatchNorm running statistics and ``num_batches_tracked`` are
-updated as ``nn.BatchNorm2d.train()`` does.  There is no fallback: without the
+in training mode with everything up to the heads' flattened conv outputs -- conv0,
+BN0 + ReLU, the two residual blocks (neural_network.py:74-91), BatchNorm on batch
+statistics, and the 1x1 policy / value convs -- on the HIP kernels: f16x3 MFMA
+implicit-GEMM convolutions (forward, input and weight gradients), BatchNorm
+statistics and backward in the conv epilogues, conv0 and the 1x1 convs in fp32.
+The FC heads (policy_fc, value_fc1/2) stay torch ops; the loss, ``clip_grad_norm_``
+and Adam of ``training.train_epoch`` (training.py:277-311) are unchanged.  The
+BatchNorm running statistics and ``num_batches_tracked`` are updated as
+``nn.BatchNorm2d.train()`` does.  There is no fallback: without the
 library this raises ``GzeroUnavailable``.
 """
 import ctypes
@@ -37,14 +38,19 @@ def _convs(net):
 
 
 def tower_params(net):
-    """The tower's parameters in the Function's order: (gamma, beta) of BN 0..4, then
-    (weight, bias) of conv 1..4 (gz_sgd_net's order)."""
+    """The parameters in the Function's order: (gamma, beta) of BN 0..4, (weight, bias)
+    of conv 1..4 (gz_sgd_net's arrays), then conv0, policy_conv, value_conv."""
     out = []
     for bn in _bns(net):
         out += [bn.weight, bn.bias]
     for cv in _convs(net):
         out += [cv.weight, cv.bias]
+    for cv in (net.conv, net.policy_conv, net.value_conv):
+        out += [cv.weight, cv.bias]
     return out
+
+
+_HEADS = ("conv0", "policy", "value")
 
 
 def _check_net(net):
@@ -56,18 +62,22 @@ def _check_net(net):
     for cv in _convs(net):
         if tuple(cv.weight.shape) != (128, 128, 3, 3) or cv.bias is None:
             raise ValueError("gz_sgd: residual convs must be 128 -> 128, 3x3, with bias")
+    if (tuple(net.conv.weight.shape) != (128, 3, 3, 3) or tuple(net.policy_conv.weight.shape) != (2, 128, 1, 1)
+            or tuple(net.value_conv.weight.shape) != (1, 128, 1, 1)):
+        raise ValueError("gz_sgd: conv0 must be 3 -> 128 (3x3), policy_conv 128 -> 2 and value_conv 128 -> 1 (1x1)")
 
 
 class _Tower(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y0, net, *params):
+    def forward(ctx, x, net, *params):
         lib = _lib.load()
-        B = y0.shape[0]
-        if not 1 <= B <= _lib.GZ_SGD_MAX_BOARDS:
-            raise ValueError(f"gz_sgd: batch of {B} boards")
-        y0n = y0.detach().permute(0, 2, 3, 1).contiguous()
-        out = torch.empty_like(y0n)
-        ws = torch.empty(int(lib.gz_sgd_workspace_bytes(B)), dtype=torch.uint8, device=y0.device)
+        B = x.shape[0]
+        if not 1 <= B <= _lib.GZ_SGD_MAX_BOARDS or tuple(x.shape[1:]) != (3, 15, 15):
+            raise ValueError(f"gz_sgd: input of shape {tuple(x.shape)}")
+        xc = x.detach().contiguous()
+        pin = torch.empty((B, 450), dtype=torch.float32, device=x.device)
+        vin = torch.empty((B, 225), dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(lib.gz_sgd_workspace_bytes(B)), dtype=torch.uint8, device=x.device)
         st = _lib.SgdNet()
         bns = _bns(net)
         for i, bn in enumerate(bns):
@@ -78,23 +88,26 @@ class _Tower(torch.autograd.Function):
         for i in range(4):
             st.conv_weight[i] = params[10 + 2 * i].data_ptr()
             st.conv_bias[i] = params[11 + 2 * i].data_ptr()
+        for i, name in enumerate(_HEADS):
+            setattr(st, f"{name}_weight", params[18 + 2 * i].data_ptr())
+            setattr(st, f"{name}_bias", params[19 + 2 * i].data_ptr())
         st.momentum = float(bns[0].momentum)
         st.eps = float(bns[0].eps)
-        _lib.check(lib.gz_sgd_forward(ctypes.byref(st), B, _ptr(y0n), _ptr(out), _ptr(ws), _stream()),
+        _lib.check(lib.gz_sgd_forward(ctypes.byref(st), B, _ptr(xc), _ptr(pin), _ptr(vin), _ptr(ws), _stream()),
                    "gz_sgd_forward")
         for bn in bns:
             if bn.track_running_stats:
                 bn.num_batches_tracked.add_(1)
         ctx.st, ctx.B, ctx.ws = st, B, ws
-        ctx.keep = (y0n, out, params)  # the forward's pointers stay valid for the backward
-        return out.permute(0, 3, 1, 2)
+        ctx.keep = (xc, params)  # the forward's pointers stay valid for the backward
+        return pin, vin
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, dpin, dvin):
         lib = _lib.load()
-        y0n, out, params = ctx.keep
-        dout = gout.permute(0, 2, 3, 1).contiguous()
-        dy0 = torch.empty_like(y0n)
+        xc, params = ctx.keep
+        dpin = dpin.contiguous() if dpin is not None else torch.zeros((ctx.B, 450), device=xc.device)
+        dvin = dvin.contiguous() if dvin is not None else torch.zeros((ctx.B, 225), device=xc.device)
         grads = [torch.empty_like(p) for p in params]
         gr = _lib.SgdGrads()
         for i in range(5):
@@ -103,25 +116,30 @@ class _Tower(torch.autograd.Function):
         for i in range(4):
             gr.conv_weight[i] = grads[10 + 2 * i].data_ptr()
             gr.conv_bias[i] = grads[11 + 2 * i].data_ptr()
-        _lib.check(lib.gz_sgd_backward(ctypes.byref(ctx.st), ctx.B, _ptr(y0n), _ptr(out), _ptr(dout), _ptr(dy0),
+        for i, name in enumerate(_HEADS):
+            setattr(gr, f"{name}_weight", grads[18 + 2 * i].data_ptr())
+            setattr(gr, f"{name}_bias", grads[19 + 2 * i].data_ptr())
+        _lib.check(lib.gz_sgd_backward(ctypes.byref(ctx.st), ctx.B, _ptr(xc), _ptr(dpin), _ptr(dvin),
                                        ctypes.byref(gr), _ptr(ctx.ws), _stream()), "gz_sgd_backward")
         ctx.keep = ctx.ws = None
-        return (dy0.permute(0, 3, 1, 2), None, *grads)
+        return (None, None, *grads)
 
 
-def tower(net, y0):
-    """relu(BN0(y0)) through both residual blocks, training mode, on the device."""
+def tower(net, x):
+    """(policy_conv output flattened [B, 450], value_conv output flattened [B, 225]) of
+    the planes x [B, 3, 15, 15]: conv0, BN0, both residual blocks, training mode, on
+    the device."""
     _check_net(net)
     params = tower_params(net)
     for p in params:
         if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
             raise ValueError("gz_sgd: tower parameters must be contiguous float32 CUDA tensors")
-    return _Tower.apply(y0.float(), net, *params)
+    return _Tower.apply(x.float(), net, *params)
 
 
 def train_forward(net, x):
-    """(logits, value) of PolicyValueNet in training mode with the device tower."""
-    h = tower(net, net.conv(x))
-    logits = net.policy_fc(torch.flatten(net.policy_conv(h), 1))
-    v = F.relu(net.value_fc1(torch.flatten(net.value_conv(h), 1)))
+    """(logits, value) of PolicyValueNet in training mode with the device convolutions."""
+    pin, vin = tower(net, x)
+    logits = net.policy_fc(pin)
+    v = F.relu(net.value_fc1(vin))
     return logits, torch.tanh(net.value_fc2(v))

@@ -315,16 +315,19 @@ int gz_dataset_build(const gz_record* d_records, int32_t n, const int32_t* d_sel
 int gz_dataset_gather(const gz_record* d_records, int32_t n, const int32_t* d_sel, int32_t m, const int64_t* d_ids,
                       int64_t count, int32_t flags, float* d_x, int64_t* d_y, float* d_v, void* stream);
 
-/* ---- f1 training step: the residual tower of the policy-value net in training mode
- * (training.py:277-311 over neural_network.py:74-91, 132-145: BatchNorm on batch
- * statistics), forward and backward on the device (csrc/gz_sgd.hip).  The tower:
- *   a0 = relu(BN0(y0)); per block: h = relu(BN1(conv1(a) + b1)), a' = relu(BN2(conv2(h) + b2) + a)
- * y0 = conv0(x) and the heads stay with the caller (gzero/sgd.py).  Tensors are fp32
- * NHWC [boards][225][128]; conv weights are torch's [128][128][3][3].  BN order:
- * bn, tower.0.bn1, tower.0.bn2, tower.1.bn1, tower.1.bn2; convs: tower.0.conv1,
- * tower.0.conv2, tower.1.conv1, tower.1.conv2.  gz_sgd_forward updates the running
- * statistics (momentum, unbiased variance) like torch.nn.BatchNorm2d.train(); the
- * workspace (gz_sgd_workspace_bytes) carries the saved activations and statistics
+/* ---- f1 training step: the policy-value net's convolutional part in training mode
+ * (training.py:277-311 over neural_network.py:74-91, 132-159: BatchNorm on batch
+ * statistics), forward and backward on the device (csrc/gz_sgd.hip):
+ *   a0 = relu(BN0(conv0(x))); per block: h = relu(BN1(conv1(a) + b1)), a' = relu(BN2(conv2(h) + b2) + a);
+ *   pin = policy_conv(a2) (flattened [boards][2 * 225]), vin = value_conv(a2) ([boards][225])
+ * The FC heads (policy_fc, value_fc1/2), the loss and the optimiser stay with the caller
+ * (gzero/sgd.py).  x = the model input planes float32 [boards][3][15][15]; activations
+ * are fp32 NHWC [boards][225][128] in the workspace.  Weights in torch's layouts:
+ * conv0 [128][3][3][3]; residual convs [128][128][3][3] (tower.0.conv1, tower.0.conv2,
+ * tower.1.conv1, tower.1.conv2); policy_conv [2][128]; value_conv [1][128].  BN order:
+ * bn, tower.0.bn1, tower.0.bn2, tower.1.bn1, tower.1.bn2.  gz_sgd_forward updates the
+ * running statistics (momentum, unbiased variance) like torch.nn.BatchNorm2d.train();
+ * the workspace (gz_sgd_workspace_bytes) carries the saved activations and statistics
  * from gz_sgd_forward to the gz_sgd_backward of the same batch. */
 #define GZ_SGD_MAX_BOARDS 65535
 typedef struct gz_sgd_net {
@@ -335,24 +338,36 @@ typedef struct gz_sgd_net {
     const float* conv_weight[4];
     const float* conv_bias[4];
     float momentum, eps;
+    const float* conv0_weight;
+    const float* conv0_bias;
+    const float* policy_weight;
+    const float* policy_bias;
+    const float* value_weight;
+    const float* value_bias;
 } gz_sgd_net;
 typedef struct gz_sgd_grads { /* outputs (overwritten, not accumulated) */
     float* bn_weight[5];
     float* bn_bias[5];
     float* conv_weight[4];
     float* conv_bias[4];
+    float* conv0_weight;
+    float* conv0_bias;
+    float* policy_weight;
+    float* policy_bias;
+    float* value_weight;
+    float* value_bias;
 } gz_sgd_grads;
 size_t gz_sgd_workspace_bytes(int32_t boards);
-/* d_out = the tower output (fp32 NHWC) of the boards' conv0 outputs d_y0 */
-int gz_sgd_forward(const gz_sgd_net* net, int32_t boards, const float* d_y0, float* d_out, void* d_workspace,
-                   void* stream);
-/* from dL/d(out): dL/dy0 (NHWC) and every tower parameter's gradient; d_y0 and d_out
- * are the forward's, the workspace the one that forward used */
-int gz_sgd_backward(const gz_sgd_net* net, int32_t boards, const float* d_y0, const float* d_out,
-                    const float* d_dout, float* d_dy0, const gz_sgd_grads* grads, void* d_workspace, void* stream);
+/* d_pin [boards][450], d_vin [boards][225]: the heads' conv outputs of planes d_x */
+int gz_sgd_forward(const gz_sgd_net* net, int32_t boards, const float* d_x, float* d_pin, float* d_vin,
+                   void* d_workspace, void* stream);
+/* from dL/dpin, dL/dvin: every parameter's gradient (d_x and the workspace are the
+ * forward's) */
+int gz_sgd_backward(const gz_sgd_net* net, int32_t boards, const float* d_x, const float* d_dpin,
+                    const float* d_dvin, const gz_sgd_grads* grads, void* d_workspace, void* stream);
 /* checkers: a copy of a saved tensor of the last gz_sgd_forward on this workspace:
  * which 0..3 = the inputs of the four residual convs (a0, h1, a1, h2), 4..7 = their
- * outputs y1..y4 (fp32 NHWC) */
+ * outputs y1..y4, 8 = the tower output a2, 9 = y0 = conv0's output (fp32 NHWC) */
 int gz_sgd_saved(const void* d_workspace, int32_t boards, int32_t which, float* d_out, void* stream);
 
 #ifdef __cplusplus

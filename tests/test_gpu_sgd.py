@@ -1,4 +1,5 @@
-"""The training step's device tower (csrc/gz_sgd.hip via gzero.sgd.train_forward)
+"""The training step's device convolutions (csrc/gz_sgd.hip via gzero.sgd.train_forward:
+conv0, the residual tower and the heads' 1x1 convs)
 against torch autograd of the same PolicyValueNet in float64 on the CPU (the
 reference's training.py:277-311 step: forward in train mode, CE + MSE loss,
 backward), on identical weights and boards.
@@ -61,16 +62,15 @@ def _saved_masks(store):
     from gzero import _lib, sgd
     orig = sgd._Tower.forward
 
-    def fwd(ctx, y0, net, *params):
-        out = orig(ctx, y0, net, *params)
+    def fwd(ctx, x, net, *params):
+        out = orig(ctx, x, net, *params)
         L = _lib.load()
         acts = []
-        for i in range(4):
-            t = torch.empty_like(ctx.keep[0])
+        for i in (0, 1, 2, 3, 8):  # a0, h1, a1, h2 and the tower output a2
+            t = torch.empty((ctx.B, 15, 15, 128), dtype=torch.float32, device="cuda")
             _lib.check(L.gz_sgd_saved(ctypes.c_void_p(ctx.ws.data_ptr()), ctx.B, i, ctypes.c_void_p(t.data_ptr()),
                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "gz_sgd_saved")
             acts.append(t)
-        acts.append(ctx.keep[1])
         store["masks"] = [(a > 0).permute(0, 3, 1, 2).double().cpu() for a in acts]
         return out
     return orig, fwd
