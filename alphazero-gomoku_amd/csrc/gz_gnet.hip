@@ -526,7 +526,11 @@ constexpr int IG = 3;  // boards per chunk
 constexpr int IMH = IG == 1 ? 1 : 2;      // M parts: waves = 4 n-tiles x IMH
 constexpr int NTI = 256 * IMH;            // wave: n-tile wave & 3, M part wave >> 2
 constexpr int IWG = IG == 1 ? 2 : 1;      // workgroups per CU
-constexpr int IWIN_MAX = 169 * 256;       // bytes of a radius-6 window (2 planes x 8 cg x 169 x 16 B)
+// a window of radius R: (2R+1)^2 positions, each channel-group plane padded to a multiple
+// of 16 positions, so that the plane stride is a whole number of 256-B bank rows (the
+// ds_read_b128 of a tile row then lands on the same bank slot in every plane)
+__host__ __device__ constexpr int ig_pw(int R) { return ((2 * R + 1) * (2 * R + 1) + 15) / 16 * 16; }
+constexpr int IWIN_MAX = ig_pw(6) * 256;  // bytes of a radius-6 window (2 planes x 8 cg x 176 x 16 B)
 // LDS: the windows at 0 (up to IG x 43 KB), each 3x3 layer's output rows at the top of
 // [0, IA) (B(ro): [plane][8 cg][ig_brows(ro)][8] halves at IA - 256 ig_brows(ro)), so
 // that the next window's fill can start as soon as the 3x3 k-loop has read its window
@@ -537,13 +541,14 @@ constexpr int ICOL = IA;                  // embed im2col [IG][4][16][8] halves
 constexpr int IPC = ICOL + IG * 1024;     // policy-conv outputs [IG][2][128] floats
 constexpr int IU = IPC + IG * 2 * 128 * 4;
 constexpr int ITAB = IU + IG * 128;         // row tables of the radius 1..5 passes, then their totals
-__host__ __device__ constexpr int itab_off(int ro) { return ro <= 1 ? 0 : itab_off(ro - 1) + IG * (2 * ro - 1) * (2 * ro - 1); }
-constexpr int ITOT = itab_off(6);            // 855 entries
+// (radius 1 has no table: the embed works on its squares directly)
+__host__ __device__ constexpr int itab_off(int ro) { return ro <= 2 ? 0 : itab_off(ro - 1) + ig_brows(ro - 1); }
+constexpr int ITOT = itab_off(6);            // 864 entries (radius 2..5 rows, padded to whole tiles)
 constexpr int ILDS = ITAB + (ITOT + 8 + 5 * IG * 8) * 4;
 static_assert(ILDS * IWG <= 160 * 1024 && IG * IWIN_MAX <= IA && ig_boff(5) >= 0, "LDS");
 // the next window vs the rows the 1x1 layer before it reads: map 1, 2 windows clear
 // of B(2), B(3); the map-3 window overlaps B(4) above ig_boff(4) (filled in two parts)
-static_assert(IG * 81 * 256 <= ig_boff(2) && IG * 121 * 256 <= ig_boff(3), "window / rows overlap");
+static_assert(IG * ig_pw(4) * 256 <= ig_boff(2) && IG * ig_pw(5) * 256 <= ig_boff(3), "window / rows overlap");
 
 struct GnUnit {
     const _Float16* base;  // maps the chain adds stones to
@@ -589,7 +594,7 @@ __device__ __forceinline__ const _Float16* ig_rfl(const _Float16* p) {
 // the board; drained by the caller's barrier
 template <int MAP>
 __device__ __forceinline__ void ig_fill(char* lds, const GnUnit* U, int ng, int tid, int lo = 0, int hi = 1 << 30) {
-    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, NB = (P + 63) / 64, rc = MAP + 1;
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, PW = Wd * Wd, P = ig_pw(R), NB = (PW + 63) / 64, rc = MAP + 1;
     // work blocks (unit g, 64 window positions): the lane's position and its source
     // are worked out once, then its 16 channel-group planes go by LDS-DMA (for a given
     // plane a wave's 64 positions are contiguous in LDS)
@@ -604,7 +609,7 @@ __device__ __forceinline__ void ig_fill(char* lds, const GnUnit* U, int ng, int 
         const int pr = cr + dr, pc = cc + dc;
         const bool on = pr >= 0 && pr < 15 && pc >= 0 && pc < 15;
         // positions past the window, and the new square (its epilogue writes it): no load
-        const bool skip = loc >= P || (on && iabs_(dr) <= rc && iabs_(dc) <= rc);
+        const bool skip = loc >= PW || (on && iabs_(dr) <= rc && iabs_(dc) <= rc);
         const char* src = (const char*)gz_gn_zero16;
         int step = 0;  // bytes between planes at the source
         if (on) {
@@ -639,22 +644,36 @@ __device__ __forceinline__ void ig_bar() {
 struct IgRow {
     int g, pr, pc, j;
 };
+constexpr int IG_PAD = 1 << 30;  // a table entry that pads a tile (a real row's geometry, no output)
 __device__ __forceinline__ IgRow ig_row(const char* lds, int ro, int i) {
     const int v = ((const int*)(lds + ITAB))[itab_off(ro) + i];
     IgRow r;
     r.g = v & 3;
     r.pr = (v >> 2) & 15;
     r.pc = (v >> 6) & 15;
-    r.j = v >> 10;
+    r.j = (v >> 10) & 1023;
     return r;
+}
+__device__ __forceinline__ bool ig_valid(const char* lds, int ro, int i) {
+    return !(((const int*)(lds + ITAB))[itab_off(ro) + i] & IG_PAD);
 }
 __device__ __forceinline__ int ig_total(const char* lds, int ro) { return ((const int*)(lds + ITAB))[ITOT + ro]; }
 
-// the row tables of a chunk (every radius), built once by the whole workgroup:
-// entry i of radius ro = unit | pr << 2 | pc << 6 | (index in its square) << 10
+// The row tables of a chunk (radius 2..5), built once by the whole workgroup: entry i
+// of radius ro = unit | pr << 2 | pc << 6 | (index in its square) << 10, N rows in
+// T = ceil(N / 16) tiles.  A 3x3 layer's tile reads, per lane, 16 B of a window plane at
+// its row's window position p, so a tile whose 16 rows share p mod 16 serialises its
+// ds_read_b128 (one bank slot per 16-B position).  The rows of radius >= 2 are therefore
+// ordered by that slot (a counting sort, p in the window of radius ro + 1 the layer
+// reads) and dealt to the tiles round-robin -- sorted row k -> tile k mod T, lane k / T
+// -- so each tile takes an even share of every slot.  The lanes past N in the deal are
+// padding entries (IG_PAD) that hold row 0's geometry.  Which lane computes a row does
+// not change its result (an MFMA output element depends on its own row only).
 __device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng, int tid) {
     int* tab = (int*)(lds + ITAB);
-    int* sqt = tab + ITOT + 8;  // [radius - 1][unit]: r0, c0, h, w, first packed row
+    int* sqt = tab + ITOT + 8;  // [radius - 1][unit]: r0, c0, h, w, first natural row
+    int* rk = (int*)lds;        // scratch in the (not yet filled) window area: rank in its slot
+    int* hist = rk + 5 * IG * 121;  // [radius - 1][16] slot counts, then [radius - 1][16] starts
     if (tid < 5) {
         const int ro = tid + 1;
         int start = 0;
@@ -666,16 +685,52 @@ __device__ __forceinline__ void ig_build_rows(char* lds, const GnUnit* U, int ng
         }
         tab[ITOT + ro] = start;
     }
+    if (tid < 5 * 16) hist[tid] = 0;
     __syncthreads();
-    for (int e = tid; e < 5 * IG * 121; e += NTI) {
-        const int ro = 1 + e / (IG * 121), r = e - (ro - 1) * IG * 121, g = r / 121, j = r - g * 121;
-        if (g >= ng) continue;
+    // every entry of the padded tables: padding with row 0's geometry
+#pragma unroll
+    for (int ro = 2; ro <= 5; ro++) {
+        const int* q = sqt + (ro - 1) * IG * 8;
+        for (int e = tid; e < ig_brows(ro); e += NTI) tab[itab_off(ro) + e] = IG_PAD | q[0] << 2 | q[1] << 6;
+    }
+    auto row_of = [&](int e, int& ro, int& nat, int& v, int& slot) -> bool {
+        ro = 1 + e / (IG * 121);
+        const int r = e - (ro - 1) * IG * 121, g = r / 121, j = r - g * 121;
+        if (g >= ng) return false;
         const int* q = sqt + ((ro - 1) * IG + g) * 8;
         const int w = q[3];
-        if (j >= q[2] * w) continue;
+        if (j >= q[2] * w) return false;
         const int rr = (int)(((float)j + 0.5f) / (float)w);  // exact: j < 121, w <= 11
-        tab[itab_off(ro) + q[4] + j] = g | (q[0] + rr) << 2 | (q[1] + j - rr * w) << 6 | j << 10;
+        const int pr = q[0] + rr, pc = q[1] + j - rr * w;
+        nat = q[4] + j;
+        v = g | pr << 2 | pc << 6 | j << 10;
+        const int cell = U[g].cell, cr = cell / 15, cc = cell - cr * 15, R = ro + 1, Wd = 2 * R + 1;
+        slot = ((pr - cr + R) * Wd + (pc - cc + R)) & 15;
+        return true;
+    };
+    for (int e = tid; e < 5 * IG * 121; e += NTI) {
+        int ro, nat, v, slot;
+        if (!row_of(e, ro, nat, v, slot) || ro == 1) continue;
+        rk[(ro - 1) * IG * 121 + nat] = atomicAdd(&hist[(ro - 1) * 16 + slot], 1);
     }
+    __syncthreads();
+    if (tid < 5) {
+        int a = 0;
+        for (int sl = 0; sl < 16; sl++) {
+            const int c = hist[tid * 16 + sl];
+            hist[80 + tid * 16 + sl] = a;
+            a += c;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 5 * IG * 121; e += NTI) {
+        int ro, nat, v, slot;
+        if (!row_of(e, ro, nat, v, slot) || ro == 1) continue;
+        const int k = hist[80 + (ro - 1) * 16 + slot] + rk[(ro - 1) * IG * 121 + nat];
+        const int T = (tab[ITOT + ro] + 15) >> 4;
+        tab[itab_off(ro) + (k % T) * 16 + k / T] = v;
+    }
+    __syncthreads();  // the scratch (window area) is free for the first fill
 }
 
 // tiles per group of the 3x3 k-loop: a group's 3 products interleave over its tiles, so
@@ -698,7 +753,7 @@ __device__ __forceinline__ void ig_sfor(F&& f, std::integer_sequence<int, I...>)
 template <int NT, int NMAX, int R>
 __device__ __forceinline__ void ig_conv3_nt(const _Float16* act, const int (&ctr)[NMAX], const _Float16* __restrict__ Wf,
                                             int nt, int lane, f32x4 (&acc)[NMAX]) {
-    constexpr int Wd = 2 * R + 1, P = Wd * Wd, KS = 18, LO = 64 * P, GT = IG_GT < NT ? IG_GT : NT, NG = (NT + GT - 1) / GT;
+    constexpr int Wd = 2 * R + 1, P = ig_pw(R), KS = 18, LO = 64 * P, GT = IG_GT < NT ? IG_GT : NT, NG = (NT + GT - 1) / GT;
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt * 64 + lane) * 16;
@@ -838,14 +893,14 @@ __device__ __forceinline__ Ig1x1W ig_w1x1(const float* __restrict__ W, int layer
 template <int MAP, int NMAX, class Pre>
 __device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, const float* __restrict__ W, int layer,
                                           int nt, int mh, int lane, Ig1x1W& next, Pre&& pre) {
-    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 2;
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = ig_pw(R), ro = MAP + 2;
     static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
     const IgTiles t = ig_tiles(lds, ro, mh, lane);
     int ctr[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
         const int i = t.i0 + 16 * m;
-        const IgRow r = ig_row(lds, ro, i < t.total ? i : 0);
+        const IgRow r = ig_row(lds, ro, i < 16 * ((t.total + 15) >> 4) ? i : 0);  // (padding: row 0's geometry)
         const int cell = U[r.g].cell, cr = cell / 15, cc = cell - (cell / 15) * 15;
         ctr[m] = r.g * 16 * P + (r.pr - cr + R) * Wd + (r.pc - cc + R);
     }
@@ -891,7 +946,7 @@ __device__ __forceinline__ void ig_layer3(char* lds, const GnUnit* U, int ng, co
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
         const int i = t.i0 + 16 * m;
-        if (m >= t.nt || i >= t.total) continue;
+        if (m >= t.nt || !ig_valid(lds, ro, i)) continue;
         h4 hi, lo;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -961,7 +1016,7 @@ __device__ __forceinline__ void ig_split(const f32x4& acc, const f32x4& bias, h4
 template <int MAP, int NMAX, class Rest>
 __device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng, const Ig1x1W& w, int nt, int mh,
                                               int lane, Rest&& rest) {
-    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = MAP + 1;
+    constexpr int R = MAP + 3, Wd = 2 * R + 1, P = ig_pw(R), ro = MAP + 1;
     static_assert(NMAX >= ig_nmax(ro), "tiles per M half");
     const IgTiles t = ig_tiles(lds, ro, mh, lane);
     f32x4 acc[NMAX];
@@ -974,7 +1029,7 @@ __device__ __forceinline__ void ig_layer1_map(char* lds, const GnUnit* U, int ng
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
         const int i = t.i0 + 16 * m;
-        if (m >= t.nt || i >= t.total) continue;
+        if (m >= t.nt || !ig_valid(lds, ro, i)) continue;
         h4 hi, lo;
         ig_split(acc[m], bias, hi, lo);
         const IgRow r = ig_row(lds, ro, i);
@@ -1067,7 +1122,7 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
             const _Float16* wf = (const _Float16*)(Wp + GH_E) + ((size_t)nt * 64 + ln) * 8;
             const h8 wh = *(const h8*)wf, wl = *(const h8*)(wf + 4 * 64 * 8);
             const f32x4 bias = *(const f32x4*)(Wp + GE_B + ch0);
-            constexpr int P0 = 49;
+            constexpr int P0 = ig_pw(3);
             for (int g = mh; g < ng; g += IMH) {
                 const h8 a = *(const h8*)(col + ((g * 4 + q) * 16 + li) * 8);
                 f32x4 acc = zero4();
@@ -1134,7 +1189,7 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
 #pragma unroll
             for (int m = 0; m < N5; m++) {
                 const int i = t.i0 + 16 * m;
-                if (m >= t.nt || i >= t.total) continue;
+                if (m >= t.nt || !ig_valid(lds, 5, i)) continue;
                 h4 hi, lo;
                 ig_split(acc[m], bias, hi, lo);
                 const int o = ((ch0 >> 3) * BR + i) * 8 + (ch0 & 7);
@@ -1145,7 +1200,7 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
             GN_STAMP(18);
             fresh(Wp, t_);
             const int total = ig_total(lds, 5);
-            if (t_ < total) {
+            if (t_ < 16 * ((total + 15) >> 4) && ig_valid(lds, 5, t_)) {
                 const IgRow r = ig_row(lds, 5, t_);
                 float p0, p1;
                 gn_pconv(Wp, sq + t_ * 8, sq + 8 * BR * 8 + t_ * 8, BR * 8, p0, p1);
