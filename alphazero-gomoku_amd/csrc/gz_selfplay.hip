@@ -498,7 +498,7 @@ struct SlotHeader {  // 128 bytes
     int64_t game_id_stride;
     int32_t n_moves;
     int32_t player;
-    int32_t pad0, pad1;
+    int64_t game_id_end;  // the slot is idle once game_id >= game_id_end (no new game starts)
     int64_t games_done;
     // totals over every search this slot ran since init: predict() calls and RNG
     // draws (main stream, simulation streams).  The checker compares them with the
@@ -524,7 +524,7 @@ __global__ void selfplay_init_kernel(char* slots, int n_slots, int64_t base, int
     h->game_id_stride = stride;
     h->n_moves = 0;
     h->player = 1;
-    h->pad0 = h->pad1 = 0;
+    h->game_id_end = INT64_MAX;
     h->games_done = 0;
     h->predicts = h->main_draws = h->sim_draws = 0;
 }
@@ -549,7 +549,8 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
         rs.player = h->player;
     }
     int64_t game_id = h->game_id;
-    const int64_t gstride = h->game_id_stride;
+    const int64_t gstride = h->game_id_stride, gend = h->game_id_end;
+    if (game_id >= gend) return;  // idle: its games are done
     long long games = 0, moves_played = 0, mcts_played = 0, npred = 0, dmain = 0, dsim = 0;
     Tree t = tree_at(smem, p.num_simulations);
     __syncthreads();
@@ -611,6 +612,7 @@ __global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_sl
                 rs.player = 1;
             }
             __syncthreads();
+            if (game_id >= gend) break;  // no next game: the slot goes idle
         }
     }
     if (lane == 0) {
@@ -638,6 +640,7 @@ __global__ __launch_bounds__(WAVE) void selfplay_commit_kernel(char* slots, int 
     if (s >= n_slots) return;
     const int lane = lane_id();
     SlotHeader* h = (SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
+    if (h->game_id >= h->game_id_end) return;  // idle (its search ran on a dead board; nothing is recorded)
     gz_record* rec = (gz_record*)(h + 1);
     BB black, white;
     load_bb(black, h->black);
@@ -1014,6 +1017,62 @@ int gz_selfplay_plan_gn_stats(void* d_workspace, int32_t n_slots, int32_t num_si
     return gz_plan_gn_stats(ws, n_slots, num_simulations, out, reset, stream);
 }
 
+__global__ void selfplay_limit_kernel(char* slots, int n_slots, int64_t end) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots) return;
+    SlotHeader* h = (SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
+    h->game_id_end = end;
+}
+
+// the new slot index of every slot: the active ones (game_id < game_id_end) first, then
+// the idle ones, each in slot order; one workgroup scans the flags in tiles of 1024
+__global__ __launch_bounds__(1024) void selfplay_order_kernel(const char* slots, int n_slots, int32_t* order,
+                                                              int32_t* n_active) {
+    __shared__ int wsum[16];
+    __shared__ int carry, total;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // pass 0 counts the active slots, pass 1 places both classes
+    for (int pass = 0; pass < 2; pass++) {
+        if (tid == 0) carry = 0;
+        __syncthreads();
+        for (int t0 = 0; t0 < n_slots; t0 += 1024) {
+            const int s = t0 + tid;
+            bool act = false;
+            if (s < n_slots) {
+                const SlotHeader* h = (const SlotHeader*)(slots + (size_t)s * slot_stride_bytes());
+                act = h->game_id < h->game_id_end;
+            }
+            const uint64_t m = __ballot(act);
+            if (lane == 0) wsum[wave] = __popcll(m);
+            __syncthreads();
+            int before = carry;
+            for (int w = 0; w < wave; w++) before += wsum[w];
+            const int rank = before + __popcll(m & ((1ull << lane) - 1));  // active slots before s
+            if (pass == 1 && s < n_slots) order[s] = act ? rank : total + (s - rank);
+            __syncthreads();
+            if (tid == 0) {
+                int c = 0;
+                for (int w = 0; w < 16; w++) c += wsum[w];
+                carry += c;
+            }
+            __syncthreads();
+        }
+        if (tid == 0 && pass == 0) {
+            total = carry;
+            *n_active = carry;
+        }
+        __syncthreads();
+    }
+}
+
+// slot s -> dst slot order[s] (16-B words, one workgroup per slot)
+__global__ __launch_bounds__(256) void selfplay_move_kernel(const char* slots, const int32_t* order, char* dst) {
+    const size_t sb = slot_stride_bytes();
+    const uint4* a = (const uint4*)(slots + (size_t)blockIdx.x * sb);
+    uint4* b = (uint4*)(dst + (size_t)order[blockIdx.x] * sb);
+    for (size_t i = threadIdx.x; i < sb / 16; i += 256) b[i] = a[i];
+}
+
 __global__ void selfplay_draws_kernel(const char* slots, int n_slots, int64_t* out) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
@@ -1021,6 +1080,26 @@ __global__ void selfplay_draws_kernel(const char* slots, int n_slots, int64_t* o
     out[3 * s] = h->predicts;
     out[3 * s + 1] = h->main_draws;
     out[3 * s + 2] = h->sim_draws;
+}
+
+int gz_selfplay_set_game_end(void* d_slots, int32_t n_slots, int64_t game_id_end, void* stream) {
+    if (!d_slots || n_slots <= 0) return fail(GZ_ERR_ARG, "gz_selfplay_set_game_end: bad arguments");
+    selfplay_limit_kernel<<<(n_slots + 255) / 256, 256, 0, as_stream(stream)>>>((char*)d_slots, n_slots, game_id_end);
+    return check_launch("selfplay_limit_kernel");
+}
+
+size_t gz_selfplay_compact_workspace_bytes(int32_t n_slots) { return (size_t)(n_slots > 0 ? n_slots : 0) * 4; }
+
+int gz_selfplay_compact(const void* d_slots, int32_t n_slots, void* d_dst, int32_t* d_n_active, void* d_workspace,
+                        void* stream) {
+    if (!d_slots || n_slots <= 0 || !d_dst || d_dst == d_slots || !d_n_active || !d_workspace)
+        return fail(GZ_ERR_ARG, "gz_selfplay_compact: bad arguments");
+    int32_t* order = (int32_t*)d_workspace;
+    selfplay_order_kernel<<<1, 1024, 0, as_stream(stream)>>>((const char*)d_slots, n_slots, order, d_n_active);
+    int rc = check_launch("selfplay_order_kernel");
+    if (rc) return rc;
+    selfplay_move_kernel<<<n_slots, 256, 0, as_stream(stream)>>>((const char*)d_slots, order, (char*)d_dst);
+    return check_launch("selfplay_move_kernel");
 }
 
 int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream) {

@@ -117,6 +117,9 @@ SIGNATURES = {
     "gz_selfplay_run": (ctypes.c_int, [_P, _I32, ctypes.POINTER(SearchParams), _I32, _P, _I32, _P, _I32, _P, _P, _P]),
     "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "gz_selfplay_draws": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "gz_selfplay_set_game_end": (ctypes.c_int, [_P, _I32, _I64, _P]),
+    "gz_selfplay_compact_workspace_bytes": (_SZ, [_I32]),
+    "gz_selfplay_compact": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P]),
     "gz_pv_weight_floats": (_SZ, []),
     "gz_pv_workspace_bytes": (_SZ, [_I32]),
     "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),

@@ -27,8 +27,11 @@ class SelfPlayEngine:
     def __init__(self, n_slots=4096, num_simulations=200, c_puct=1.6, exploration=0.05, beta=0.2,
                  seed=0, max_depth=100, pv_weights=None, plies_per_step=1, game_id_base=0,
                  game_id_stride=None, planner_steps=0, planner_difficulty="medium", gn_weights=None,
-                 pv_mode="full"):
-        """planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
+                 pv_mode="full", game_id_end=None):
+        """game_id_end: a slot whose next game id would be >= game_id_end goes idle
+        instead of restarting (gz_selfplay_set_game_end; default: continuous refill);
+        :meth:`compact` then moves the active slots to the front so that only those run.
+        planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
         planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights.
         pv_mode: "full" = one full forward per node (gz_pv_forward); "tree" = the
         incremental forward (gz_pv_forward_tree: a root's children and grandchildren
@@ -38,6 +41,7 @@ class SelfPlayEngine:
         (gz_pv_forward_tree_mode GZ_TREE_DELTA: within 1e-4 of the full forward)."""
         self.lib = require_gpu()
         self.n_slots = int(n_slots)
+        self.n_active = self.n_slots  # the slots the launches run (the first n_active)
         self.plies_per_step = int(plies_per_step)
         self.gather = pv_weights is not None
         self.planner_steps = int(planner_steps)
@@ -87,6 +91,26 @@ class SelfPlayEngine:
         stride = self.n_slots if game_id_stride is None else int(game_id_stride)
         _lib.check(self.lib.gz_selfplay_init(ptr(self.d_slots), self.n_slots, S, base, stride, stream()),
                    "gz_selfplay_init")
+        self.d_slots_alt = self.d_compact_ws = self.d_n_active = None
+        if game_id_end is not None:
+            _lib.check(self.lib.gz_selfplay_set_game_end(ptr(self.d_slots), self.n_slots, int(game_id_end), stream()),
+                       "gz_selfplay_set_game_end")
+            self.d_slots_alt = torch.empty_like(self.d_slots)
+            self.d_compact_ws = torch.empty(self.lib.gz_selfplay_compact_workspace_bytes(self.n_slots),
+                                            dtype=torch.uint8, device="cuda")
+            self.d_n_active = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def compact(self):
+        """Launch gz_selfplay_compact: the active slots to the front of the slot buffer
+        (the two buffers swap).  Returns the device int32 [1] active count; the caller
+        sets :attr:`n_active` from it once read (the next launches run that many)."""
+        if self.d_slots_alt is None:
+            raise ValueError("compact() needs an engine built with game_id_end")
+        _lib.check(self.lib.gz_selfplay_compact(ptr(self.d_slots), self.n_slots, ptr(self.d_slots_alt),
+                                                ptr(self.d_n_active), ptr(self.d_compact_ws), stream()),
+                   "gz_selfplay_compact")
+        self.d_slots, self.d_slots_alt = self.d_slots_alt, self.d_slots
+        return self.d_n_active
 
     # ---- launches (asynchronous, current torch stream)
     def launch_search(self, n_plies=None):
@@ -94,14 +118,16 @@ class SelfPlayEngine:
         if n > self.plies_per_step and self.gather:
             raise ValueError("n_plies exceeds the leaf buffer sized for plies_per_step")
         self.d_counters.zero_()
+        if self.n_active == 0:  # every game is done
+            return
         if self.planner_steps:
-            _lib.check(self.lib.gz_selfplay_plan_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params),
+            _lib.check(self.lib.gz_selfplay_plan_run(ptr(self.d_slots), self.n_active, ctypes.byref(self.params),
                                                      ctypes.byref(self.pparams), ptr(self.gn_weights.tensor),
                                                      ptr(self.d_plan_ws), n, ptr(self.d_records), self.record_cap,
                                                      ptr(self.d_leaves), self.leaf_cap, ptr(self.d_meta),
                                                      ptr(self.d_counters), stream()), "gz_selfplay_plan_run")
             return
-        _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_slots, ctypes.byref(self.params), n,
+        _lib.check(self.lib.gz_selfplay_run(ptr(self.d_slots), self.n_active, ctypes.byref(self.params), n,
                                             ptr(self.d_records), self.record_cap, ptr(self.d_leaves),
                                             self.leaf_cap, ptr(self.d_meta), ptr(self.d_counters), stream()),
                    "gz_selfplay_run")
@@ -137,7 +163,7 @@ class SelfPlayEngine:
                                                 ptr(self.d_counters), stream()), "gz_selfplay_run")
 
     def launch_pv(self):
-        if not self.gather:
+        if not self.gather or self.n_active == 0:
             return
         d_count = self.d_counters[4:8]  # counters.leaves
         if self.tree:

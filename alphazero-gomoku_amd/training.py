@@ -219,16 +219,22 @@ def selfplay(n_games: int, num_simulations: int = 200, difficulty: str = "medium
 
 def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int = 200, difficulty: str = "medium",
                     beta: float = 0.2, seed: int = 0, n_slots: int = 4096, game_id_base: int = 0, model=None,
-                    plies_per_step: int = 16, planner_steps: int = 0, planner=None, pv_mode: str = "tree"):
+                    plies_per_step: int = 16, planner_steps: int = 0, planner=None, pv_mode: str = "tree",
+                    compact: bool = True):
     """training.run_iteration's self-play on every rank: this rank plays game ids
     [game_id_base, game_id_base + n_games) as ``selfplay`` does, and each step's
     finished games go through the sync-free RecordExchange (one all-gather per step,
     RCCL) into a ReplayCollector, so every rank ends with the rows of ALL ranks'
     games in [id_lo, id_hi), sorted by (game id, ply), on the device -- each game
-    once: rank r's rows count only for rank r's own ids (its slots' refill games
-    carry rank r + 1's ids).  One host synchronisation per step reads the played
-    moves, the finished-game count and every loss counter (exchange overflow,
-    collector drops, engine record drops: any of them raises at once).  The loop
+    once: rank r's rows count only for rank r's own ids.  compact=True: a slot whose
+    games are done goes idle instead of starting the next id (game_id_end), and after
+    every step the active slots move to the front, so that the next step runs only
+    those (the games and rows are the same; the refill games a slot would otherwise
+    play while the last games finish -- rank r + 1's ids, discarded -- are not
+    played).  compact=False: continuous refill.  One host synchronisation per step
+    reads the played moves, the finished-game count, the active slots and every loss
+    counter (exchange overflow, collector drops, engine record drops: any of them
+    raises at once).  The loop
     ends when every one of those games has arrived (the count every rank computes
     from the same chunks, so the ranks stop together), or raises after a bound on
     the steps the games can take.
@@ -250,15 +256,16 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
                          beta=beta, seed=seed, pv_weights=pvw,
                          plies_per_step=min(plies_per_step, 4) if tree else plies_per_step,
                          game_id_base=game_id_base, planner_steps=planner_steps,
-                         planner_difficulty=difficulty, gn_weights=gnw, pv_mode="tree" if tree else "full")
+                         planner_difficulty=difficulty, gn_weights=gnw, pv_mode="tree" if tree else "full",
+                         game_id_end=game_id_base + n_games if compact else None)
     # a chunk of a quarter of the engine's record buffer: a game's records leave the
     # outbox in one or a few steps even when many games end together
     ex = gdist.RecordExchange(eng.record_cap, max(2 * eng.n_slots * eng.plies_per_step, eng.record_cap // 4), "cuda")
     want = id_hi - id_lo
     if want != ws * n_games or not id_lo <= game_id_base < id_hi:
         raise ValueError("selfplay_device: [id_lo, id_hi) must be the ranks' n_games-wide shares")
-    # rank r keeps only its own share from rank r's rows: its slots' refill games
-    # (id + n_slots) run into rank r + 1's ids
+    # rank r keeps only its own share from rank r's rows: with continuous refill its
+    # slots' refill games (id + n_slots) run into rank r + 1's ids
     col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda", per_rank=n_games)
     moves = steps = 0
     # a slot plays ceil(n_games / slots) games of <= 200 plies: past that bound a
@@ -270,10 +277,16 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
         ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
         col.absorb(*ex.exchange())
         steps += 1
-        # the step's one host synchronisation: moves, finished games and every loss counter
-        c = torch.cat([eng.d_counters.view(torch.int64)[2:3], col.games, ex.overflow, col.dropped,
-                       eng.d_counters[0:16].view(torch.int32)[2:3].to(torch.int64)]).cpu().tolist()
+        parts = [eng.d_counters.view(torch.int64)[2:3], col.games, ex.overflow, col.dropped,
+                 eng.d_counters[0:16].view(torch.int32)[2:3].to(torch.int64)]
+        if compact:
+            parts.append(eng.compact().to(torch.int64))
+        # the step's one host synchronisation: moves, finished games, active slots and
+        # every loss counter
+        c = torch.cat(parts).cpu().tolist()
         moves += int(c[0])
+        if compact:
+            eng.n_active = int(c[5])
         if c[2] or c[3] or c[4]:
             raise RuntimeError(f"selfplay_device: records lost (exchange overflow {c[2]}, collector {c[3]}, "
                                f"engine buffer {c[4]})")

@@ -162,6 +162,18 @@ int gz_selfplay_plan_run(void* d_slots, int32_t n_slots, const gz_search_params*
  * predict() calls, d_out[3s+1] = main-stream RNG draws, d_out[3s+2] = simulation-
  * stream draws (the checker's view of rollout / planner decisions, ai_agent.py:168-285) */
 int gz_selfplay_draws(const void* d_slots, int32_t n_slots, int64_t* d_out, void* stream);
+/* A bounded game range (training.py:374-377 plays exactly its n games per iteration):
+ * a slot whose next game id would be >= game_id_end goes idle instead of restarting --
+ * gz_selfplay_run / gz_selfplay_plan_run skip it and record nothing for it (default:
+ * no end, continuous refill). */
+int gz_selfplay_set_game_end(void* d_slots, int32_t n_slots, int64_t game_id_end, void* stream);
+/* Copies the slots into d_dst (another n_slots-slot buffer) with the active ones first
+ * and the idle ones after, each in slot order; *d_n_active = the active count.  A slot
+ * holds its whole game state, so the caller may then run the first *d_n_active slots
+ * of d_dst only.  d_workspace: gz_selfplay_compact_workspace_bytes(n_slots). */
+size_t gz_selfplay_compact_workspace_bytes(int32_t n_slots);
+int gz_selfplay_compact(const void* d_slots, int32_t n_slots, void* d_dst, int32_t* d_n_active, void* d_workspace,
+                        void* stream);
 /* current board of every slot (for inspection / tests) */
 int gz_selfplay_boards(const void* d_slots, int32_t n_slots, int32_t num_simulations,
                        gz_board_state* d_out, int64_t* d_game_ids, void* stream);

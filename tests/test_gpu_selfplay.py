@@ -234,3 +234,36 @@ def test_config2_4096_slot_step_properties(oracle):
     assert torch.allclose(probs.sum(dim=1), torch.ones(n, device="cuda"), atol=1e-5)
     ps = eng.d_prior[: n * 225].view(n, 225).sum(dim=1)
     assert torch.allclose(ps, torch.ones_like(ps), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("planner_steps", [0, 2])
+def test_selfplay_device_bounded_games_compaction(planner_steps):
+    """training.selfplay_device with a bounded game range (game_id_end: a slot whose
+    games are done goes idle) and the active slots compacted after every step
+    (gz_selfplay_compact) against continuous refill: the same rows bit for bit, every
+    game once, fewer plies played.  40 games on 16 slots (each slot plays 2-3 games,
+    then idles), 12 simulations, with the PV tree forward; planner_steps 2 runs the
+    planner pipeline (gz_selfplay_plan_run: idle slots are searched within a step
+    and must record nothing)."""
+    import training
+    from bg_planner import BGPlannerAI
+    from gzero import planner_nets, weights
+    from neural_network import GomokuModel
+    model = GomokuModel(device="cpu")
+    model.model.load_state_dict(weights.init_state_dict(seed=3))
+    planner = None
+    if planner_steps:
+        planner = BGPlannerAI(1, "medium", seed=0)
+        planner.graph_net.load_state_dict(planner_nets.init_graphnet_state(21))
+        planner.opp_dqn.load_state_dict(planner_nets.init_dqn_state(22))
+    out = {}
+    for compact in (False, True):
+        rows, n, st = training.selfplay_device(40, 0, 40, num_simulations=12, beta=0.2, seed=SEED, n_slots=16,
+                                               model=model, plies_per_step=4, planner_steps=planner_steps,
+                                               planner=planner, compact=compact)
+        out[compact] = (rows[:n].cpu().numpy().copy(), st)
+    (a, sa), (b, sb) = out[False], out[True]
+    assert a.shape == b.shape and np.array_equal(a, b)
+    recs = np.frombuffer(b.tobytes(), boards.RECORD_DTYPE)
+    assert sorted(set(int(g) for g in recs["game_id"])) == list(range(40))
+    assert sb["moves_played"] == len(recs) < sa["moves_played"]
