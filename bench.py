@@ -352,9 +352,11 @@ def config5(games, sims, seed, iterations=2):
             "first_iteration_s": round(its[0]["iteration_s"], 2),
             "workload": (f"BASELINE config 5 on 1 GPU: training.run_iteration with {games} self-play games per "
                          f"iteration ({sims} sims, medium, beta 0.2, planner_steps 5, tree PV forward on every node, "
-                         "records through gzero.dist.RecordExchange), 35 % augmentation, 2 epochs of SGD "
-                         "(batch 128, Adam 8e-4, clip 0.8; residual tower on gz_sgd_forward/backward, f16x3 MFMA; conv0 and the "
-                         "heads torch), StepLR; games per iteration fixed by the builder (BASELINE names none); "
+                         "records through gzero.dist.RecordExchange; each game played once: slots idle past the "
+                         "iteration's ids and are compacted), 35 % augmentation, 2 epochs of SGD "
+                         "(batch 128, Adam 8e-4, clip 0.8; conv0, residual tower and 1x1 head convs on "
+                         "gz_sgd_forward/backward, f16x3 MFMA tower; the FC heads torch), StepLR; games per iteration "
+                         "fixed by the builder (BASELINE names none); "
                          "value from the last of "
                          f"{iterations} iterations")}
 
