@@ -180,7 +180,7 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_conv0_kernel(const float* __re
 // fp64), BN scale/shift, the running-stat update (momentum, unbiased variance) --
 // torch BatchNorm2d in training mode.  1024 threads: channel c = tid % 128 over the
 // boards b = tid / 128 (mod 8), combined in LDS.
-constexpr int RED_THREADS = 1024, RED_PARTS = RED_THREADS / CH, RED_THREADS_H = 512;
+constexpr int RED_THREADS = 1024, RED_PARTS = RED_THREADS / CH;
 __device__ __forceinline__ double red_sum(double v, double* sh, int c, int h) {
     __syncthreads();
     sh[h * CH + c] = v;
@@ -277,7 +277,9 @@ __global__ __launch_bounds__(RED_THREADS) void sgd_bn_bwd_reduce_kernel(const fl
 // The heads' 1x1 convs backward and the tower output's ReLU: dL/da2[p][c] =
 // dpin[0][p] wp[0][c] + dpin[1][p] wp[1][c] + dvin[p] wv[c]; g4 = that [a2 > 0] and
 // its BN-backward partials (sum g, sum g xhat, max |g|); the board's partial weight
-// gradients of policy_conv / value_conv (sum_p dpin[k][p] a2[p][c], sum_p dvin[p] a2[p][c]).
+// gradients of policy_conv / value_conv (sum_p dpin[k][p] a2[p][c], sum_p dvin[p] a2[p][c])
+// and of their biases (sum_p dpin[k][p], sum_p dvin[p]): hpart[b][HP], HP = 3 CH + 4.
+constexpr int HP = 3 * CH + 4;
 __global__ __launch_bounds__(PB_THREADS) void sgd_heads_bwd_kernel(const float* __restrict__ dpin,
                                                                   const float* __restrict__ dvin,
                                                                   const float* __restrict__ act,
@@ -294,11 +296,14 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_heads_bwd_kernel(const float* 
     const size_t base = (size_t)b * NPOS * 32 + q;
     const float* dp = dpin + (size_t)b * 2 * NPOS;
     const float* dv = dvin + (size_t)b * NPOS;
-    f32x4 s = zero4(), sx = zero4(), mx = zero4(), h0 = zero4(), h1 = zero4(), h2 = zero4();
+    f32x4 s = zero4(), sx = zero4(), mx = zero4(), h0 = zero4(), h1 = zero4(), h2 = zero4(), hb = zero4();
 #pragma unroll 4
     for (int p = h; p < NPOS; p += PB_STRIDES) {
         const size_t o = base + (size_t)p * 32;
         const float d0 = dp[p], d1 = dp[NPOS + p], d2 = dv[p];
+        hb[0] += d0;
+        hb[1] += d1;
+        hb[2] += d2;
         const f32x4 a = ((const f32x4*)act)[o], yv = ((const f32x4*)y)[o];
         const f32x4 da = d0 * w0 + d1 * w1 + d2 * w2;
         f32x4 v;
@@ -320,53 +325,42 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_heads_bwd_kernel(const float* 
     h0 = pb_reduce(h0, sh, q, h, false);
     h1 = pb_reduce(h1, sh, q, h, false);
     h2 = pb_reduce(h2, sh, q, h, false);
+    hb = pb_reduce(hb, sh, q, h, false);  // (the same in every q)
     if (h == 0) {
         float* o = part + (size_t)b * PART + 4 * q;
         *(f32x4*)o = s;
         *(f32x4*)(o + CH) = sx;
         *(f32x4*)(o + 2 * CH) = mx;
-        float* oh = hpart + (size_t)b * 3 * CH + 4 * q;
+        float* oh = hpart + (size_t)b * HP + 4 * q;
         *(f32x4*)oh = h0;
         *(f32x4*)(oh + CH) = h1;
         *(f32x4*)(oh + 2 * CH) = h2;
+        if (q == 0) *(f32x4*)(hpart + (size_t)b * HP + 3 * CH) = hb;
     }
 }
 
-// the heads' weight and bias gradients: sums of the boards' partials (weights) and of
-// dpin / dvin (biases)
-__global__ __launch_bounds__(RED_THREADS_H) void sgd_heads_reduce_kernel(const float* __restrict__ hpart,
-                                                                        const float* __restrict__ dpin,
-                                                                        const float* __restrict__ dvin, int B,
-                                                                        float* __restrict__ dwp, float* __restrict__ dbp,
-                                                                        float* __restrict__ dwv, float* __restrict__ dbv) {
-    __shared__ float sh[3][RED_THREADS_H];
-    const int t = threadIdx.x;
-    if (t < 3 * CH) {
-        float a = 0.f;
-        for (int b = 0; b < B; b++) a += hpart[(size_t)b * 3 * CH + t];
-        if (t < 2 * CH) dwp[t] = a; else dwv[t - 2 * CH] = a;
+// the heads' weight and bias gradients: the sums of the boards' partials.  Workgroup k
+// takes outputs [128 k, 128 k + 128) of the HP (the last 3 = the biases), 4 threads per
+// output over interleaved quarters of the boards, combined in a fixed order.
+constexpr int HR_THREADS = 512;
+__global__ __launch_bounds__(HR_THREADS) void sgd_heads_reduce_kernel(const float* __restrict__ hpart, int B,
+                                                                     float* __restrict__ dwp, float* __restrict__ dbp,
+                                                                     float* __restrict__ dwv, float* __restrict__ dbv) {
+    __shared__ float sh[HR_THREADS];
+    const int t = threadIdx.x, o = blockIdx.x * 128 + (t & 127), qq = t >> 7;
+    float a = 0.f;
+    if (o < 3 * CH + 3) {
+#pragma unroll 8
+        for (int b = qq; b < B; b += 4) a += hpart[(size_t)b * HP + o];
     }
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int i = t; i < B * NPOS; i += RED_THREADS_H) {
-        const int b = i / NPOS, p = i - b * NPOS;
-        s0 += dpin[(size_t)b * 2 * NPOS + p];
-        s1 += dpin[(size_t)b * 2 * NPOS + NPOS + p];
-        s2 += dvin[i];
-    }
-    sh[0][t] = s0;
-    sh[1][t] = s1;
-    sh[2][t] = s2;
+    sh[t] = a;
     __syncthreads();
-    for (int w = RED_THREADS_H / 2; w > 0; w >>= 1) {
-        if (t < w)
-            for (int k = 0; k < 3; k++) sh[k][t] += sh[k][t + w];
-        __syncthreads();
-    }
-    if (t == 0) {
-        dbp[0] = sh[0][0];
-        dbp[1] = sh[1][0];
-        dbv[0] = sh[2][0];
-    }
+    if (qq || o >= 3 * CH + 3) return;
+    a = (sh[t] + sh[t + 128]) + (sh[t + 256] + sh[t + 384]);
+    if (o < 2 * CH) dwp[o] = a;
+    else if (o < 3 * CH) dwv[o - 2 * CH] = a;
+    else if (o < 3 * CH + 2) dbp[o - 3 * CH] = a;
+    else dbv[0] = a;
 }
 
 // conv0's weight / bias gradient partials of a board: dy0 = k (g0 - mg - xhat mgx)
@@ -901,7 +895,7 @@ struct Ws {
     float* fpart;     // [NBN][B][PART]
     float* bpart;     // [NBN][B][PART]
     float* wpart;     // [9][NG][CH][CH]
-    float* hpart;     // [B][3][CH] heads' weight-gradient partials
+    float* hpart;     // [B][HP] heads' weight- and bias-gradient partials
     float* c0part;    // [B][CH][28] conv0's weight / bias gradient partials
     int NG, G;
 };
@@ -929,7 +923,7 @@ size_t ws_layout(int B, Ws* w, char* base) {
     t.fpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.bpart = (float*)take((size_t)NBN * B * PART * sizeof(float));
     t.wpart = (float*)take((size_t)9 * NG * CH * CH * sizeof(float));
-    t.hpart = (float*)take((size_t)B * 3 * CH * sizeof(float));
+    t.hpart = (float*)take((size_t)B * HP * sizeof(float));
     t.c0part = (float*)take((size_t)B * CH * (C0K + 1) * sizeof(float));
     t.NG = NG;
     t.G = G;
@@ -1049,8 +1043,8 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
     sgd_heads_bwd_kernel<<<B, PB_THREADS, 0, s>>>(d_dpin, d_dvin, w.out, w.y[4], w.coef + 4 * CO_FLOATS,
                                                   net->policy_weight, net->value_weight, w.g[4],
                                                   w.bpart + (size_t)4 * B * PART, w.hpart);
-    sgd_heads_reduce_kernel<<<1, RED_THREADS_H, 0, s>>>(w.hpart, d_dpin, d_dvin, B, gr->policy_weight,
-                                                        gr->policy_bias, gr->value_weight, gr->value_bias);
+    sgd_heads_reduce_kernel<<<(HP + 127) / 128, HR_THREADS, 0, s>>>(w.hpart, B, gr->policy_weight, gr->policy_bias,
+                                                                    gr->value_weight, gr->value_bias);
     for (int L = LAYERS; L >= 1; L--) {
         float* coefL = w.coef + (size_t)L * CO_FLOATS;
         sgd_bn_bwd_reduce_kernel<<<1, RED_THREADS, 0, s>>>(w.bpart + (size_t)L * B * PART, B, net->bn_weight[L],

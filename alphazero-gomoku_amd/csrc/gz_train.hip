@@ -172,3 +172,133 @@ extern "C" int gz_dataset_gather(const gz_record* d_records, int32_t n, const in
     return launch(d_records, n, d_sel, m, d_ids, count, flags, d_x, d_y, d_v, (hipStream_t)stream,
                   "gz_dataset_gather");
 }
+
+// ============================================================ optimiser step
+// clip_grad_norm_ + torch.optim.Adam (training.py:303-304) over the parameter tensors:
+// adam_norm_kernel sums g^2 in float64 over a fixed slice of the concatenated elements per
+// workgroup; adam_update_kernel re-reduces those partials in the same order in every
+// workgroup (so every workgroup has the same clip factor, no grid barrier), then applies
+// the clip and the Adam update to its slice.
+namespace {
+constexpr int ADAM_BLOCKS = 512, ADAM_THREADS = 256;
+
+struct AdamTable {  // by value (kernel arguments)
+    gz_adam_tensor t[GZ_ADAM_MAX_TENSORS];
+    int64_t start[GZ_ADAM_MAX_TENSORS + 1];  // prefix of numel
+    int n;
+};
+
+__device__ __forceinline__ int adam_find(const AdamTable& T, int64_t i) {
+    int k = 0;
+    while (k + 1 < T.n && T.start[k + 1] <= i) k++;
+    return k;
+}
+
+template <class F>
+__device__ __forceinline__ void adam_slice(const AdamTable& T, F&& f) {
+    const int64_t total = T.start[T.n];
+    const int64_t per = (total + ADAM_BLOCKS - 1) / ADAM_BLOCKS;
+    const int64_t b = per * blockIdx.x, e = b + per < total ? b + per : total;
+    for (int64_t i0 = b; i0 < e; i0 += ADAM_THREADS) {
+        const int64_t i = i0 + threadIdx.x;
+        if (i >= e) break;
+        const int k = adam_find(T, i);
+        f(T.t[k], i - T.start[k]);
+    }
+}
+
+__device__ __forceinline__ double adam_block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int j = 0; j < ADAM_THREADS / 64; j++) s += red[j];
+    __syncthreads();
+    return s;
+}
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_norm_kernel(AdamTable T, double* partial) {
+    __shared__ double red[ADAM_THREADS / 64];
+    double s = 0.0;
+    adam_slice(T, [&](const gz_adam_tensor& t, int64_t j) {
+        const double g = t.grad[j];
+        s += g * g;
+    });
+    s = adam_block_sum(s, red);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(AdamTable T, const double* partial, float lr,
+                                                                   float beta1, float beta2, float eps, float wd,
+                                                                   float bc1, float bc2s, float max_norm,
+                                                                   float* norm_out) {
+    __shared__ double red[ADAM_THREADS / 64];
+    float clip = 1.f;
+    if (max_norm > 0.f) {
+        double s = 0.0;
+        for (int j = threadIdx.x; j < ADAM_BLOCKS; j += ADAM_THREADS) s += partial[j];
+        s = adam_block_sum(s, red);
+        const float norm = (float)sqrt(s);
+        const float c = max_norm / (norm + 1e-6f);
+        clip = c < 1.f ? c : 1.f;
+        if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) *norm_out = norm;
+    }
+    const float step_size = lr / bc1;
+    adam_slice(T, [&](const gz_adam_tensor& t, int64_t j) {
+        float g = t.grad[j];
+        if (max_norm > 0.f) {
+            g *= clip;
+            t.grad[j] = g;
+        }
+        const float p = t.param[j];
+        if (wd != 0.f) g = g + wd * p;
+        const float m0 = t.exp_avg[j];
+        const float m = m0 + (1.f - beta1) * (g - m0);  // torch's exp_avg.lerp_(grad, 1 - beta1)
+        const float v = beta2 * t.exp_avg_sq[j] + (1.f - beta2) * g * g;
+        t.exp_avg[j] = m;
+        t.exp_avg_sq[j] = v;
+        const float denom = sqrtf(v) / bc2s + eps;
+        t.param[j] = p - step_size * (m / denom);
+    });
+}
+}  // namespace
+
+extern "C" size_t gz_adam_workspace_bytes(void) { return ADAM_BLOCKS * sizeof(double); }
+
+extern "C" int gz_adam_step(const gz_adam_tensor* tensors, int32_t n_tensors, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int64_t step, float max_norm, float* d_norm,
+                            void* d_workspace, void* stream) {
+    if (!tensors || n_tensors < 1 || n_tensors > GZ_ADAM_MAX_TENSORS || step < 1 || !d_workspace) {
+        gz_internal_set_error("gz_adam_step: bad arguments");
+        return GZ_ERR_ARG;
+    }
+    AdamTable T;
+    T.n = n_tensors;
+    T.start[0] = 0;
+    for (int k = 0; k < n_tensors; k++) {
+        const gz_adam_tensor& t = tensors[k];
+        if (t.numel < 0 || (t.numel > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq))) {
+            gz_internal_set_error("gz_adam_step: bad tensor");
+            return GZ_ERR_ARG;
+        }
+        T.t[k] = t;
+        T.start[k + 1] = T.start[k] + t.numel;
+    }
+    for (int k = n_tensors; k < GZ_ADAM_MAX_TENSORS; k++) T.t[k] = gz_adam_tensor{};
+    if (T.start[n_tensors] == 0) return GZ_OK;
+    hipStream_t st = (hipStream_t)stream;
+    double* partial = (double*)d_workspace;
+    // torch's bias corrections: 1 - beta^step in float64, then used in float32
+    const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+    const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+    if (max_norm > 0.f) adam_norm_kernel<<<ADAM_BLOCKS, ADAM_THREADS, 0, st>>>(T, partial);
+    adam_update_kernel<<<ADAM_BLOCKS, ADAM_THREADS, 0, st>>>(T, partial, lr, beta1, beta2, eps, weight_decay, bc1,
+                                                             bc2s, max_norm, d_norm);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gz_internal_set_error((std::string("gz_adam_step: ") + hipGetErrorString(e)).c_str());
+        return GZ_ERR_HIP;
+    }
+    return GZ_OK;
+}

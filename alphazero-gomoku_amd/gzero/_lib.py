@@ -96,6 +96,12 @@ class SgdGrads(ctypes.Structure):  # gz_sgd_grads
 
 
 GZ_SGD_MAX_BOARDS = 65535
+GZ_ADAM_MAX_TENSORS = 48
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -118,6 +124,9 @@ SIGNATURES = {
     "gz_selfplay_boards": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
     "gz_selfplay_draws": (ctypes.c_int, [_P, _I32, _P, _P]),
     "gz_selfplay_set_game_end": (ctypes.c_int, [_P, _I32, _I64, _P]),
+    "gz_adam_workspace_bytes": (_SZ, []),
+    "gz_adam_step": (ctypes.c_int, [_P, _I32, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float, _I64, ctypes.c_float, _P, _P, _P]),
     "gz_selfplay_compact_workspace_bytes": (_SZ, [_I32]),
     "gz_selfplay_compact": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P]),
     "gz_pv_weight_floats": (_SZ, []),

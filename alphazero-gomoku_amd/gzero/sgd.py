@@ -95,9 +95,9 @@ class _Tower(torch.autograd.Function):
         st.eps = float(bns[0].eps)
         _lib.check(lib.gz_sgd_forward(ctypes.byref(st), B, _ptr(xc), _ptr(pin), _ptr(vin), _ptr(ws), _stream()),
                    "gz_sgd_forward")
-        for bn in bns:
-            if bn.track_running_stats:
-                bn.num_batches_tracked.add_(1)
+        counts = [bn.num_batches_tracked for bn in bns if bn.track_running_stats]
+        if counts:
+            torch._foreach_add_(counts, 1)  # one launch for the five counters
         ctx.st, ctx.B, ctx.ws = st, B, ws
         ctx.keep = (xc, params)  # the forward's pointers stay valid for the backward
         return pin, vin

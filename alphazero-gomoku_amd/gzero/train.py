@@ -157,8 +157,8 @@ class DeviceTrainer:
     On a GPU the training forward/backward of the residual tower runs on the HIP
     kernels of csrc/gz_sgd.hip (``gzero.sgd.train_forward``; ``native=False``: torch's
     own convolutions, kept for comparison); on the CPU (gloo rehearsals of the
-    data-parallel loop) it is torch's.  On the GPU Adam is torch's fused
-    implementation (one kernel per step instead of a dozen multi-tensor passes)."""
+    data-parallel loop) it is torch's.  With the native kernels, clip_grad_norm_ + Adam
+    are gzero.optim.DeviceAdam (csrc/gz_train.hip: two launches per step)."""
 
     def __init__(self, model, lr=8e-4, weight_decay=1e-5, grad_clip=0.8, step_size=2, gamma=0.85, group=None,
                  device="cuda", native=None):
@@ -178,8 +178,12 @@ class DeviceTrainer:
         self.group = group
         self.world, self.rank = _world(group)
         self.params = [p for p in self.net.parameters()]
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay,
-                                          fused=True if self.device.type == "cuda" else None)
+        if self.native:
+            from .optim import DeviceAdam
+            self.optimizer = DeviceAdam(self.params, lr=lr, weight_decay=weight_decay)
+        else:
+            self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay,
+                                              fused=True if self.device.type == "cuda" else None)
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=step_size, gamma=gamma)
         self.ce, self.mse = nn.CrossEntropyLoss(), nn.MSELoss()
         if self.world > 1:
@@ -207,6 +211,16 @@ class DeviceTrainer:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
             p.grad.copy_(g.view_as(p))
+
+    def clip_and_step(self):
+        """clip_grad_norm_(params, grad_clip) then the Adam step (training.py:303-304)."""
+        clip = self.grad_clip is not None and self.grad_clip > 0
+        if self.native:
+            self.optimizer.step(max_norm=self.grad_clip if clip else None)
+            return
+        if clip:
+            nn.utils.clip_grad_norm_(self.params, self.grad_clip)
+        self.optimizer.step()
 
     def _slices(self, order, batch_size):
         """Per-step (this rank's ids, local count, global count) of a permutation."""
@@ -250,9 +264,7 @@ class DeviceTrainer:
                 self._allreduce_grads()
                 lval = lval * (local / gcount)
                 dist.all_reduce(lval, group=self.group)
-            if self.grad_clip is not None and self.grad_clip > 0:
-                nn.utils.clip_grad_norm_(self.params, self.grad_clip)
-            self.optimizer.step()
+            self.clip_and_step()
             total += lval.double()
             batches += 1
         if self.world > 1:

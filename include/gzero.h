@@ -382,6 +382,28 @@ int gz_sgd_backward(const gz_sgd_net* net, int32_t boards, const float* d_x, con
  * outputs y1..y4, 8 = the tower output a2, 9 = y0 = conv0's output (fp32 NHWC) */
 int gz_sgd_saved(const void* d_workspace, int32_t boards, int32_t which, float* d_out, void* stream);
 
+/* The optimiser step of training.train_epoch (training.py:303-304): clip_grad_norm_(params,
+ * max_norm) then Adam(lr, betas, eps, weight_decay) (torch.optim.Adam, L2 weight decay),
+ * over up to GZ_ADAM_MAX_TENSORS tensors in two launches.  max_norm > 0: the gradients are
+ * scaled by min(1, max_norm / (||g||_2 + 1e-6)) (the norm over every tensor, summed in
+ * float64 in a fixed order: deterministic) -- in place, as clip_grad_norm_ does; max_norm
+ * <= 0: no clipping.  step = the step number after this update (1 on the first).  Then per
+ * element g' = g + wd p; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2;
+ * p -= (lr / (1-b1^step)) m / (sqrt(v) / sqrt(1-b2^step) + eps).  d_norm (optional): the
+ * pre-clip norm (float32, as clip_grad_norm_ returns).  d_workspace:
+ * gz_adam_workspace_bytes(). */
+#define GZ_ADAM_MAX_TENSORS 48
+typedef struct gz_adam_tensor {
+    float* param;
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+} gz_adam_tensor;
+size_t gz_adam_workspace_bytes(void);
+int gz_adam_step(const gz_adam_tensor* tensors, int32_t n_tensors, float lr, float beta1, float beta2, float eps,
+                 float weight_decay, int64_t step, float max_norm, float* d_norm, void* d_workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

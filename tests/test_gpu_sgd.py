@@ -178,11 +178,41 @@ def test_sgd_tower_two_steps_match_torch_trainer():
             lg, val = tr._forward(x.cuda())
             loss = nn.CrossEntropyLoss()(lg, y.cuda()) + nn.MSELoss()(val, v.cuda())
             loss.backward()
-            nn.utils.clip_grad_norm_(tr.params, 0.8)
-            tr.optimizer.step()
+            tr.clip_and_step()  # (grad_clip 0.8: DeviceAdam on the native trainer, torch's on the other)
             ls.append(float(loss))
         losses.append(ls)
     np.testing.assert_allclose(losses[0], losses[1], rtol=1e-3)
     for (k, a), (_, b) in zip(nets[0].named_buffers(), nets[1].named_buffers()):
         assert torch.allclose(a.float(), b.float(), rtol=1e-2, atol=1e-2), k
 
+
+
+def test_device_adam_matches_torch_adam_with_clipping():
+    """gzero.optim.DeviceAdam.step(max_norm) against clip_grad_norm_ + torch.optim.Adam
+    (the reference's training.py:303-304 pair) on the policy-value net's parameter
+    shapes: 6 steps with fresh random gradients (one step unclipped: norm below
+    max_norm), a learning-rate change half way (StepLR's), weight decay 1e-5.  The
+    parameters within 1e-6 (relative, max-norm), the pre-clip norm within 1e-6."""
+    from gzero.optim import DeviceAdam
+    net = _net(SEED).cuda()
+    ref = [p.detach().clone() for p in net.parameters()]
+    mine = [p.detach().clone() for p in net.parameters()]
+    opt_ref = torch.optim.Adam(ref, lr=8e-4, weight_decay=1e-5)
+    opt = DeviceAdam(mine, lr=8e-4, weight_decay=1e-5)
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    for k in range(6):
+        scale = 1e-4 if k == 2 else 1.0  # step 2: total norm < max_norm, no clipping
+        for a, b in zip(ref, mine):
+            g = torch.randn(a.shape, generator=gen, device="cuda") * scale
+            a.grad, b.grad = g.clone(), g.clone()
+        if k == 3:
+            for o in (opt_ref, opt):
+                o.param_groups[0]["lr"] = 8e-4 * 0.85
+        n_ref = float(nn.utils.clip_grad_norm_(ref, 0.8))
+        opt_ref.step()
+        opt.step(max_norm=0.8)
+        assert abs(float(opt.last_norm) - n_ref) <= 1e-6 * n_ref
+        for a, b in zip(ref, mine):
+            assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=0), k  # clipped in place
+            err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-12)
+            assert err < 1e-6, (k, err)

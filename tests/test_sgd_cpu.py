@@ -53,3 +53,18 @@ def test_gz_sgd_argument_errors_and_workspace():
     assert L.gz_sgd_forward(ctypes.byref(net), 0, None, None, None, ws, None) == -1
     assert L.gz_sgd_backward(ctypes.byref(net), 70000, None, None, None, None, ws, None) == -1
     assert L.gz_sgd_saved(ws, 4, 10, None, None) == -1
+
+
+def test_gz_adam_argument_errors():
+    L = _lib.load()
+    assert L.gz_adam_workspace_bytes() >= 8
+    t = (_lib.AdamTensor * 1)()
+    ws = ctypes.c_void_p(1)  # never dereferenced: the arguments are checked first
+    args = (ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999), ctypes.c_float(1e-8),
+            ctypes.c_float(0.0))
+    assert L.gz_adam_step(t, 0, *args, 1, ctypes.c_float(0.0), None, ws, None) == -1
+    assert L.gz_adam_step(t, _lib.GZ_ADAM_MAX_TENSORS + 1, *args, 1, ctypes.c_float(0.0), None, ws, None) == -1
+    assert L.gz_adam_step(t, 1, *args, 0, ctypes.c_float(0.0), None, ws, None) == -1  # step counts from 1
+    t[0].numel = 5  # null tensor pointers
+    assert L.gz_adam_step(t, 1, *args, 1, ctypes.c_float(0.0), None, ws, None) == -1
+    assert b"gz_adam_step" in L.gz_last_error()
