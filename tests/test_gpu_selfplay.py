@@ -267,3 +267,28 @@ def test_selfplay_device_bounded_games_compaction(planner_steps):
     recs = np.frombuffer(b.tobytes(), boards.RECORD_DTYPE)
     assert sorted(set(int(g) for g in recs["game_id"])) == list(range(40))
     assert sb["moves_played"] == len(recs) < sa["moves_played"]
+
+
+def test_selfplay_device_two_ranks_on_one_gpu(tmp_path):
+    """training.selfplay_device under torchrun with 2 ranks (gloo, both on GPU 0:
+    GZ_DIST_SAME_DEVICE) through the record exchange, each rank playing its own 24
+    game ids with the bounded game range and slot compaction, planner on: every rank
+    ends with all 48 games' rows, bit for bit those of one process playing the 48
+    (tools/dist_selfplay_check.py)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tool = os.path.join(root, "tools", "dist_selfplay_check.py")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, GZ_DIST_BACKEND="gloo", GZ_DIST_SAME_DEVICE="1")
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), tool, str(tmp_path)],
+                   env=env, check=True, timeout=240)
+    out = subprocess.run([sys.executable, tool, str(tmp_path)], check=True, timeout=180, capture_output=True,
+                         text=True).stdout
+    assert "every rank's rows == the single-process rows" in out
