@@ -137,6 +137,10 @@ class SelfPlayEngine:
         "mismatched"} (gz_selfplay_plan_gn_stats; synchronises).  check=True/False
         turns GZ_FLAG_GN_CHECK (every incremental row re-run by the full forward and
         compared bitwise) on/off for the following searches."""
+        if getattr(self, "d_slots_alt", None) is not None:
+            # a compacting engine carves the planner workspace for n_active slots, so the
+            # counters' place moves with it: they cannot be read at n_slots
+            raise ValueError("gn_stats() is not available on an engine built with game_id_end (compaction)")
         if check is not None:
             f = self.params.flags & ~_lib.GZ_FLAG_GN_CHECK
             self.params.flags = f | (_lib.GZ_FLAG_GN_CHECK if check else 0)

@@ -56,9 +56,13 @@ _HEADS = ("conv0", "policy", "value")
 def _check_net(net):
     if len(net.residual_tower) != 2:
         raise ValueError("gz_sgd: the device tower has two residual blocks (neural_network.py:98)")
-    for bn in _bns(net):
+    bns = _bns(net)
+    for bn in bns:
         if bn.momentum is None or not bn.affine:
             raise ValueError("gz_sgd: BatchNorm needs affine parameters and an exponential momentum")
+        # gz_sgd_net carries one momentum and one eps (taken from the first BatchNorm)
+        if bn.momentum != bns[0].momentum or bn.eps != bns[0].eps:
+            raise ValueError("gz_sgd: every BatchNorm must have the same momentum and eps")
     for cv in _convs(net):
         if tuple(cv.weight.shape) != (128, 128, 3, 3) or cv.bias is None:
             raise ValueError("gz_sgd: residual convs must be 128 -> 128, 3x3, with bias")
@@ -105,6 +109,9 @@ class _Tower(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dpin, dvin):
         lib = _lib.load()
+        if ctx.keep is None:
+            raise RuntimeError("gz_sgd: the device tower's saved state is released by its first backward; a second "
+                               "backward through the same graph (retain_graph=True) is not supported")
         xc, params = ctx.keep
         dpin = dpin.contiguous() if dpin is not None else torch.zeros((ctx.B, 450), device=xc.device)
         dvin = dvin.contiguous() if dvin is not None else torch.zeros((ctx.B, 225), device=xc.device)

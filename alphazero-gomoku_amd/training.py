@@ -262,8 +262,10 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
     # outbox in one or a few steps even when many games end together
     ex = gdist.RecordExchange(eng.record_cap, max(2 * eng.n_slots * eng.plies_per_step, eng.record_cap // 4), "cuda")
     want = id_hi - id_lo
-    if want != ws * n_games or not id_lo <= game_id_base < id_hi:
-        raise ValueError("selfplay_device: [id_lo, id_hi) must be the ranks' n_games-wide shares")
+    if want != ws * n_games or game_id_base != id_lo + rank * n_games:
+        raise ValueError(f"selfplay_device: rank {rank} must play ids [id_lo + rank * n_games, +n_games) of "
+                         f"[id_lo, id_hi) (got game_id_base {game_id_base}, id_lo {id_lo}, id_hi {id_hi}, "
+                         f"n_games {n_games}, {ws} ranks)")
     # rank r keeps only its own share from rank r's rows: with continuous refill its
     # slots' refill games (id + n_slots) run into rank r + 1's ids
     col = gdist.ReplayCollector(want * _MAX_GAME_RECORDS, id_lo, id_hi, "cuda", per_rank=n_games)
@@ -277,8 +279,12 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
         ex.push(eng.d_records, eng.d_counters[0:4].view(torch.int32))
         col.absorb(*ex.exchange())
         steps += 1
-        parts = [eng.d_counters.view(torch.int64)[2:3], col.games, ex.overflow, col.dropped,
-                 eng.d_counters[0:16].view(torch.int32)[2:3].to(torch.int64)]
+        # this rank's own losses (outbox overflow, engine record drops) made collective
+        # before anyone reads them: a rank that raised alone would leave the others
+        # blocked in the next exchange (col.dropped comes from the gathered chunks and
+        # is the same on every rank already)
+        lost = collective_losses([ex.overflow, eng.d_counters[0:16].view(torch.int32)[2:3]], ws)
+        parts = [eng.d_counters.view(torch.int64)[2:3], col.games, lost[0:1], col.dropped, lost[1:2]]
         if compact:
             parts.append(eng.compact().to(torch.int64))
         # the step's one host synchronisation: moves, finished games, active slots and
@@ -289,7 +295,7 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
             eng.n_active = int(c[5])
         if c[2] or c[3] or c[4]:
             raise RuntimeError(f"selfplay_device: records lost (exchange overflow {c[2]}, collector {c[3]}, "
-                               f"engine buffer {c[4]})")
+                               f"engine buffer {c[4]}; max over ranks)")
         if c[1] >= want:  # every game's first record is in
             break
         if steps >= max_steps:
@@ -310,6 +316,16 @@ def selfplay_device(n_games: int, id_lo: int, id_hi: int, num_simulations: int =
 
 
 _MAX_GAME_RECORDS = 225  # a game has at most 225 plies (one record each)
+
+
+def collective_losses(counters, ws):
+    """selfplay_device's per-rank loss counters (one-element device tensors),
+    concatenated and MAX-all-reduced over the `ws` ranks (no host synchronisation), so
+    every rank sees the same values in the step's one host read and all raise together."""
+    lost = torch.cat([c.reshape(1).to(torch.int64) for c in counters])
+    if ws > 1:
+        torch.distributed.all_reduce(lost, op=torch.distributed.ReduceOp.MAX)
+    return lost
 
 
 # ---------------------------------------------------------------- arena (training.py:221-270)

@@ -33,7 +33,11 @@ run as labelled secondaries, the prior-elided MCTS-only rate (moves identical
 without the priors), and the CPU baseline: the C oracle + torch-fp32 forwards
 ("port") on the host cores -- P processes x 1 thread, 1 process x P threads, and
 config 1.
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torchrun.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 either under torchrun
+(one rank per GPU from its env) or self-launched: without WORLD_SIZE in the
+environment, bench.py starts `python -m torch.distributed.run --nproc-per-node N`
+as a child process and relays rank 0's line.  The line's `distributed` block names
+the backend, the world size and every rank's device (PCI address).
 """
 import argparse
 import json
@@ -361,6 +365,101 @@ def config5(games, sims, seed, iterations=2):
                          f"{iterations} iterations")}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n):
+    """`bench.py --gpus N` (N > 1) started without torchrun's environment: run the N
+    ranks as ONE child process, `python -m torch.distributed.run --nproc-per-node N`
+    on 127.0.0.1, before this process touches the GPU (no exec), relay rank 0's
+    JSON line to stdout and return the child's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("self-launch: " + " ".join(cmd))
+    env = dict(os.environ, GZ_BENCH_SELF_LAUNCHED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    line = None
+    for raw in proc.stdout:  # rank 0's JSON line; anything else goes to stderr
+        s = raw.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        elif s:
+            log(s)
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        log("self-launch: the ranks exited 0 without a JSON line")
+        rc = 1
+    return rc
+
+
+def rank_devices(ws, stub=False):
+    """Per rank: local rank, the device it ran on and that device's PCI address and
+    name, gathered to every rank (all_gather_object) -- so the line shows that the
+    collective backend saw N ranks on N devices."""
+    me = {"rank": dist.get_rank() if ws > 1 else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "host": os.uname().nodename}
+    if stub:
+        me["device"] = "cpu"
+    else:
+        d = torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(d)
+        me.update({"device": d, "name": p.name, "arch": p.gcnArchName,
+                   "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"})
+    if ws == 1:
+        return [me]
+    out = [None] * ws
+    dist.all_gather_object(out, me)
+    return out
+
+
+def distributed_info(ws, stub=False):
+    ranks = rank_devices(ws, stub)
+    return {"backend": dist.get_backend() if ws > 1 else None, "world_size": ws,
+            "launch": ("self-launched torch.distributed.run" if os.environ.get("GZ_BENCH_SELF_LAUNCHED")
+                       else ("torchrun (external)" if ws > 1 else "single process")),
+            "distinct_devices": len({(r["host"], r.get("pci_bus_id", r["device"])) for r in ranks}),
+            "ranks": ranks}
+
+
+def stub_main(args):
+    """--stub: the multi-rank plumbing alone, no GPU (CPU tests): rendezvous, the
+    per-rank device report, EXACTLY `steps` timed steps (a step = one all-reduce)
+    bracketed by barriers, max over ranks, rank 0's JSON line."""
+    rank, ws = gdist.init_from_env(backend=os.environ.get("GZ_DIST_BACKEND", "gloo"))
+    info = distributed_info(ws, stub=True)
+    x = torch.ones(1024)
+
+    def step():
+        if ws > 1:
+            dist.all_reduce(x)
+    for _ in range(args.warmup):
+        step()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if ws > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if ws > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC + " [stub: multi-rank plumbing only, no GPU work]", "value": 0.0,
+                          "unit": "moves/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(float(el.item()) / max(1, args.steps) * 1e3, 3), "stub": True,
+                          "distributed": info}), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
 def roofline_of(m, precision):
     mean_leaves = float(np.mean(m["leaves"]))
     mean_pv_s = float(np.mean(m["pv_ms"])) / 1e3
@@ -469,8 +568,14 @@ def main():
                          "per iteration (0 = skip)")
     ap.add_argument("--fp32-steps", type=int, default=4,
                     help="N = 1 secondary: the exact-fp32 PV forward timed over this many steps (0 = skip)")
+    ap.add_argument("--stub", action="store_true",
+                    help="multi-rank plumbing only (rendezvous, device report, timing, JSON line) without a GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
+    if args.stub:
+        return stub_main(args)
     rank, ws = gdist.init_from_env()
     pool = None
     procs = 0
@@ -484,6 +589,7 @@ def main():
     torch.cuda.set_device(gdist.local_device())
     if ws != args.gpus and rank == 0:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; reporting n_gpus={ws}")
+    dinfo = distributed_info(ws)
 
     sd = weights.init_state_dict(0)
     w = PVWeights(weights.pack_pv_weights(sd), precision=args.pv_precision)
@@ -557,6 +663,7 @@ def main():
                            "share": round(m["mcts"] / m["moves"], 4) if m["moves"] else None,
                            "note": "plies decided by a search (SURVEY 8d): value counts every ply, incl. the opening "
                                    "plies 0-5 that _opening_move plays without one (ai_agent.py:138-166)"},
+            "distributed": dinfo,
         }
     if ex is not None and rank == 0:
         out["record_exchange"] = {"chunk_records": ex.chunk, "bytes_per_rank_per_step": ex.chunk * ex.item,

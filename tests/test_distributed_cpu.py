@@ -261,3 +261,54 @@ def test_training_main_ranks_stay_in_step(tmp_path):
     # rank 0's losses: improve at iterations 1-2, then 3 without improvement -> stop after 5
     assert res[0][0] == res[1][0] == 5
     assert res[0][1] == res[1][1], (res[0][1], res[1][1])
+
+
+def test_bench_self_launches_n_ranks_stub():
+    """`bench.py --gpus 2` without torchrun's env starts the 2 ranks itself (a child
+    torch.distributed.run) and relays rank 0's line: n_gpus 2, the backend and both
+    ranks' devices (--stub: the plumbing without GPU work, gloo)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GZ_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--stub", "--steps", "3",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["stub"] is True
+    d = out["distributed"]
+    assert d["backend"] == "gloo" and d["world_size"] == 2
+    assert d["launch"] == "self-launched torch.distributed.run"
+    assert [x["rank"] for x in d["ranks"]] == [0, 1] and [x["local_rank"] for x in d["ranks"]] == [0, 1]
+
+
+def _loss_worker(rank, ws, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    import training
+    # only rank 1 lost records (its outbox overflowed); rank 0 dropped one in its engine
+    overflow = torch.tensor([7 if rank == 1 else 0])
+    drops = torch.tensor([1 if rank == 0 else 0])
+    lost = training.collective_losses([overflow, drops], ws)
+    q.put((rank, lost.tolist()))
+    dist.destroy_process_group()
+
+
+def test_selfplay_loss_counters_are_collective():
+    """a loss counter that only one rank sees must reach every rank in the
+    same step (else that rank raises alone and the others block in the next all-gather)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_loss_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert got[0] == got[1] == [7, 1]
