@@ -125,7 +125,7 @@ struct TreeArgs {
     const _Float16* maps;
     _Float16* patches;
     float* hbuf;
-    int32_t* tiles;  // pv_sib_kernel: 16-row MFMA tiles executed per residual conv [children, grandchildren]
+    int32_t* tiles;  // pv_sib_kernel: 16-row MFMA tile-taps executed by the residual convs [children, grandchildren]
     const float* pres;  // pv_delta_kernel: the roots' pre-BN accumulator maps (4 x PV_PRE_FLOATS per root)
 };
 
@@ -576,7 +576,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
     constexpr bool SKIP = LAYER == 1;
     SibPos<NMAX> tp;
     const int nt = sib_positions<NMAX, G>(U, ng, ro, lane, mh, tp);
-    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);  // the executed tiles, one count per M half
+    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, 9 * nt);  // the executed tile-taps, one count per M half
     int ctr[NMAX];
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
@@ -669,7 +669,7 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     const int nt = T - t0 < T0 ? (T - t0 > 0 ? T - t0 : 0) : T0;
     TilePos<NMAX> tp;
     tile_positions<NMAX, 6>(rows, t0, lane, tp);
-    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);
+    if (tiles && np == 0 && lane == 0) atomicAdd(tiles, 9 * nt);
     int ctr[NMAX];
     tile_centres<NMAX, Win<6>>(tp, cr, cc, ctr);
     f32x4 acc[2][NMAX];
@@ -1405,7 +1405,7 @@ __device__ __forceinline__ void dl_pass(const _Float16* in, float* acc, const Dl
     const int q = lane >> 4, li = lane & 15;
     {
         const int nt = (gi.start[G] + 15) >> 4;
-        if (tiles && np == 0 && lane == 0) atomicAdd(tiles, nt);
+        if (tiles && np == 0 && lane == 0) atomicAdd(tiles, 9 * nt);
         int pr[NMAX], pc[NMAX], ob[NMAX], ow[NMAX];
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
@@ -1735,6 +1735,11 @@ __global__ __launch_bounds__(NTS, 1) void pv_delta_kernel(TreeArgs A, _Float16* 
 }  // namespace
 
 extern "C" void gz_internal_set_error(const char* msg);
+extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
+                                      const int32_t* d_pslot, const int32_t* d_cinfo, const _Float16* d_maps,
+                                      const float* d_pres, _Float16* d_patches, float* d_hbuf, _Float16* d_scratch,
+                                      int32_t* d_tiles, const int32_t* d_children, const int32_t* d_nchildren,
+                                      int grid, void* stream);
 
 // Launches of the incremental forward's own kernels (called by gz_pv_forward_tree in
 // gz_pvnet.hip, which runs the full kernel on the root and full lists in between).
@@ -1777,9 +1782,11 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          int delta, const float* d_pres, void* stream) {
     TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles, d_pres};
     hipStream_t s = (hipStream_t)stream;
-    if (delta)
-        pv_delta_kernel<<<grid, NTS, 0, s>>>(A, d_scratch, d_children, d_nchildren);
-    else
+    if (delta) {
+        const int rc = gz_internal_tree_delta(d_weights, d_boards, d_meta, d_pslot, d_cinfo, d_maps, d_pres, d_patches,
+                                              d_hbuf, d_scratch, d_tiles, d_children, d_nchildren, grid, stream);
+        if (rc) return rc;
+    } else
         pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_children, d_nchildren);
     pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();

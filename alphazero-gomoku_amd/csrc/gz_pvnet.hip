@@ -975,7 +975,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr int PV_PATCH_HALVES = 164 * 256;  // a root child's recomputed squares (gz_pvinc.hip)
-constexpr size_t SIB_SCRATCH_HALVES = 6 * (size_t)PV_PATCH_HALVES;  // per workgroup of pv_sib_kernel
+constexpr size_t SIB_SCRATCH_HALVES = 12 * (size_t)PV_PATCH_HALVES;  // per workgroup: pv_sib_kernel 6, pv_dg_kernel 12
 inline int32_t patch_cap_of(int32_t root_cap) { return 16 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;
@@ -983,7 +983,7 @@ struct TreeWs {
     _Float16* maps;
     float* pres;        // the roots' pre-BN accumulators (pv_delta_kernel)
     _Float16* patches;
-    _Float16* scratch;  // pv_sib_kernel / pv_delta_kernel: 6 patch-sized areas per workgroup
+    _Float16* scratch;  // pv_sib_kernel / pv_dg_kernel: 12 patch-sized areas per workgroup
 };
 TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);

@@ -62,7 +62,7 @@ METRIC = "self-play moves/sec at 200 sims/move, 15x15 board, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2 dense peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (spec)
 PV_FLOP = 2 * weights.PV_MACS  # 267.38 MFLOP per board
-TILE_FLOP = 2 * 16 * 128 * 1152  # one 16-row tile of a residual 3x3 conv (fp32-equivalent)
+TILETAP_FLOP = 2 * 16 * 128 * 128  # one 16-row tile x one tap of a residual 3x3 conv (fp32-equivalent)
 # per incremental node besides its residual tiles: conv0 (one 16-row tile, K 27), the
 # 1x1 head convs on the radius-5 square (121 rows unclipped) and the FC heads
 INC_EXTRA_FLOP = 2 * (16 * 128 * 27 + 121 * 128 * 3 + 450 * 225 + 225 * 64 + 64)
@@ -275,7 +275,7 @@ def measure(eng, steps, warmup, burn_in, ws, ex=None):
             tst = torch.zeros(8, dtype=torch.int32, device="cuda")
             _lib.check(eng.lib.gz_pv_tree_stats(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst), stream()),
                        "gz_pv_tree_stats")
-            # [6:8] = the residual-conv MFMA tiles the incremental kernels executed
+            # [6:8] = the residual-conv MFMA tile-taps the incremental kernels executed
             _lib.check(eng.lib.gz_pv_tree_exec_tiles(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tst[6:]), stream()),
                        "gz_pv_tree_exec_tiles")
         if ex is not None:
@@ -470,13 +470,13 @@ def roofline_of(m, precision):
         # roots seen, roots w/ maps, children, full, grandchildren, patch slots
         t = np.mean(np.array(m["tree"], dtype=np.float64), axis=0)
         # executed MFMA FLOP (fp32-equivalent): full-forward nodes x 267.38 MFLOP + the
-        # residual-conv tiles the incremental kernels counted x 16 rows x 128 x 1152 x 2
+        # residual-conv tile-taps the incremental kernels counted x 16 rows x 128 x 128 x 2
         # + per incremental node its conv0 tile, 1x1 heads (radius-5 square, unclipped:
-        # an upper bound) and FC heads; if the kernels counted no tiles (GZ_PVINC_SIB=0),
-        # the model of tree_exec_flops
+        # an upper bound) and FC heads; if the kernels counted nothing, the model of
+        # tree_exec_flops
         tiles = float(t[6] + t[7])
         if tiles > 0:
-            executed = (t[1] + t[3]) * PV_FLOP + tiles * TILE_FLOP + (t[2] + t[4]) * INC_EXTRA_FLOP
+            executed = (t[1] + t[3]) * PV_FLOP + tiles * TILETAP_FLOP + (t[2] + t[4]) * INC_EXTRA_FLOP
         else:
             executed = m["exec_per_board"] * mean_leaves
         achieved = executed / mean_pv_s / 1e12 if mean_pv_s > 0 else 0.0
@@ -486,7 +486,7 @@ def roofline_of(m, precision):
                 "child_share": round(float((t[2] + t[4]) / max(1.0, mean_leaves)), 4),
                 "executed_flop_per_launch": round(float(executed), 0),
                 "algorithmic_tflops_full_forward_equivalent": round(algorithmic, 3),
-                "executed_tiles_per_launch": round(tiles, 1),
+                "executed_tile_taps_per_launch": round(tiles, 1),
                 "executed_mflop_per_child": round((executed - (t[1] + t[3]) * PV_FLOP)
                                                   / max(1.0, t[2] + t[4]) / 1e6, 2),
                 "note": ("achieved = MFMA work executed / kernel time: roots and untagged nodes the full 267.38 "

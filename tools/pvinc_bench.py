@@ -75,6 +75,14 @@ def main():
         import ctypes
         lib.gz_pvinc_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
         st = np.zeros(34, np.uint64)
+    dgst = hasattr(lib, "gz_pvdg_stamps_read")
+    if dgst:  # -DGZ_PVDG_STAMPS build (make -C tools variant VAR=dgstamps EXTRA=-DGZ_PVDG_STAMPS)
+        import ctypes
+        lib.gz_pvdg_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        dst = np.zeros(17, np.uint64)
+    dg_names = ["chunk start (units, conv0, y1 rows)", "rows of the next pass", "y1 k-loop", "x1 k-loop",
+                "y2 k-loop", "x2 k-loop", "barrier after the k-loop", "y1 epilogue", "x1 epilogue", "y2 epilogue",
+                "x2 epilogue + heads", "store drain + barrier", "records", "fill + barrier"]
     outs = {}
     tiles = torch.zeros(2, dtype=torch.int32, device="cuda")
     sib_names = ["select nodes", "window fills (not overlapped)", "conv0", "y1 k-loop", "y1 barrier + next fill",
@@ -92,8 +100,19 @@ def main():
                                                    (eng.d_prior, 225))]
         _lib.check(lib.gz_pv_tree_exec_tiles(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tiles), stream()), "tiles")
         t2 = [int(x) for x in tiles.cpu()]
-        print(f"  executed 16-row x 3x3 tiles: children {t2[0]} ({t2[0] * 9 / max(1, st_kids):.1f} tile-taps per "
-              f"child), grandchildren {t2[1]}", flush=True)
+        print(f"  executed 16-row tile-taps: children {t2[0]} ({t2[0] / max(1, st_kids):.1f} per child), "
+              f"grandchildren {t2[1]}", flush=True)
+        if dgst and m == "delta":
+            lib.gz_pvdg_stamps_read(dst.ctypes.data, 1)
+            run()
+            torch.cuda.synchronize()
+            lib.gz_pvdg_stamps_read(dst.ctypes.data, 0)
+            kids = max(1, int(dst[16]))
+            vals = [int(x) for x in dst[: len(dg_names)]]
+            tot = sum(vals)
+            print(f"  stamps, workgroup 0 children (pv_dg_kernel): {kids} nodes, {tot / kids:.0f} ticks per node")
+            for i, x in enumerate(dg_names):
+                print(f"    {x:36s} {vals[i] / kids:9.0f}  {vals[i] / max(1, tot) * 100:5.1f}%")
         if stamps:
             lib.gz_pvinc_stamps_read(st.ctypes.data, 1)
             run()
