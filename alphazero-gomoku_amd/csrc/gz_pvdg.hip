@@ -81,7 +81,7 @@ struct K {
     // zero slot (the last), rounded to 16 so that a channel group's plane starts at bank 0
     __host__ __device__ static constexpr int npos(int L) { return dgk_npos(L); }
     static constexpr int MAXNPOS = 112;            // npos(2) = max over the layers (static_assert below)
-    static constexpr int NMAX = 11;                // output tiles of a pass at most (y2: 2 x 81 rows)
+    static constexpr int NMAX = 12;                // output tiles of a pass at most (y2: 2 x 81 rows in 11)
     static constexpr int ROWS = NMAX * 16;         // row-table entries per pass
     static constexpr int GB = 2;                   // epilogue: tiles per load group
     static constexpr int WPS = 2;                  // workgroups per CU
@@ -363,6 +363,11 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
                 }
                 if (h == 1) ad[m] = addr(tap + 1, ri[m]);  // tile m is read for this tap: the next tap's address
                 if ((tm >> m) & 1u) {
+#ifdef GZ_PVDG_PROBE_M  // (wrong results) no MFMAs: the loop's skeleton (reads kept alive)
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; k2++) c[0][m][0] += (float)fh[pm][k2][0] + (float)fl[pm][k2][0] + (float)b[2 * h + k2][0][0][0];
+                    continue;
+#endif
 #pragma unroll
                     for (int k2 = 0; k2 < 2; k2++) {
                         const int sl = 2 * h + k2;
@@ -418,8 +423,8 @@ __device__ __forceinline__ void put_hl_lds(_Float16* p, int plane_halves, const 
 //   child = relu(z + s * acc + D_skip),  root = relu(z),  D = child - root
 // into the node's D square of map L + 1 (its patch: the child value); x2 reduces the
 // child values into the 1x1 heads' partial sums (hpart, per wave) instead.  Rows in
-// groups of GB tiles, loads two groups ahead; mid() (the next pass's fill, when it does
-// not read this pass's squares) runs once the first two groups' loads are issued, so
+// groups of GB tiles, loads a group ahead; mid() (the next pass's fill, when it does
+// not read this pass's squares) runs once the first group's loads are issued, so
 // that only later loads queue behind its LDS-DMA.
 template <int L, class Mid>
 __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const uint32_t* rt, const float* __restrict__ W,
@@ -427,7 +432,7 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
     constexpr int RO = L + 2, SO = dg_so(L), SSO = SO * SO;
     constexpr bool SKIP = L == 1 || L == 3;
     constexpr int RS = L == 1 ? 1 : 3, SK = 2 * RS + 1, SSK = SK * SK;
-    constexpr int GB = K::GB, NGRP = K::NMAX / GB, ST = 3;
+    constexpr int GB = K::GB, NGRP = (K::NMAX + GB - 1) / GB, ST = 2;
     float* hpart = (float*)(lds + K::HP);
     const int q = lane >> 4, li = lane & 15;
     const float* cst = (const float*)(lds + K::CST);  // staged at kernel start
@@ -449,6 +454,7 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
 #pragma unroll
         for (int j = 0; j < GB; j++) {
             const int m = grp * GB + j;
+            if (m >= K::NMAX) break;  // (an odd NMAX: the last group's second tile)
             const uint32_t e = rt[m * 16 + li];
             ent[st][j] = e;
             const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
@@ -470,16 +476,16 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
         }
     };
     loads(0, 0);
-    if (GB < nt) loads(1, 1);
     mid();
 #pragma unroll
     for (int grp = 0; grp < NGRP; grp++) {
         if (grp * GB >= nt) break;
         const int st = grp % ST;
-        if ((grp + 2) * GB < nt) loads(grp + 2, (grp + 2) % ST);
+        if ((grp + ST - 1) * GB < nt) loads(grp + ST - 1, (grp + ST - 1) % ST);
 #pragma unroll
         for (int j = 0; j < GB; j++) {
             const int m = grp * GB + j;
+            if (m >= K::NMAX) break;
             const uint32_t e = ent[st][j];
             const bool v = (e >> 21) & 1u;
             const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
@@ -532,7 +538,7 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
 
 // a node's head-conv record: the radius-5 square from the partials (bias + the 4
 // waves' sums), everything else the root's record (rec: this thread's entries of the
-// root's record, loaded by dg_record_load before the epilogue)
+// root's record, dg_record_load)
 constexpr int REC_K = (HSTRIDE + NTD - 1) / NTD;
 __device__ __forceinline__ void dg_record_load(const DgUnit& u, const float* __restrict__ hbuf, float (&rec)[REC_K],
                                                int tid) {
@@ -649,15 +655,34 @@ __device__ __forceinline__ void dg_conv0(char* lds, const _Float16* col, const D
         wt[n] = *(const f32x4*)(W + C0_T + ch0);
     }
     _Float16* in = (_Float16*)(lds + K::IN);
-#pragma unroll 1
-    for (int g = 0; g < ng; g++) {
+    // every node's root x0 values first (one round of latency for the chunk), then the MFMAs
+    h4 rxh[K::C][2], rxl[K::C][2];
+#pragma unroll
+    for (int g = 0; g < K::C; g++) {
+        const DgUnit& u = U[g < ng ? g : 0];
+        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
+        const int r0 = cr > 0 ? cr - 1 : 0, r1 = cr < BN - 1 ? cr + 1 : BN - 1;
+        const int c0 = cc > 0 ? cc - 1 : 0, c1 = cc < BN - 1 ? cc + 1 : BN - 1, wr = c1 - c0 + 1;
+        const bool rowok = li < (r1 - r0 + 1) * wr;
+        const int pr = rowok ? r0 + li / wr : cr, pc = rowok ? c0 + li % wr : cc, pos = pr * BN + pc;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            const int ch0 = (2 * np + n) * 16 + 4 * q;
+            const _Float16* rp = u.gm + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);
+            rxh[g][n] = gld<h4>(rp);
+            rxl[g][n] = gld<h4>(rp + PV_MAP_PLANE);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < K::C; g++) {
+        if (g >= ng) break;
         const h8 a = *(const h8*)(col + g * 512 + li * 32 + 8 * q);
         const DgUnit& u = U[g];
         const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
         const int r0 = cr > 0 ? cr - 1 : 0, r1 = cr < BN - 1 ? cr + 1 : BN - 1;
         const int c0 = cc > 0 ? cc - 1 : 0, c1 = cc < BN - 1 ? cc + 1 : BN - 1, wr = c1 - c0 + 1;
         const bool rowok = li < (r1 - r0 + 1) * wr;
-        const int pr = rowok ? r0 + li / wr : cr, pc = rowok ? c0 + li % wr : cc, pos = pr * BN + pc;
+        const int pr = rowok ? r0 + li / wr : cr, pc = rowok ? c0 + li % wr : cc;
         const int idx = (pr - cr + 1) * 3 + (pc - cc + 1);
 #pragma unroll
         for (int n = 0; n < 2; n++) {
@@ -666,8 +691,7 @@ __device__ __forceinline__ void dg_conv0(char* lds, const _Float16* col, const D
             acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a, acc, 0, 0, 0);
             if (rowok) {
-                const _Float16* rp = u.gm + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);  // the root's x0
-                const h4 rh = gld<h4>(rp), rl = gld<h4>(rp + PV_MAP_PLANE);
+                const h4 rh = rxh[g][n], rl = rxl[g][n];  // the root's x0
                 f32x4 y, d;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
@@ -839,8 +863,6 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             auto mid = [&]() {
                 if (pre) fill();
             };
-            float rec[REC_K];  // x2: the root's record entries of this thread (K::g(3) == 1 node per pass)
-            if (L == 3) dg_record_load(U[u0], A.hbuf, rec, t);
             if (L == 0) dg_epilogue<0>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
             else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
             else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
@@ -851,7 +873,11 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // the squares are stored; hpart is complete
             st(11);
-            if (L == 3) dg_record(U[u0], 0, (const float*)(lds + K::CST) + 896, A.hbuf, (const float*)(lds + K::HP), rec, t);
+            if (L == 3) {  // (the root's record entries loaded here: held across the epilogue they were spilled)
+                float rec[REC_K];
+                dg_record_load(U[u0], A.hbuf, rec, t);
+                dg_record(U[u0], 0, (const float*)(lds + K::CST) + 896, A.hbuf, (const float*)(lds + K::HP), rec, t);
+            }
             st(12);
             if (more && !pre) {
                 fill();
