@@ -893,7 +893,7 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
 
 extern "C" void gz_internal_set_error(const char* msg);
 
-// the root children (list, list_count entries) of gz_pv_forward_tree_mode(GZ_TREE_DELTA)
+// the root children (list, list_count entries) of gz_pv_forward_tree
 // through pv_dg_kernel; scratch: 12 patch-sized areas per CU (grid = CUs)
 extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                       const int32_t* d_pslot, const int32_t* d_cinfo, const _Float16* d_maps,

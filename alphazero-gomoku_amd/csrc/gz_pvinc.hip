@@ -1,30 +1,25 @@
-// gz_pvinc.hip -- incremental policy-value forward of a search's root children and
-// their children (AlphaZeroGomokuNet, neural_network.py:74-159, f16x3 precision).
+// gz_pvinc.hip -- incremental policy-value forward of a search's grandchildren, and
+// the tree forward's classification kernels (AlphaZeroGomokuNet, neural_network.py:
+// 74-159, f16x3 precision).
 //
 // MCTSNode.__init__ runs GomokuModel.predict for every new node (ai_agent.py:
 // 522-523).  A root child differs from the root by one stone at cell m, so in
 // layer L of the tower (x0 = conv0, y1, x1, y2, x2) only the positions within
 // Chebyshev radius L+1 of m can differ from the root's maps: 3x3, 5x5, 7x7, 9x9,
 // 11x11 squares (clipped to the board) -- about 31 % of the 4 x 225 positions of
-// the residual convs.  The root is evaluated by the full kernel, which also
-// stores its x0, y1, x1, y2 maps (gz_pvnet.hip, pv_kernel_f16x3<.., true>) and, for
-// the delta mode, its pre-BN accumulators.  Two kernels compute the root children:
+// the residual convs.  The root is evaluated by the full kernel, which also stores
+// its x0, y1, x1, y2 maps and its pre-BN accumulators (gz_pvnet.hip,
+// pv_kernel_f16x3<.., true>).  The root children are computed as a delta of the
+// root's accumulators by pv_dg_kernel (gz_pvdg.hip); a child with children of its
+// own also stores its recomputed squares (its "patch").
 //
-// * pv_sib_kernel (tree mode "exact"): every recomputed position takes the same
-//   products in the same order as the full kernel (k = tap*128 + cin in 32-deep MFMA
-//   k-steps, hi*hi, w_lo*a_hi, w_hi*a_lo; the same epilogue, the same hi/lo split,
-//   the same head-conv partial sums per wave), and an MFMA output element depends
-//   only on its own row and column operands, so the child's logits, value, softmax
-//   and prior are bit for bit those of a full forward of the child's board
-//   (tests/test_gpu_pvinc.py).  Windows of the root's maps around m are filled into
-//   LDS, the child's own squares overlaid.
-// * pv_delta_kernel (tree mode "delta"): the root's accumulators plus the
-//   convolution of the child's input differences (below; tests/test_gpu_pvdelta.py).
-//
-// Grandchildren (a child of a root child, one more stone at m2): the parent also
-// stores its recomputed squares (its "patch"), and the grandchild's windows are the
-// root's maps overlaid with the parent's patch around the parent's stone; the rest
-// is the same computation around m2 (pv_sib_kernel<true>, both modes).
+// Grandchildren (a child of a root child, one more stone at m2): pv_sib_kernel below.
+// Their windows are the root's maps overlaid with the parent's patch around the
+// parent's stone; the recomputed positions (radius L+1 around m2) take the full
+// kernel's products in the full kernel's order (k = tap*128 + cin in 32-deep MFMA
+// k-steps, hi*hi, w_lo*a_hi, w_hi*a_lo; the same epilogue, hi/lo split and head-conv
+// partial sums per wave).  Given the parent's patch they are the full forward's
+// values; the patch itself carries the delta's rounding (tests/test_gpu_pvinc.py).
 #include <hip/hip_runtime.h>
 #include <type_traits>
 
@@ -44,7 +39,7 @@ using namespace gzc;
 // Phase stamps (tools/pvinc_bench.py only): -DGZ_PVINC_STAMPS accumulates s_memtime
 // deltas of workgroup 0 / thread 0 per phase (vector atomics); compiled out otherwise.
 #ifdef GZ_PVINC_STAMPS
-__device__ unsigned long long gz_pvinc_stamps[32];  // [0, 16): pv_sib_kernel, [16, 32): pv_delta_kernel
+__device__ unsigned long long gz_pvinc_stamps[32];  // [0, 16): pv_sib_kernel
 __device__ unsigned long long gz_pvinc_stamps_n[2];
 #endif
 constexpr int P_X0 = 49, P_Y1 = 81, P_X1 = 121, P_Y2 = 169;  // window positions, radius 3..6
@@ -125,8 +120,7 @@ struct TreeArgs {
     const _Float16* maps;
     _Float16* patches;
     float* hbuf;
-    int32_t* tiles;  // pv_sib_kernel: 16-row MFMA tile-taps executed by the residual convs [children, grandchildren]
-    const float* pres;  // pv_delta_kernel: the roots' pre-BN accumulator maps (4 x PV_PRE_FLOATS per root)
+    int32_t* tiles;  // 16-row MFMA tile-taps executed by the residual convs [children, grandchildren]
 };
 
 // ============================================================ sibling-batched incremental forward
@@ -198,7 +192,7 @@ struct MapLoc {
     const _Float16* base;
     int cs, lo;
 };
-template <int MAP, bool GC>
+template <int MAP>
 __device__ __forceinline__ MapLoc map_loc(const SibUnit& u, int pr, int pc) {
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
@@ -206,7 +200,7 @@ __device__ __forceinline__ MapLoc map_loc(const SibUnit& u, int pr, int pc) {
     L.base = u.gm + MAP * PV_MAP_HALVES + (pr * BN + pc) * 8;
     L.cs = 256 * 8;
     L.lo = PV_MAP_PLANE;
-    if (GC) {
+    {  // the parent's square
         const int r1 = u.pcell / BN, c1 = u.pcell - (u.pcell / BN) * BN;
         if (iabs(pr - r1) <= rc && iabs(pc - c1) <= rc) {
             L.base = u.par + PATCH_OFF[MAP] + ((pr - r1 + rc) * S + (pc - c1 + rc)) * 8;
@@ -257,7 +251,7 @@ __device__ __forceinline__ SibU sib_uniform(const SibUnit& u) {
     return s;
 }
 
-template <int MAP, bool GC>
+template <int MAP>
 __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, int ng, int tid) {
     constexpr int R = MAP + 3, Wd = 2 * R + 1, P = Wd * Wd, PER = 2 * 16 * P;
     constexpr int rc = MAP + 1, S = 2 * rc + 1, SS = S * S;
@@ -286,7 +280,7 @@ __device__ __forceinline__ void sib_fill(char* lds, const SibUnit* U, int u0, in
             src = u.own + PATCH_OFF[MAP] + ((dr + rc) * S + (dc + rc)) * 8;
             stride = SS * 8;
         }
-        if (GC && on && !own && iabs(pr - u.r1) <= rc && iabs(pc - u.c1) <= rc) {
+        if (on && !own && iabs(pr - u.r1) <= rc && iabs(pc - u.c1) <= rc) {
             src = u.par + PATCH_OFF[MAP] + ((pr - u.r1 + rc) * S + (pc - u.c1 + rc)) * 8;
             stride = SS * 8;
         }
@@ -568,7 +562,7 @@ __device__ __forceinline__ int sib_positions(const SibUnit* U, int ng, int ro, i
 // One map layer (LAYER 0 = y1: X0 r3 windows -> y1 r2; 1 = x1: Y1 r4 -> x1 r3, + x0;
 // 2 = y2: X1 r5 -> y2 r4) over units [u0, u0 + ng): the k-loop, then the epilogue into
 // each node's own square (global)
-template <int LAYER, int NMAX, int G, bool GC, class Mid>
+template <int LAYER, int NMAX, int G, class Mid>
 __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int ng, const float* __restrict__ W, int np,
                                               int mh, int lane, int32_t* tiles, SibStamp<>& st, int si, Mid&& mid) {
     constexpr int R = LAYER + 3, Wd = 2 * R + 1, P = Wd * Wd, ro = R - 1;
@@ -595,7 +589,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
     auto skip_loads = [&]() {
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
-            const MapLoc L = map_loc<0, GC>(U[tp.g[m]], tp.pr[m], tp.pc[m]);
+            const MapLoc L = map_loc<0>(U[tp.g[m]], tp.pr[m], tp.pc[m]);
 #pragma unroll
             for (int n = 0; n < 2; n++) {
                 const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
@@ -658,7 +652,7 @@ __device__ __forceinline__ void sib_map_layer(char* lds, const SibUnit* U, int n
 // x2 + the 1x1 head convs for one unit (Y2 r6 window at LDS 0): wave np = n-tile pair
 // over all the unit's M tiles; the head partial sums in tree_node's per-lane chain
 // (n-tile 2np then 2np+1, channels in order) and cross-lane order, to hpart
-template <bool GC, class Mid>
+template <class Mid>
 __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, const float* __restrict__ W, int np,
                                                int mh, int lane, float* __restrict__ hpart, int32_t* tiles,
                                                SibStamp<>& st, int si, Mid&& mid) {
@@ -683,7 +677,7 @@ __device__ __forceinline__ void sib_head_layer(char* lds, const SibUnit& u, cons
     auto skip_loads = [&]() {
 #pragma unroll
         for (int m = 0; m < NMAX; m++) {
-            const MapLoc L = map_loc<2, GC>(u, tp.pr[m], tp.pc[m]);
+            const MapLoc L = map_loc<2>(u, tp.pr[m], tp.pc[m]);
 #pragma unroll
             for (int n = 0; n < 2; n++) {
                 const int ch0 = (2 * np + n) * 16 + 4 * (lane >> 4);
@@ -787,10 +781,8 @@ __device__ __forceinline__ void sib_record(const UT& u, const float* __restrict_
     }
 }
 
-// list: the root children (GC = false, tree_lists_kernel) or the grandchildren (GC =
-// true, tree_grand_order_kernel), list_count entries.  scratch: SIB_G patch-sized
-// areas per workgroup.
-template <bool GC>
+// list: the grandchildren (tree_grand_order_kernel), list_count entries.  scratch:
+// SIB_G patch-sized areas per workgroup.
 __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __restrict__ scratch, int n,
                                                        const int32_t* __restrict__ d_count,
                                                        const int32_t* __restrict__ list,
@@ -812,7 +804,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
     const float* W = A.W;
-    int32_t* tiles = A.tiles ? A.tiles + (GC ? 1 : 0) : nullptr;
+    int32_t* tiles = A.tiles ? A.tiles + 1 : nullptr;
     SibStamp<> st;
     // the units of the chunk at pos_ (wave 0, one lane per node)
     auto build = [&](SibUnit* Ud, int pos_, int ng_) {
@@ -826,18 +818,11 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
             u.cell = ci & 0xff;
             u.base = A.meta[b];
             u.own = myscr + (size_t)lane * PATCH_HALVES;
-            u.par = nullptr;
-            u.pcell = 0;
 #pragma unroll
             for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
-            if (GC) {  // the parent (a root child with a patch slot)
-                const int pa = u.base;
-                u.pcell = A.cinfo[pa] & 0xff;
-                u.par = A.patches + (size_t)A.pslot[pa] * PATCH_HALVES;
-            } else {
-                const int ps = A.pslot[b];
-                if (ps >= 0) u.own = A.patches + (size_t)ps * PATCH_HALVES;  // it has grandchildren: its patch
-            }
+            const int pa = u.base;  // the parent: a root child with a patch slot
+            u.pcell = A.cinfo[pa] & 0xff;
+            u.par = A.patches + (size_t)A.pslot[pa] * PATCH_HALVES;
             Ud[lane] = u;
         }
     };
@@ -872,14 +857,14 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
             }
         };
         auto fill = [&](int L, int u0, int g, int t) {
-            if (L == 1) sib_fill<1, GC>(lds, U, u0, g, t);
-            else if (L == 2) sib_fill<2, GC>(lds, U, u0, g, t);
-            else if (L == 3) sib_fill<3, GC>(lds, U, u0, g, t);
+            if (L == 1) sib_fill<1>(lds, U, u0, g, t);
+            else if (L == 2) sib_fill<2>(lds, U, u0, g, t);
+            else if (L == 3) sib_fill<3>(lds, U, u0, g, t);
         };
         {
             int t = tid;
             asm volatile("" : "+v"(t));
-            sib_fill<0, GC>(lds, U, 0, ng, t);
+            sib_fill<0>(lds, U, 0, ng, t);
             sib_col((_Float16*)hpart, U, ng, t);
             __syncthreads();  // drains the fill; conv0 then overwrites the nodes' own x0 squares
             st(1);
@@ -914,11 +899,11 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                 if (pre) fill(L2, v0, g2, t);
             };
             if (L == 0) {
-                sib_map_layer<0, sib_tiles(10), SIB_G, GC>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
+                sib_map_layer<0, sib_tiles(10), SIB_G>(lds, U, g, Wp, np, mh, t & 63, tiles, st, 3, mid);
             } else if (L == 1) {
-                sib_map_layer<1, sib_tiles(10), 3, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 6, mid);
+                sib_map_layer<1, sib_tiles(10), 3>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 6, mid);
             } else if (L == 2) {
-                sib_map_layer<2, sib_tiles(11), 2, GC>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 9, mid);
+                sib_map_layer<2, sib_tiles(11), 2>(lds, U + u0, g, Wp, np, mh, t & 63, tiles, st, 9, mid);
             } else {
                 float rec[SIB_REC];  // the base's record entries of this thread, loaded before the x2 k-loop
 #pragma unroll
@@ -926,7 +911,7 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
                     const int j = t + k * NTS;
                     rec[k] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
                 }
-                sib_head_layer<GC>(lds, U[u0], Wp, np, mh, t & 63, hpart, tiles, st, 12, mid);
+                sib_head_layer(lds, U[u0], Wp, np, mh, t & 63, hpart, tiles, st, 12, mid);
                 __syncthreads();  // hpart complete; the next pass's windows have landed
                 st(14);
                 sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
@@ -1131,607 +1116,6 @@ __global__ void tree_grand_order_kernel(int n, const int32_t* __restrict__ d_cou
     for (int g = h; g >= 0; g = gnext[g]) grand[at++] = g;
 }
 
-// ============================================================ delta (scatter) incremental forward
-// pv_delta_kernel: the root children's forward as a DELTA of the root's (tree mode
-// "delta"; results within the fp32 tolerance of a full forward, not bitwise).  A
-// child's input differs from its root's only in the square of radius L-1 around its
-// stone at layer L's input (x0 r1, y1 r2, x1 r3, y2 r4 for y1, x1, y2, x2), so its
-// pre-BN accumulator is the root's plus the convolution of that difference:
-//     B_child(p) = B_root(p) + sum_t W_t * D(p + t),   D = child - root (zero elsewhere).
-// Scatter form: every row of D (the packed on-board positions of the nodes' squares
-// -- exact row counts, no window of root values) is multiplied by all 9 taps' weights
-// and tap t's product is added to output row p = q - t of an fp32 accumulator in
-// LDS.  Per node that is 164 instead of 276 row-convolutions (the 9 + 25 + 49 + 81
-// changed inputs instead of the 25 + 49 + 81 + 121 changed outputs; 0.59 of the exact
-// incremental forward's MFMA work, 0.67 with tile padding and the board's edges).
-// The epilogue adds the root's accumulator (gz_pvnet.hip's dump of the roots,
-// PV_PRE_FLOATS per layer), applies BN / skip / ReLU as the full kernel does, and
-// writes the node's next difference D = child - root (the root's map value, hi + lo)
-// to its squares; the x2 pass reduces the 1x1 heads as pv_sib_kernel does.
-// Layout and schedule follow pv_sib_kernel: chunks of 6 consecutive children, y1 over
-// all 6, x1 in passes of 3, y2 of 2, x2 + heads one node at a time, 4 waves (wave np:
-// output channels [32 np, 32 np + 32) in the MFMAs, the accumulator RMW and the
-// epilogue, so no two waves ever touch the same accumulator word).  Accumulation is
-// in a fixed order (taps 0..8, each tap's products in the k-loop's order): results
-// are deterministic.  A node with grandchildren also writes its CHILD values (hi/lo,
-// the patch layout) for pv_sib_kernel<true>.
-constexpr int DL_RIN = 112;                      // input rows per pass (7 tiles): y1 6x9, x1 3x25, y2 2x49, x2 81
-constexpr int DL_ROUT = 176;                     // output rows per pass (11 tiles): 150, 147, 162, 121
-constexpr int DL_AS = CH + 4;                    // floats per accumulator row: 528 B spreads rows over the banks
-constexpr int DL_IN_PLANE = 16 * DL_RIN * 8;     // halves per hi / lo plane of the input rows
-constexpr int DL_OFF_ACC = 2 * DL_IN_PLANE * 2;  // bytes
-constexpr int DL_OFF_HP = DL_OFF_ACC + DL_ROUT * DL_AS * 4;
-constexpr int DL_OFF_U = DL_OFF_HP + 4 * 3 * HP_ROWS * 4;
-constexpr int LDS_D = DL_OFF_U + SIB_G * 128;
-static_assert(LDS_D <= 160 * 1024, "LDS budget");
-static_assert(4 * 3 * HP_ROWS * 4 >= SIB_G * 512 * 2, "conv0's im2col fits the head partials");
-
-struct DlUnit {
-    const _Float16* gm;  // the root's maps x0, y1, x1, y2 (hi / lo)
-    _Float16* own;       // this node's differences D (patch layout), workgroup scratch
-    _Float16* patch;     // its patch slot (child values for its grandchildren), or nullptr
-    const float* pre;    // the root's pre-BN accumulators of y1, x1, y2, x2
-    int leaf, base, cell, pad0;
-    int pad[4];
-    uint32_t board[16];  // the node's bit-plane board (conv0's input)
-};
-static_assert(sizeof(DlUnit) == 128, "unit size");
-
-// per pass, for its g <= G nodes and radius R: each node's clipped square (row-major)
-// and its first row in the pass -- wave-uniform (scalar registers)
-template <int G>
-struct DlGeo {
-    int start[G + 1], r0[G], c0[G], wr[G], n[G];
-};
-template <int G>
-__device__ __forceinline__ DlGeo<G> dl_geo(const DlUnit* U, int ng, int R) {
-    DlGeo<G> o;
-    o.start[0] = 0;
-#pragma unroll
-    for (int h = 0; h < G; h++) {
-        Rows q = make_rows(0, 0, 0);
-        q.n = 0;
-        if (h < ng) {
-            const int cell = __builtin_amdgcn_readfirstlane(U[h].cell);
-            q = make_rows(cell / BN, cell % BN, R);
-        }
-        o.r0[h] = q.r0;
-        o.c0[h] = q.c0;
-        o.wr[h] = q.wr;
-        o.n[h] = q.n;
-        o.start[h + 1] = o.start[h] + q.n;
-    }
-    return o;
-}
-// row i of the pass -> its node g and position (pr, pc); valid = false past the rows
-template <int G>
-__device__ __forceinline__ bool dl_row(const DlGeo<G>& geo, int i, int& g, int& pr, int& pc) {
-    g = 0;
-#pragma unroll
-    for (int h = 1; h < G; h++) g += i >= geo.start[h] ? 1 : 0;
-    int j = i, R0 = 0, C0 = 0, WR = 1;
-#pragma unroll
-    for (int h = 0; h < G; h++)
-        if (h == g) {
-            j = i - geo.start[h];
-            R0 = geo.r0[h];
-            C0 = geo.c0[h];
-            WR = geo.wr[h];
-        }
-    const int rr = (int)(((float)j + 0.5f) / (float)WR);  // exact: j < 121, WR <= 11
-    pr = R0 + rr;
-    pc = C0 + (j - rr * WR);
-    return i < geo.start[G];
-}
-
-// The pass's scatter k-loop for the wave's n-tiles {nt0, nt0 + 1} over its NT input
-// tiles: per tap the 4 k-steps of the full kernel's k-loop (3 products each),
-// started from zero, then added into the accumulator rows q - t (read during the
-// tap's first k-step, written after its last; a wave's own LDS accesses stay in
-// order).  pr / pc: the lane's input row position (pr < -1: no row); ob / ow: its
-// node's output row of position (pr, pc) and the output square's width.  A lane
-// whose row q - t is off the board reads and writes the trash row DL_TRASH (no exec
-// masks).  Weights: a ring of 4 k-steps, refilled 3 k-steps ahead; issue order per
-// k-step: tile 0's MFMAs, then the refill, then the other tiles, so the wait the
-// compiler puts at the loop header covers only loads issued a k-step earlier.  (Taps
-// in pairs with an 8-deep ring spill 110+ registers.)
-constexpr int DL_TRASH = DL_ROUT - 1;
-template <int NT, int NMAX>
-__device__ __forceinline__ void dl_conv_nt(const _Float16* in, float* acc, const int (&pr)[NMAX],
-                                           const int (&pc)[NMAX], const int (&ob)[NMAX], const int (&ow)[NMAX],
-                                           const _Float16* __restrict__ Wf, int nt0, int lane) {
-    constexpr int CQ = 4, KS = 9 * CQ, RING = 4;
-    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
-    const int q = lane >> 4, li = lane & 15;
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
-    const int wo = (nt0 * 64 + lane) * 16;
-    auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
-    };
-    h8 b[RING][2][2];
-#pragma unroll
-    for (int c = 0; c < RING - 1; c++)
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            b[c][n][0] = wload(c, n, 0);
-            b[c][n][1] = wload(c, n, 1);
-        }
-    // B operand: row 16 m + li of the input rows, channel group cq * 4 + q -- the same
-    // for every tap (the scatter form reads each row at its own position), so all of
-    // it is read once and held (NT x 32 registers; MFMAs take B from AGPRs too): the
-    // only LDS traffic of the taps is the accumulator rows' read-add-write
-    const _Float16* bp = in + (q * DL_RIN + li) * 8;
-    h8 ah[NT][CQ], al[NT][CQ];
-#pragma unroll
-    for (int m = 0; m < NT; m++)
-#pragma unroll
-        for (int cq = 0; cq < CQ; cq++) {
-            ah[m][cq] = *(const h8*)(bp + m * 128 + cq * 4 * DL_RIN * 8);
-            al[m][cq] = *(const h8*)(bp + DL_IN_PLANE + m * 128 + cq * 4 * DL_RIN * 8);
-        }
-    const int cl = nt0 * 16 + 4 * q;  // the lane's first accumulator channel
-    int base[NT], step[NT];           // float offset of output row (pr, pc); per output row
-#pragma unroll
-    for (int m = 0; m < NT; m++) {
-        base[m] = ob[m] * DL_AS + cl;
-        step[m] = ow[m] * DL_AS;
-    }
-#pragma unroll 1
-    for (int tap = 0; tap < 9; tap++) {
-        constexpr int h = 0;
-        const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-        int ad[NT];
-        f32x4 old[2][NT];
-        f32x4 c[2][NT];
-#pragma unroll
-        for (int cq = 0; cq < CQ; cq++) {
-            const int sl = (h * CQ + cq) % RING, sr = (h * CQ + cq + RING - 1) % RING;
-#pragma unroll
-            for (int m = 0; m < NT; m++) {
-#pragma unroll
-                for (int n = 0; n < 2; n++)
-                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah[m][cq], cq == 0 ? zero4() : c[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++)
-                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah[m][cq], c[n][m], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < 2; n++)
-                    c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al[m][cq], c[n][m], 0, 0, 0);
-                if (m == 0) {  // k-step ks + RING - 1 into the slot of ks - 1 (past the end: unused)
-                    const int ksr = tap * CQ + cq + RING - 1;
-                    const int kn = ksr < KS ? ksr : ksr - KS;
-#pragma unroll
-                    for (int n2 = 0; n2 < 2; n2++) {
-                        b[sr][n2][0] = wload(kn, n2, 0);
-                        b[sr][n2][1] = wload(kn, n2, 1);
-                    }
-                }
-                if (cq == 0) {  // this tap's output row and its current sum
-                    const int r = pr[m] - dy, cc = pc[m] - dx;
-                    const bool ok = (unsigned)r < (unsigned)BN && (unsigned)cc < (unsigned)BN;
-                    ad[m] = ok ? base[m] - dy * step[m] - dx * DL_AS : DL_TRASH * DL_AS + cl;
-                    old[0][m] = *(const f32x4*)(acc + ad[m]);
-                    old[1][m] = *(const f32x4*)(acc + ad[m] + 16);
-                }
-                if (cq == CQ - 1 && m > 0) {  // the previous tile's sum is complete
-                    *(f32x4*)(acc + ad[m - 1]) = old[0][m - 1] + c[0][m - 1];
-                    *(f32x4*)(acc + ad[m - 1] + 16) = old[1][m - 1] + c[1][m - 1];
-                }
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA (tile 0)
-            __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);  // VMEM read
-#pragma unroll
-            for (int m = 1; m < NT; m++) __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA
-        }
-        *(f32x4*)(acc + ad[NT - 1]) = old[0][NT - 1] + c[0][NT - 1];
-        *(f32x4*)(acc + ad[NT - 1] + 16) = old[1][NT - 1] + c[1][NT - 1];
-    }
-}
-
-template <int NMAX>
-__device__ __forceinline__ void dl_conv(const _Float16* in, float* acc, int nt, const int (&pr)[NMAX],
-                                        const int (&pc)[NMAX], const int (&ob)[NMAX], const int (&ow)[NMAX],
-                                        const _Float16* __restrict__ Wf, int nt0, int lane) {
-    static_assert(NMAX == 7, "tile counts");
-    switch (nt) {
-        case 1: dl_conv_nt<1, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 2: dl_conv_nt<2, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 3: dl_conv_nt<3, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 4: dl_conv_nt<4, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 5: dl_conv_nt<5, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 6: dl_conv_nt<6, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        case 7: dl_conv_nt<7, NMAX>(in, acc, pr, pc, ob, ow, Wf, nt0, lane); break;
-        default: break;
-    }
-}
-
-// hi / lo of the 4 channels at ch0 of position pos in a root map (x0, y1, x1, y2) or a
-// node's square of radius R (patch layout), as fp32
-__device__ __forceinline__ f32x4 dl_map4(const _Float16* m, int ch0, int pos) {
-    const _Float16* p = m + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);
-    const h4 h = *(const h4*)p, l = *(const h4*)(p + PV_MAP_PLANE);
-    f32x4 v;
-#pragma unroll
-    for (int r = 0; r < 4; r++) v[r] = (float)h[r] + (float)l[r];
-    return v;
-}
-// raw hi / lo halves of 4 channels (converted where they are used, so that a
-// pipelined load phase never waits for its own loads)
-struct H4x2 {
-    h4 h, l;
-};
-__device__ __forceinline__ H4x2 dl_map4_raw(const _Float16* m, int ch0, int pos) {
-    const _Float16* p = m + ((ch0 >> 3) * 256 + pos) * 8 + (ch0 & 7);
-    return H4x2{*(const h4*)p, *(const h4*)(p + PV_MAP_PLANE)};
-}
-__device__ __forceinline__ H4x2 dl_sq4_raw(const _Float16* sq, int SS, int ch0, int idx) {
-    const _Float16* p = sq + ((ch0 >> 3) * SS + idx) * 8 + (ch0 & 7);
-    return H4x2{*(const h4*)p, *(const h4*)(p + 16 * SS * 8)};
-}
-__device__ __forceinline__ float h2f(const H4x2& x, int r) { return (float)x.h[r] + (float)x.l[r]; }
-__device__ __forceinline__ void dl_put_sq(_Float16* sq, int SS, int ch0, int idx, const f32x4& v) {
-    h4 hi, lo;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const _Float16 h = (_Float16)v[r];
-        hi[r] = h;
-        lo[r] = (_Float16)(v[r] - (float)h);
-    }
-    _Float16* p = sq + ((ch0 >> 3) * SS + idx) * 8 + (ch0 & 7);
-    *(h4*)p = hi;
-    *(h4*)(p + 16 * SS * 8) = lo;
-}
-
-// One pass of layer LAYER (0 y1, 1 x1, 2 y2, 3 x2 + heads) over nodes U[0, g): the
-// scatter k-loop over the nodes' difference rows (radius LAYER + 1) into the
-// accumulator rows of their output squares (radius LAYER + 2); then, for every output
-// row of the wave, the loads of the epilogue are issued at once -- the root's pre-ReLU
-// value z (gz_pvnet.hip's dump: BN(acc) [+ the skip input]) and, for x1 / x2 near the
-// stone, the difference of the skip input -- before the caller's barrier (mid: the
-// barrier and the next pass's fill), so their latency hides behind it; then
-//   child = relu(z + s * sum [+ D(skip)]),  root = relu(z),  D = child - root
-// into the node's square LAYER + 1 (the child value into its patch); x2 reduces the
-// child values into the 1x1 heads' partials instead.  The accumulator rows read go
-// back to zero.  NMO: output tiles of the pass at most.
-template <int LAYER, int G, int NMO, class Mid>
-__device__ __forceinline__ void dl_pass(const _Float16* in, float* acc, const DlUnit* U, int g,
-                                        const float* __restrict__ W, int np, int lane, int32_t* tiles,
-                                        float* __restrict__ hpart, Mid&& mid) {
-    constexpr int NMAX = 7, RO = LAYER + 2, S = 2 * RO + 1, SS = S * S;
-    constexpr bool SKIP = LAYER == 1 || LAYER == 3;
-    constexpr int RS = LAYER == 1 ? 1 : 3;  // radius of the skip input's difference (x0 r1, x1 r3)
-    constexpr int SS_SK = (2 * RS + 1) * (2 * RS + 1);
-    const DlGeo<G> gi = dl_geo<G>(U, g, LAYER + 1), go = dl_geo<G>(U, g, RO);
-    const int q = lane >> 4, li = lane & 15;
-    {
-        const int nt = (gi.start[G] + 15) >> 4;
-        if (tiles && np == 0 && lane == 0) atomicAdd(tiles, 9 * nt);
-        int pr[NMAX], pc[NMAX], ob[NMAX], ow[NMAX];
-#pragma unroll
-        for (int m = 0; m < NMAX; m++) {
-            int h, r, c;
-            const bool v = dl_row<G>(gi, m * 16 + li, h, r, c);
-            int b = 0, w = 1;
-#pragma unroll
-            for (int k = 0; k < G; k++)
-                if (k == h) {
-                    w = go.wr[k];
-                    b = go.start[k] + (r - go.r0[k]) * w + (c - go.c0[k]);
-                }
-            pr[m] = v ? r : -64;
-            pc[m] = c;
-            ob[m] = b;
-            ow[m] = w;
-        }
-        dl_conv<NMAX>(in, acc, nt, pr, pc, ob, ow, (const _Float16*)(W + F16_RES0 + LAYER * F16_STRIDE), 2 * np,
-                      lane);
-    }
-    const int nto = (go.start[G] + 15) >> 4;
-    f32x4 z[2][NMO];
-    H4x2 dsk[2][NMO];
-    int hh[NMO], sq[NMO];
-    bool near[NMO];
-#pragma unroll
-    for (int mo = 0; mo < NMO; mo++) {
-        int h, pr, pc;
-        const bool v = dl_row<G>(go, mo * 16 + li, h, pr, pc) && mo < nto;
-        const DlUnit& u = U[v ? h : 0];
-        const int cell = u.cell, cr = cell / BN, cc = cell - cr * BN;
-        const int pos = v ? pr * BN + pc : 0;
-        hh[mo] = v ? h : -1;
-        sq[mo] = (pr - cr + RO) * S + (pc - cc + RO);
-        near[mo] = SKIP && iabs(pr - cr) <= RS && iabs(pc - cc) <= RS;
-        const int ssq = near[mo] ? (pr - cr + RS) * (2 * RS + 1) + (pc - cc + RS) : 0;
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * q;
-            z[n][mo] = *(const f32x4*)(u.pre + LAYER * PV_PRE_FLOATS + pos * CH + ch0);
-            if constexpr (SKIP) dsk[n][mo] = dl_sq4_raw(u.own + PATCH_OFF[LAYER - 1], SS_SK, ch0, ssq);
-        }
-    }
-    const float* Rw = W + RES0 + LAYER * RES_STRIDE;
-    f32x4 es[2], e0[2], e1[2], ev[2];
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        const int ch0 = (2 * np + n) * 16 + 4 * q;
-        es[n] = *(const f32x4*)(Rw + RES_S + ch0);
-        if (LAYER == 3) {
-            e0[n] = *(const f32x4*)(W + P_W + ch0);
-            e1[n] = *(const f32x4*)(W + P_W + CH + ch0);
-            ev[n] = *(const f32x4*)(W + V_W + ch0);
-        }
-    }
-    mid();  // every wave's taps are in the accumulator rows; the next pass's fill is in flight
-#pragma unroll
-    for (int mo = 0; mo < NMO; mo++) {
-        if (mo >= nto) continue;
-        const int i = mo * 16 + li;
-        const bool v = hh[mo] >= 0;
-        float s0 = 0.f, s1 = 0.f, sv = 0.f;
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * q;
-            float* ap = acc + (v ? i : 0) * DL_AS + ch0;
-            const f32x4 a = *(const f32x4*)ap;
-            f32x4 y, d;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float dk = 0.f;
-                if constexpr (SKIP) dk = near[mo] ? h2f(dsk[n][mo], r) : 0.f;
-                float tc = __builtin_fmaf(a[r], es[n][r], z[n][mo][r]) + dk;
-                tc = tc > 0.f ? tc : 0.f;
-                if (LAYER == 3) {
-                    s0 = __builtin_fmaf(e0[n][r], tc, s0);
-                    s1 = __builtin_fmaf(e1[n][r], tc, s1);
-                    sv = __builtin_fmaf(ev[n][r], tc, sv);
-                } else {
-                    const float tr = z[n][mo][r] > 0.f ? z[n][mo][r] : 0.f;
-                    y[r] = tc;
-                    d[r] = tc - tr;
-                }
-            }
-            if (v) {
-                if (LAYER < 3) {
-                    const DlUnit& u = U[hh[mo]];
-                    dl_put_sq(u.own + PATCH_OFF[LAYER + 1], SS, ch0, sq[mo], d);
-                    if (u.patch) dl_put_sq(u.patch + PATCH_OFF[LAYER + 1], SS, ch0, sq[mo], y);
-                }
-                *(f32x4*)ap = zero4();
-            }
-        }
-        if (LAYER == 3) {
-            s0 += __shfl_xor(s0, 16);
-            s1 += __shfl_xor(s1, 16);
-            sv += __shfl_xor(sv, 16);
-            s0 += __shfl_xor(s0, 32);
-            s1 += __shfl_xor(s1, 32);
-            sv += __shfl_xor(sv, 32);
-            if (lane < 16 && v) {
-                hpart[(np * 3 + 0) * HP_ROWS + i] = s0;
-                hpart[(np * 3 + 1) * HP_ROWS + i] = s1;
-                hpart[(np * 3 + 2) * HP_ROWS + i] = sv;
-            }
-        }
-    }
-}
-
-// conv0 + BN + ReLU at the <= 9 positions around each node's stone (as sib_conv0),
-// then D(x0) = child - root into the y1 pass's input rows (LDS) and the node's square
-__device__ __forceinline__ void dl_conv0(_Float16* in, const _Float16* col, const DlUnit* U, int ng,
-                                         const float* __restrict__ W, int np, int lane) {
-    const int li = lane & 15, q = lane >> 4;
-    const DlGeo<SIB_G> gi = dl_geo<SIB_G>(U, ng, 1);
-    h8 wh[2], wl[2];
-    f32x4 ws[2], wt[2];
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        const int nt = 2 * np + n, ch0 = nt * 16 + 4 * q;
-        const _Float16* wf = (const _Float16*)(W + F16_C0) + ((size_t)nt * 64 + lane) * 8;
-        wh[n] = *(const h8*)wf;
-        wl[n] = *(const h8*)(wf + 8 * 64 * 8);
-        ws[n] = *(const f32x4*)(W + C0_S + ch0);
-        wt[n] = *(const f32x4*)(W + C0_T + ch0);
-    }
-#pragma unroll
-    for (int g = 0; g < SIB_G; g++) {
-        if (g >= ng) break;
-        const h8 a = *(const h8*)(col + g * 512 + li * 32 + 8 * q);
-        const DlUnit& u = U[g];
-        const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
-        const bool rowok = li < gi.n[g];
-        const int wr = gi.wr[g];
-        const int rr = rowok ? (int)(((float)li + 0.5f) / (float)wr) : 0;
-        const int pr = gi.r0[g] + rr, pc = gi.c0[g] + (li - rr * wr), pos = pr * BN + pc;
-        const int row = gi.start[g] + li, idx = (pr - cr + 1) * 3 + (pc - cc + 1);
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int ch0 = (2 * np + n) * 16 + 4 * q;
-            f32x4 acc = zero4();
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[n], a, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[n], a, acc, 0, 0, 0);
-            if (rowok) {
-                const f32x4 rt = dl_map4(u.gm, ch0, pos);
-                f32x4 y, d;
-                h4 dh, dl;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float t = __builtin_fmaf(acc[r], ws[n][r], wt[n][r]);
-                    t = t > 0.f ? t : 0.f;
-                    y[r] = t;
-                    d[r] = t - rt[r];
-                    const _Float16 hh = (_Float16)d[r];
-                    dh[r] = hh;
-                    dl[r] = (_Float16)(d[r] - (float)hh);
-                }
-                _Float16* ip = in + ((ch0 >> 3) * DL_RIN + row) * 8 + (ch0 & 7);
-                *(h4*)ip = dh;
-                *(h4*)(ip + DL_IN_PLANE) = dl;
-                dl_put_sq(u.own + PATCH_OFF[0], 9, ch0, idx, d);
-                if (u.patch) dl_put_sq(u.patch + PATCH_OFF[0], 9, ch0, idx, y);
-            }
-        }
-    }
-}
-
-// the input rows of layer L (L >= 1: the nodes' D squares of map L, radius L + 1) for
-// nodes U[0, g), by LDS-DMA: position-major, a lane's row then its 32 planes
-template <int G>
-__device__ __forceinline__ void dl_fill(_Float16* in, const DlUnit* U, int g, int L, int tid) {
-    const int R = L + 1, S = 2 * R + 1, SS = S * S, off = L == 1 ? PATCH_OFF[1] : (L == 2 ? PATCH_OFF[2] : PATCH_OFF[3]);
-    const DlGeo<G> gi = dl_geo<G>(U, g, R);
-    const int rows = gi.start[G], nb = (rows + 63) >> 6;
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int w = wave; w < nb * 8; w += NTS / 64) {  // (64-row block, group of 4 planes)
-        const int blk = w >> 3, p0 = (w & 7) * 4, i = blk * 64 + lane;
-        int h, pr, pc;
-        const bool v = dl_row<G>(gi, i, h, pr, pc);
-        const _Float16* src = (const _Float16*)gz_sib_zero16;
-        int stride = 0;
-        if (v) {
-            const DlUnit& u = U[h];
-            const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
-            src = u.own + off + ((pr - cr + R) * S + (pc - cc + R)) * 8 + p0 * SS * 8;
-            stride = SS * 8;
-        }
-        char* dst = (char*)in + ((size_t)p0 * DL_RIN + blk * 64) * 16;
-        if (i < DL_RIN) {
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                __builtin_amdgcn_global_load_lds((glb_void_t*)(src + k * stride), (lds_void_t*)(dst + k * DL_RIN * 16), 16,
-                                                 0, 0);
-        }
-    }
-}
-
-// list: the root children (tree_children_kernel), list_count entries; scratch: SIB_G
-// patch-sized areas per workgroup (the nodes' D squares)
-__global__ __launch_bounds__(NTS, 1) void pv_delta_kernel(TreeArgs A, _Float16* __restrict__ scratch,
-                                                          const int32_t* __restrict__ list,
-                                                          const int32_t* __restrict__ list_count) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_D];
-    DlUnit* const U = (DlUnit*)(lds + DL_OFF_U);
-    _Float16* const in = (_Float16*)lds;
-    float* const acc = (float*)(lds + DL_OFF_ACC);
-    float* const hpart = (float*)(lds + DL_OFF_HP);
-    const int count = *list_count;
-    const int nx = gridDim.x >= 8 ? 8 : 1;
-    const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
-    if (k >= per) return;
-    const int xchunk = (count + nx - 1) / nx;
-    const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
-    _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3;
-    const float* W = A.W;
-    int32_t* tiles = A.tiles;
-    SibStamp<16> st;  // phases: 0 units, 1 conv0, 2 exposed fills, 3..6 k-loops, 7 barrier, 8..11 epilogues, 12 record, 13 barrier
-    for (int i = tid; i < DL_ROUT * DL_AS / 4; i += NTS) ((f32x4*)acc)[i] = zero4();
-    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
-        __syncthreads();  // the previous chunk's readers of U are done
-        const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
-        if (wave == 0 && lane < ng) {
-            const int b = list[pos + lane];
-            DlUnit u;
-            const int ci = A.cinfo[b];
-            const int o = (ci >> 8) & 0x3fffff;
-            u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
-            u.pre = A.pres + (size_t)o * 4 * PV_PRE_FLOATS;
-            u.leaf = b;
-            u.cell = ci & 0xff;
-            u.base = A.meta[b];
-            u.own = myscr + (size_t)lane * PATCH_HALVES;
-            const int ps = A.pslot[b];
-            u.patch = ps >= 0 ? A.patches + (size_t)ps * PATCH_HALVES : nullptr;
-            u.pad0 = 0;
-#pragma unroll
-            for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
-            U[lane] = u;
-        }
-        __syncthreads();
-        st(0);
-#ifdef GZ_PVINC_STAMPS
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&gz_pvinc_stamps_n[1], (unsigned long long)ng);
-#endif
-        {
-            int t = tid;
-            asm volatile("" : "+v"(t));
-            sib_col((_Float16*)hpart, U, ng, t);
-            __syncthreads();
-            const float* Wp = W;
-            asm volatile("" : "+s"(Wp));
-            dl_conv0(in, (const _Float16*)hpart, U, ng, Wp, np, t & 63);
-            __syncthreads();  // the y1 input rows are in LDS, D(x0) in the squares
-            st(1);
-        }
-        const int nx1 = (ng + 2) / 3, ny2 = (ng + 1) / 2, npass = 1 + nx1 + ny2 + ng;
-        auto pass_of = [&](int p, int& L, int& u0, int& g) {
-            if (p == 0) {
-                L = 0, u0 = 0, g = ng;
-            } else if (p <= nx1) {
-                L = 1, u0 = 3 * (p - 1), g = ng - u0 < 3 ? ng - u0 : 3;
-            } else if (p <= nx1 + ny2) {
-                L = 2, u0 = 2 * (p - 1 - nx1), g = ng - u0 < 2 ? ng - u0 : 2;
-            } else {
-                L = 3, u0 = p - 1 - nx1 - ny2, g = 1;
-            }
-        };
-        auto fill = [&](int L, int u0, int g, int t) {
-            if (L == 1) dl_fill<3>(in, U + u0, g, 1, t);
-            else if (L == 2) dl_fill<2>(in, U + u0, g, 2, t);
-            else if (L == 3) dl_fill<1>(in, U + u0, g, 3, t);
-        };
-        bool filled = true;  // y1's input rows: dl_conv0
-        for (int p = 0; p < npass; p++) {
-            int L, u0, g, L2 = 0, v0 = 0, g2 = 0;
-            pass_of(p, L, u0, g);
-            // the next pass's input rows can be loaded as soon as this pass's k-loop is
-            // done unless this pass's epilogue writes them
-            bool pre = p + 1 < npass;
-            if (pre) {
-                pass_of(p + 1, L2, v0, g2);
-                pre = !(L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2);
-            }
-            const float* Wp = W;
-            int t = tid;
-            asm volatile("" : "+s"(Wp), "+v"(t));
-            if (!filled) {
-                fill(L, u0, g, t);
-                __syncthreads();
-                st(2);
-            }
-            auto mid = [&]() {
-                st(3 + L);
-                __syncthreads();  // every tap is in the accumulator rows; the input rows are free
-                st(7);
-                if (pre) fill(L2, v0, g2, t);
-            };
-            if (L == 0) {
-                dl_pass<0, SIB_G, 10>(in, acc, U, g, Wp, np, t & 63, tiles, hpart, mid);
-            } else if (L == 1) {
-                dl_pass<1, 3, 10>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
-            } else if (L == 2) {
-                dl_pass<2, 2, 11>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
-            } else {
-                float rec[SIB_REC];  // the root's record entries of this thread
-#pragma unroll
-                for (int kk = 0; kk < SIB_REC; kk++) {
-                    const int j = t + kk * NTS;
-                    rec[kk] = j < HSTRIDE ? A.hbuf[(size_t)U[u0].base * HSTRIDE + j] : 0.f;
-                }
-                dl_pass<3, 1, 8>(in, acc, U + u0, g, Wp, np, t & 63, tiles, hpart, mid);
-                __syncthreads();  // hpart complete
-                st(11);
-                sib_record(U[u0], Wp, A.hbuf, hpart, rec, t);
-                st(12);
-            }
-            filled = pre;
-            if (L < 3) st(8 + L);
-            __syncthreads();  // the squares are stored; the accumulator rows are zero again
-            st(13);
-        }
-    }
-}
-
 }  // namespace
 
 extern "C" void gz_internal_set_error(const char* msg);
@@ -1771,24 +1155,21 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     return GZ_OK;
 }
 
-// delta != 0: the root children through pv_delta_kernel (d_pres: the roots' pre-BN
-// accumulators), else pv_sib_kernel (bitwise); grandchildren always pv_sib_kernel<true>
+// the root children through pv_dg_kernel (gz_pvdg.hip; d_pres: the roots' pre-BN
+// accumulators), then the grandchildren through pv_sib_kernel
 extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                          const int32_t* d_ord, const int32_t* d_pslot, int32_t n,
                                          const int32_t* d_count, const _Float16* d_maps, _Float16* d_patches,
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         int delta, const float* d_pres, void* stream) {
-    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles, d_pres};
+                                         const float* d_pres, void* stream) {
+    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
     hipStream_t s = (hipStream_t)stream;
-    if (delta) {
-        const int rc = gz_internal_tree_delta(d_weights, d_boards, d_meta, d_pslot, d_cinfo, d_maps, d_pres, d_patches,
-                                              d_hbuf, d_scratch, d_tiles, d_children, d_nchildren, grid, stream);
-        if (rc) return rc;
-    } else
-        pv_sib_kernel<false><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_children, d_nchildren);
-    pv_sib_kernel<true><<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
+    const int rc = gz_internal_tree_delta(d_weights, d_boards, d_meta, d_pslot, d_cinfo, d_maps, d_pres, d_patches,
+                                          d_hbuf, d_scratch, d_tiles, d_children, d_nchildren, grid, stream);
+    if (rc) return rc;
+    pv_sib_kernel<<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("tree children: ") + hipGetErrorString(e)).c_str());
@@ -1800,7 +1181,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
 #ifdef GZ_PVINC_STAMPS
 // phase stamps of workgroup 0 (-DGZ_PVINC_STAMPS builds, tools/pvinc_bench.py)
 extern "C" int gz_pvinc_stamps_read(unsigned long long* out, int reset) {
-    // out[0..31] = ticks per phase (pv_sib_kernel, then pv_delta_kernel), out[32..33] = their nodes
+    // out[0..15] = ticks per phase of pv_sib_kernel, out[32] = its nodes (out[16..31], out[33]: 0)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_pvinc_stamps), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(gz_pvinc_stamps_n), 2 * sizeof(unsigned long long)) != hipSuccess)
         return -1;

@@ -970,7 +970,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         int delta, const float* d_pres, void* stream);
+                                         const float* d_pres, void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -981,7 +981,7 @@ struct TreeWs {
     float* hbuf;
     int32_t *ord, *pslot, *roots, *full, *grand, *gnext, *cinfo, *children, *ghead, *ctr;
     _Float16* maps;
-    float* pres;        // the roots' pre-BN accumulators (pv_delta_kernel)
+    float* pres;        // the roots' pre-BN accumulators (pv_dg_kernel)
     _Float16* patches;
     _Float16* scratch;  // pv_sib_kernel / pv_dg_kernel: 12 patch-sized areas per workgroup
 };
@@ -1023,14 +1023,9 @@ extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
            (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
 }
 
-extern "C" int gz_pv_forward_tree_mode(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
-                                       int32_t n, const int32_t* d_count, int32_t root_cap, float* d_logits,
-                                       float* d_value, float* d_probs, double* d_prior, void* d_workspace,
-                                       int32_t mode, void* stream) {
-    if (mode != GZ_TREE_EXACT && mode != GZ_TREE_DELTA) {
-        gz_internal_set_error("gz_pv_forward_tree_mode: unknown mode");
-        return GZ_ERR_ARG;
-    }
+extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
+                                  const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
+                                  float* d_probs, double* d_prior, void* d_workspace, void* stream) {
     if (n < 0 || root_cap < 0 || (n > 0 && (!d_weights || !d_boards || !d_meta || !d_logits || !d_value || !d_workspace))) {
         gz_internal_set_error("gz_pv_forward_tree: bad arguments");
         return GZ_ERR_ARG;
@@ -1050,14 +1045,13 @@ extern "C" int gz_pv_forward_tree_mode(const float* d_weights, const uint32_t* d
     // roots (full forward, maps stored), then every board without a stored root or
     // patch (full forward), then the roots' children and their children (incremental);
     // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed]
-    const bool delta = mode == GZ_TREE_DELTA;
     pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
-                                                     t.ord, t.maps, root_cap, delta ? t.pres : nullptr);
+                                                     t.ord, t.maps, root_cap, t.pres);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
                                    t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, t.children, t.ctr + 2, grid,
-                                   delta ? 1 : 0, t.pres, stream);
+                                   t.pres, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
@@ -1069,12 +1063,6 @@ extern "C" int gz_pv_forward_tree_mode(const float* d_weights, const uint32_t* d
     return GZ_OK;
 }
 
-extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
-                                  const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
-                                  float* d_probs, double* d_prior, void* d_workspace, void* stream) {
-    return gz_pv_forward_tree_mode(d_weights, d_boards, d_meta, n, d_count, root_cap, d_logits, d_value, d_probs,
-                                   d_prior, d_workspace, GZ_TREE_EXACT, stream);
-}
 
 // the 16-row MFMA tiles of the residual convs the last tree forward's incremental
 // kernels executed: [root children, grandchildren]

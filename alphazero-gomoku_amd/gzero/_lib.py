@@ -18,7 +18,6 @@ GZ_MAX_SIMULATIONS = 4095
 GZ_MAX_GAME_PLIES = 200
 GZ_PV_FP32 = 0
 GZ_PV_F16X3 = 1
-GZ_TREE_EXACT, GZ_TREE_DELTA = 0, 1  # gz_pv_forward_tree_mode
 GZ_AUG_FIX_LABELS = 1
 
 
@@ -134,7 +133,6 @@ SIGNATURES = {
     "gz_pv_forward": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "gz_pv_tree_workspace_bytes": (_SZ, [_I32, _I32]),
     "gz_pv_forward_tree": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _P]),
-    "gz_pv_forward_tree_mode": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _I32, _P]),
     "gz_pv_tree_stats": (ctypes.c_int, [_P, _I32, _P, _P]),
     "gz_pv_tree_exec_tiles": (ctypes.c_int, [_P, _I32, _P, _P]),
     "gz_gn_weight_floats": (_SZ, []),

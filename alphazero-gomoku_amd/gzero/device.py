@@ -211,12 +211,11 @@ def pv_forward(weights, leaf_rows, want_prior=False):
     return out
 
 
-def pv_forward_tree(weights, leaf_rows, meta, root_cap=None, mode="exact"):
-    """Host convenience for gz_pv_forward_tree_mode: [n,16] uint32 leaf rows and their
+def pv_forward_tree(weights, leaf_rows, meta, root_cap=None):
+    """Host convenience for gz_pv_forward_tree: [n,16] uint32 leaf rows and their
     int32 meta (-1 root, >= 0 the parent's index for a root child or a child of
     one, -2 other) ->
-    (logits [n,225], value [n], probs [n,225], prior [n,225], list sizes).
-    mode: "exact" (bit-identical to the full forward) or "delta"."""
+    (logits [n,225], value [n], probs [n,225], prior [n,225], list sizes)."""
     lib = require_gpu()
     rows = np.ascontiguousarray(leaf_rows, np.uint32).reshape(-1, 16)
     n = rows.shape[0]
@@ -230,10 +229,9 @@ def pv_forward_tree(weights, leaf_rows, meta, root_cap=None, mode="exact"):
     d_p = torch.empty(n * 225, dtype=torch.float32, device="cuda")
     d_pr = torch.empty(n * 225, dtype=torch.float64, device="cuda")
     ws = torch.empty(lib.gz_pv_tree_workspace_bytes(n, root_cap), dtype=torch.uint8, device="cuda")
-    tm = {"exact": _lib.GZ_TREE_EXACT, "delta": _lib.GZ_TREE_DELTA}[mode]
-    _lib.check(lib.gz_pv_forward_tree_mode(ptr(weights.tensor), ptr(d_b), ptr(d_m), n, None, int(root_cap),
-                                           ptr(d_lg), ptr(d_v), ptr(d_p), ptr(d_pr), ptr(ws), tm, stream()),
-               "gz_pv_forward_tree_mode")
+    _lib.check(lib.gz_pv_forward_tree(ptr(weights.tensor), ptr(d_b), ptr(d_m), n, None, int(root_cap),
+                                      ptr(d_lg), ptr(d_v), ptr(d_p), ptr(d_pr), ptr(ws), stream()),
+               "gz_pv_forward_tree")
     st = torch.zeros(6, dtype=torch.int32, device="cuda")
     _lib.check(lib.gz_pv_tree_stats(ptr(ws), n, ptr(st), stream()), "gz_pv_tree_stats")
     torch.cuda.synchronize()

@@ -34,11 +34,10 @@ class SelfPlayEngine:
         planner_steps > 0: BG-planner rollout plies (config 4); gn_weights = the
         planner's GraphNet/DQN blob (gzero.planner_nets) or a GNWeights.
         pv_mode: "full" = one full forward per node (gz_pv_forward); "tree" = the
-        incremental forward (gz_pv_forward_tree: a root's children and grandchildren
-        recompute only the windows around their new stone; bit-identical outputs;
-        f16x3 only); "delta" = the incremental forward with the root children as the
+        incremental forward (gz_pv_forward_tree, f16x3 only): a root's children as the
         root's pre-BN accumulators plus the convolution of their input differences
-        (gz_pv_forward_tree_mode GZ_TREE_DELTA: within 1e-4 of the full forward)."""
+        (within 2e-5 of the full forward), its grandchildren recomputing the windows
+        around their new stone; roots and other nodes bit-identical to "full"."""
         self.lib = require_gpu()
         self.n_slots = int(n_slots)
         self.n_active = self.n_slots  # the slots the launches run (the first n_active)
@@ -57,10 +56,9 @@ class SelfPlayEngine:
             self.gn_stats(reset=True)
         self.pv_weights = pv_weights if (pv_weights is None or isinstance(pv_weights, PVWeights)) \
             else PVWeights(pv_weights)
-        if pv_mode not in ("full", "tree", "delta"):
-            raise ValueError(f"pv_mode must be 'full', 'tree' or 'delta', not {pv_mode!r}")
-        self.tree = pv_mode in ("tree", "delta") and self.gather
-        self.tree_mode = _lib.GZ_TREE_DELTA if pv_mode == "delta" else _lib.GZ_TREE_EXACT
+        if pv_mode not in ("full", "tree"):
+            raise ValueError(f"pv_mode must be 'full' or 'tree', not {pv_mode!r}")
+        self.tree = pv_mode == "tree" and self.gather
         self.pv_mode = pv_mode if self.gather else "full"
         if self.tree and self.pv_weights.mode != _lib.GZ_PV_F16X3:
             raise ValueError(f"pv_mode={pv_mode!r} needs f16x3 weights")
@@ -171,11 +169,11 @@ class SelfPlayEngine:
             return
         d_count = self.d_counters[4:8]  # counters.leaves
         if self.tree:
-            _lib.check(self.lib.gz_pv_forward_tree_mode(ptr(self.pv_weights.tensor), ptr(self.d_leaves),
-                                                        ptr(self.d_meta), self.leaf_cap, ptr(d_count), self.root_cap,
-                                                        ptr(self.d_logits), ptr(self.d_value), ptr(self.d_probs),
-                                                        ptr(self.d_prior), ptr(self.d_tree_ws), self.tree_mode,
-                                                        stream()), "gz_pv_forward_tree_mode")
+            _lib.check(self.lib.gz_pv_forward_tree(ptr(self.pv_weights.tensor), ptr(self.d_leaves),
+                                                   ptr(self.d_meta), self.leaf_cap, ptr(d_count), self.root_cap,
+                                                   ptr(self.d_logits), ptr(self.d_value), ptr(self.d_probs),
+                                                   ptr(self.d_prior), ptr(self.d_tree_ws), stream()),
+                       "gz_pv_forward_tree")
             return
         _lib.check(self.lib.gz_pv_forward(ptr(self.pv_weights.tensor), ptr(self.d_leaves), self.leaf_cap,
                                           ptr(d_count), ptr(self.d_logits), ptr(self.d_value),

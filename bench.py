@@ -22,9 +22,11 @@ every ply played by every rank.
 
 The PV forward (default --pv-mode tree) is gz_pv_forward_tree: each search
 root runs the full f16x3 tower (3-term fp16 split on MFMA, f32 accumulate) and
-keeps its maps; each root child and grandchild recomputes only the windows its
-new stone changes, with the full kernel's products in the full kernel's order,
-so every output is bit-identical to the full forward's (--pv-mode full).
+keeps its maps and pre-BN accumulators (bit-identical to --pv-mode full); each
+root child is the root's accumulators plus the convolution of its one-stone input
+differences (pv_dg_kernel) and each grandchild recomputes the windows its stone
+changes from its parent's squares (pv_sib_kernel): within 2e-5 of the full
+forward's logits / value (1e-4 of the reference's fp32 forward).
 --pv-precision fp32 runs the exact-f32 MFMA kernel.
 
 Also reported: the roofline of the PV forward (executed MFMA FLOP / kernel time,
@@ -88,7 +90,7 @@ def load_traffic(boards, mode):
 def load_clock(kernel):
     """Measured shader clock and MFMA-busy share of `kernel` under load (newest
     profiles/rNN/clock.json that has it), or None."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(REPO, "profiles", rnd, "clock.json")
         if os.path.exists(p):
             with open(p) as f:
@@ -490,10 +492,10 @@ def roofline_of(m, precision):
                 "executed_mflop_per_child": round((executed - (t[1] + t[3]) * PV_FLOP)
                                                   / max(1.0, t[2] + t[4]) / 1e6, 2),
                 "note": ("achieved = MFMA work executed / kernel time: roots and untagged nodes the full 267.38 "
-                         "MFLOP; root children and grandchildren the 16-row MFMA tiles their kernel counted "
-                         "(pv_sib_kernel packs several nodes' recomputed squares into each layer pass) plus conv0 "
-                         "and the heads; every node's logits, value, softmax and prior are bit-identical to the "
-                         "full forward's")}
+                         "MFLOP; root children (pv_dg_kernel: the delta convolution, rows sorted by tap class so a "
+                         "tile skips the taps none of its rows needs) and grandchildren (pv_sib_kernel) the 16-row "
+                         "MFMA tile-taps their kernels counted, plus conv0 and the heads; roots and untagged nodes "
+                         "bit-identical to the full forward, children and grandchildren within 2e-5")}
     traffic, _ = load_traffic(mean_leaves, "tree" if m.get("tree") else "full") if precision == "f16x3" \
         else (None, None)
     if precision == "fp32":
@@ -519,11 +521,10 @@ def roofline_of(m, precision):
         "note": note,
     }
     if tree:
-        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + untagged nodes, pv_sib_kernel on "
-                       "root children and, second launch, on their children; pv_heads_kernel, pv_prior_kernel)")
+        r["kernel"] = ("gz_pv_forward_tree<f16x3> (pv_kernel_f16x3 on roots + untagged nodes, pv_dg_kernel on "
+                       "root children, pv_sib_kernel on their children; pv_heads_kernel, pv_prior_kernel)")
         r["incremental"] = tree
-    dominant = (("pv_sib_kernel" if os.environ.get("GZ_PVINC_SIB", "1") != "0" else "pv_child_kernel") if tree
-                else ("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32"))
+    dominant = ("pv_dg_kernel" if tree else ("pv_kernel_f16x3" if precision == "f16x3" else "pv_kernel_f32"))
     clk = load_clock(dominant)
     if clk:  # DVFS context: the spec peak assumes 2.4 GHz; the kernel holds less under load
         r["clock"] = {"kernel": dominant, "ghz": clk["median_ghz"], "mfma_busy": clk["median_mfma_busy"],
@@ -545,10 +546,10 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--pv-precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="policy-value forward: 3-term fp16 split (f32 accumulate) or exact fp32 MFMA")
-    ap.add_argument("--pv-mode", default="tree", choices=["full", "tree", "delta"],
-                    help="full: one full forward per node; tree: the incremental forward of a root's children "
-                         "(gz_pv_forward_tree, bit-identical outputs); delta: root children as the root's "
-                         "pre-activations plus a scatter convolution of their input differences (within 2e-5)")
+    ap.add_argument("--pv-mode", default="tree", choices=["full", "tree"],
+                    help="full: one full forward per node; tree: the incremental forward (gz_pv_forward_tree): "
+                         "root children as the root's pre-BN accumulators plus the convolution of their input "
+                         "differences, grandchildren from their parent's squares (within 2e-5 of full)")
     ap.add_argument("--elided-warmup", type=int, default=40, help="plies before timing the prior-elided run")
     ap.add_argument("--elided-plies", type=int, default=20)
     ap.add_argument("--no-elided", action="store_true")
@@ -632,7 +633,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if args.pv_precision == "fp32" else "f16x3 (fp32-equivalent split, f32 accumulate)",
+            "dtype": "fp32" if args.pv_precision == "fp32" else (
+                "f16x3 (fp32-equivalent split, f32 accumulate)"
+                + ("; tree forward: root children as a delta of the root's fp32 accumulators, within 2e-5 of the "
+                   "full forward and 1e-4 of the reference (tests/test_gpu_pvdelta.py)" if eng.tree else "")),
             "data": "synthetic: self-play from the empty board with random-init weights (numpy default_rng(0))",
             "config": {
                 "workload": (f"BASELINE config {4 if args.planner_steps else 2}: {args.slots} concurrent self-play "
@@ -641,10 +645,8 @@ def main():
                              f"{burn_in} burn-in plies: the steady-state mix of game plies); policy-value "
                              "forward + masked prior on every non-terminal node the searches create "
                              f"(reference-work mode, {args.pv_precision}"
-                             + (", incremental forward of root children and grandchildren: bit-identical outputs"
-                                if eng.tree and args.pv_mode == "tree" else "")
-                             + (", delta forward of root children (within 2e-5 of the full forward)"
-                                if eng.tree and args.pv_mode == "delta" else "")
+                             + (", incremental forward of root children (delta of the root's accumulators) and "
+                                "grandchildren: within 2e-5 of the full forward" if eng.tree else "")
                              + ")"),
                 "pv_mode": args.pv_mode if eng.tree else "full",
                 "games_per_gpu": args.slots,

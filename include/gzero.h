@@ -203,30 +203,23 @@ int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
 /* Incremental forward of the nodes of MCTS searches (MCTSNode.__init__ ->
  * GomokuModel.predict, ai_agent.py:522-523; neural_network.py:132-159), f16x3:
  * d_meta as written by gz_selfplay_run.  Roots and untagged nodes run the full
- * forward (roots also keep their intermediate maps, at most root_cap of them);
- * a root's children recompute only the windows around their one new stone
- * (radius 1..5 per layer) from the root's maps, and the children of a root child
- * (grandchildren) from the root's maps overlaid with their parent's recomputed
- * squares (at most 16 * root_cap parents).  A tag whose board does not differ
- * from its parent's by exactly one cell is ignored (full forward), so the tags
- * only decide speed.  Outputs are bit-identical to gz_pv_forward(...,
- * GZ_PV_F16X3, ...) of the same boards.  d_workspace:
+ * forward (roots also keep their intermediate maps and pre-BN accumulators, at
+ * most root_cap of them) and are bit-identical to gz_pv_forward(..., GZ_PV_F16X3,
+ * ...) of the same boards.  A root's children are the root's pre-BN accumulators
+ * plus the convolution of their one-stone input differences (radius 1..4 per
+ * layer's input): the same network in f16x3 arithmetic with fp32 accumulation in
+ * another order, within 2e-5 of the full forward's logits / value (1e-4 of the
+ * reference's fp32 forward).  The children of a root child (grandchildren)
+ * recompute the windows around their stone from the root's maps overlaid with
+ * their parent's recomputed squares (at most 16 * root_cap parents).  A tag whose
+ * board does not differ from its parent's by exactly one cell is ignored (full
+ * forward), so the tags only decide speed.  d_workspace:
  * gz_pv_tree_workspace_bytes(n, root_cap) bytes (~2.4 MB per root: maps 512 KB,
  * pre-BN accumulators 512 KB, 16 patches of 84 KB). */
 size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap);
 int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
                        const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value, float* d_probs,
                        double* d_prior, void* d_workspace, void* stream);
-/* gz_pv_forward_tree with a mode: GZ_TREE_EXACT = gz_pv_forward_tree (bit-identical
- * to the full forward); GZ_TREE_DELTA = the root children as the root's pre-BN
- * accumulators plus the convolution of their one-stone input differences (the same
- * network, fp32-equivalent f16x3 arithmetic in another order: within 1e-4 of the
- * full forward, not bitwise; 0.59 of the exact mode's residual-conv MFMA work per
- * root child).  Grandchildren and every other board as in GZ_TREE_EXACT. */
-enum { GZ_TREE_EXACT = 0, GZ_TREE_DELTA = 1 };
-int gz_pv_forward_tree_mode(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
-                            const int32_t* d_count, int32_t root_cap, float* d_logits, float* d_value,
-                            float* d_probs, double* d_prior, void* d_workspace, int32_t mode, void* stream);
 /* d_out6 (device int32[6]) = the last tree forward's list sizes: roots seen, roots
  * with stored maps, incremental children, full-forward boards, incremental
  * grandchildren, parents that claimed a patch slot. */

@@ -1,13 +1,13 @@
-"""Delta tree forward (gz_pv_forward_tree_mode GZ_TREE_DELTA, csrc/gz_pvinc.hip
-pv_delta_kernel): a root child's pre-BN accumulators are the root's plus the
+"""Delta tree forward of the root children (gz_pv_forward_tree, csrc/gz_pvdg.hip
+pv_dg_kernel): a root child's pre-BN accumulators are the root's plus the
 convolution of its one-stone input differences.  The network and its f16x3
 (fp32-equivalent) arithmetic are the same as the full forward's, the order of the
 additions is not, so the outputs are compared within tolerance, stated here:
 
 * against the full f16x3 forward of the same boards: logits and value within
   DELTA_TOL = 2e-5 (measured ~1e-6), softmax within 1e-6, the fp64 masked prior
-  within 1e-6 -- and roots, untagged boards and everything the exact mode runs
-  bit for bit the same;
+  within 1e-6 -- and roots and untagged boards (the full kernel) bit for bit the
+  same;
 * against the REFERENCE (tests/golden pvnet2, weight seed 29): within the
   north star's 1e-4, as the full forward;
 * at weights x3 (larger activations and differences) within 1e-4 of torch fp32.
@@ -19,29 +19,14 @@ import pytest
 
 from conftest import SEED, golden
 from gzero import boards, weights
-from test_gpu_pvinc import _concat, _grand_family, _root_family, _rows
+from test_gpu_pvinc import _close, _concat, _grand_family, _root_family, _rows
 
 pytestmark = pytest.mark.gpu
-
-DELTA_TOL = 2e-5
-
 
 @pytest.fixture(scope="module")
 def pvw():
     from gzero.device import PVWeights
     return PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision="f16x3")
-
-
-def _close(full, got, n, exact_rows=(), tol=DELTA_TOL):
-    lg, v, p, pr = (np.asarray(x).reshape(n, -1) for x in got[:4])
-    flg, fv, fp, fpr = (np.asarray(x).reshape(n, -1) for x in full[:4])
-    err = {"logits": np.abs(lg - flg).max(), "value": np.abs(v - fv).max(), "probs": np.abs(p - fp).max(),
-           "prior": np.abs(pr - fpr).max()}
-    assert err["logits"] < tol and err["value"] < tol, err
-    assert err["probs"] < 1e-6 and err["prior"] < 1e-6, err
-    for i in exact_rows:
-        assert np.array_equal(lg[i], flg[i]) and np.array_equal(v[i], fv[i]) and np.array_equal(pr[i], fpr[i]), i
-    return err
 
 
 def test_delta_children_on_every_cell(pvw):
@@ -67,28 +52,10 @@ def test_delta_children_on_every_cell(pvw):
             meta.append(-2)
     rows = _rows(cells)
     full = device.pv_forward(pvw, rows, want_prior=True)
-    tree = device.pv_forward_tree(pvw, rows, meta, mode="delta")
+    tree = device.pv_forward_tree(pvw, rows, meta)
     assert tree[4] == [3, 3, len(cells) - 3 - 15, 15, 0, 0]
     err = _close(full, tree, len(cells), exact)
     print("delta vs full:", err)
-
-
-def test_delta_grandchildren(pvw):
-    """Grandchildren around parents at corners, edges and the centre: the parents'
-    patches hold the child values the delta kernel computed, the grandchildren run
-    pv_sib_kernel<true> on them -- within DELTA_TOL of the full forward."""
-    from gzero import device
-    rng = np.random.default_rng(SEED + 2)
-    corners = [0, 14, 210, 224]
-    fams = [_grand_family(rng, 6, corners + [112, 113, 97]),
-            _grand_family(rng, 41, [7, 105, 119, 217, 16], every=2),
-            _grand_family(rng, 120, list(range(0, 225, 11)), every=5)]
-    cells, meta = _concat(fams)
-    rows = _rows(cells)
-    full = device.pv_forward(pvw, rows, want_prior=True)
-    tree = device.pv_forward_tree(pvw, rows, meta, mode="delta")
-    assert tree[4][4] > 0
-    _close(full, tree, len(cells))
 
 
 @pytest.mark.parametrize("planner", [False, True])
@@ -102,7 +69,7 @@ def test_delta_forward_of_real_searches(pvw, planner):
     if planner:
         gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
         kw = dict(n_slots=64, beta=0.2, planner_steps=2, gn_weights=gnw)
-    eng = SelfPlayEngine(num_simulations=200, seed=SEED, pv_weights=pvw, plies_per_step=1, pv_mode="delta", **kw)
+    eng = SelfPlayEngine(num_simulations=200, seed=SEED, pv_weights=pvw, plies_per_step=1, pv_mode="tree", **kw)
     eng.advance(60 if not planner else 40)
     for _ in range(2):
         eng.step()
@@ -130,7 +97,7 @@ def test_delta_pvnet2_vs_reference(oracle):
     rows, cells = _fixture_rows(oracle, g)
     n = len(cells)
     meta = np.array([c["parent"] for c in g["cases"]], np.int32)
-    tree = device.pv_forward_tree(w, rows, meta, mode="delta")
+    tree = device.pv_forward_tree(w, rows, meta)
     roots = int((meta == -1).sum())
     assert tree[4][2] == 12 * roots and tree[4][4] == 5 * roots, tree[4]
     lg, v, pr, prior = tree[:4]
@@ -160,7 +127,7 @@ def test_delta_scaled_weights_vs_torch(scale):
     rng = np.random.default_rng(SEED + 9)
     cells, meta = _concat([_grand_family(rng, 30, [0, 112, 200], every=3), _grand_family(rng, 90, [14, 60], every=4)])
     rows = _rows(cells)
-    tree = device.pv_forward_tree(w, rows, meta, mode="delta")
+    tree = device.pv_forward_tree(w, rows, meta)
     ref_lg, ref_v = weights.reference_forward(sd, boards.planes_from_cells(np.asarray(cells, np.int8)))
     lscale = max(1.0, float(np.abs(ref_lg).max()))  # as test_gpu_pvnet.test_pv_scaled_conv_weights
     assert np.abs(tree[0] - ref_lg).max() < 1e-4 * lscale, (np.abs(tree[0] - ref_lg).max(), lscale)

@@ -1,15 +1,18 @@
-"""Incremental policy-value forward (gz_pv_forward_tree, csrc/gz_pvinc.hip).
+"""Incremental policy-value forward (gz_pv_forward_tree: csrc/gz_pvdg.hip for the
+root children, csrc/gz_pvinc.hip for the grandchildren and the classification).
 
-A root child recomputes only the windows around its new stone from the root's
-stored maps; every recomputed position takes the full kernel's products in the
-full kernel's order, so the outputs -- logits, value, softmax, masked prior --
-must equal the full forward's (gz_pv_forward, f16x3) BIT FOR BIT, for children
-on every cell (corners and edges clip the windows), several roots in one launch,
-grandchildren (a child of a root child: its windows come from the root's maps
-overlaid with the parent's recomputed squares) on every cell around parents at
-corners, edges and the centre, deeper nodes (full forward), roots beyond the map
-capacity and parents beyond the patch capacity (full forward), and the leaves of
-real 200-simulation searches.
+Roots and every board the tree forward runs through the full kernel (untagged nodes,
+roots beyond the map capacity and their children, children of parents beyond the
+patch capacity, wrongly tagged nodes) must equal the full forward (gz_pv_forward,
+f16x3) BIT FOR BIT.  Root children are the root's pre-BN accumulators plus the
+convolution of their input differences and grandchildren are computed from their
+parent's recomputed squares: the same network in the same f16x3 arithmetic, the
+additions in another order, so they are compared within the tolerance stated here:
+logits and value within DELTA_TOL = 2e-5 of the full forward (measured ~2e-7),
+softmax and the fp64 masked prior within 1e-6.  Covered: grandchildren on every
+cell around parents at corners, edges and the centre, both capacity fallbacks and
+wrong tags; children on every cell, real searches and the reference fixtures are in
+tests/test_gpu_pvdelta.py.
 """
 import numpy as np
 import pytest
@@ -32,8 +35,29 @@ def _rows(cells):
     return boards.leaf_words(bl, wh)
 
 
-def _same(a, b):
-    return all(np.array_equal(x, y) for x, y in zip(a, b))
+DELTA_TOL = 2e-5
+
+
+def _close(full, got, n, exact_rows=(), tol=DELTA_TOL):
+    """Every row within the tolerance; the rows in exact_rows bitwise."""
+    lg, v, p, pr = (np.asarray(x).reshape(n, -1) for x in got[:4])
+    flg, fv, fp, fpr = (np.asarray(x).reshape(n, -1) for x in full[:4])
+    err = {"logits": np.abs(lg - flg).max(), "value": np.abs(v - fv).max(), "probs": np.abs(p - fp).max(),
+           "prior": np.abs(pr - fpr).max()}
+    assert err["logits"] < tol and err["value"] < tol, err
+    assert err["probs"] < 1e-6 and err["prior"] < 1e-6, err
+    for i in exact_rows:
+        assert np.array_equal(lg[i], flg[i]) and np.array_equal(v[i], fv[i]) and np.array_equal(p[i], fp[i]) \
+            and np.array_equal(pr[i], fpr[i]), i
+    return err
+
+
+def _bitwise_rows(full, got, n):
+    """How many rows equal the full forward bit for bit on every output."""
+    eq = np.ones(n, bool)
+    for a, b in zip(full[:4], got[:4]):
+        eq &= np.all(np.asarray(a).reshape(n, -1) == np.asarray(b).reshape(n, -1), axis=1)
+    return int(eq.sum())
 
 
 def _root_family(rng, n_stones, mover=None):
@@ -49,34 +73,6 @@ def _root_family(rng, n_stones, mover=None):
         k[c] = mover
         kids.append(k)
     return cells, kids
-
-
-def test_tree_children_on_every_cell_bitwise(pvw):
-    """3 roots (4, 40 and 150 stones) with a child on every empty cell, plus deeper
-    nodes: tree forward == full forward, bitwise, on every output."""
-    from gzero import device
-    rng = np.random.default_rng(SEED)
-    cells, meta = [], []
-    for ns in (4, 40, 150):
-        root, kids = _root_family(rng, ns)
-        r = len(cells)
-        cells.append(root)
-        meta.append(-1)
-        cells += kids
-        meta += [r] * len(kids)
-        for k in kids[:5]:  # untagged grandchildren (meta -2) -> full forward
-            g = k.copy()
-            g[np.flatnonzero(g == 0)[0]] = 3 - (1 if ns % 2 == 0 else 2)
-            cells.append(g)
-            meta.append(-2)
-    rows = _rows(cells)
-    full = device.pv_forward(pvw, rows, want_prior=True)
-    tree = device.pv_forward_tree(pvw, rows, meta)
-    assert tree[4] == [3, 3, len(cells) - 3 - 15, 15, 0, 0]
-    for name, a, b in zip(("logits", "value", "probs", "prior"), full, tree[:4]):
-        bad = np.flatnonzero(~np.all(np.asarray(a).reshape(len(cells), -1) == np.asarray(b).reshape(len(cells), -1),
-                                     axis=1))
-        assert len(bad) == 0, (name, bad[:10], np.abs(np.asarray(a) - np.asarray(b)).max())
 
 
 def _grand_family(rng, n_stones, parent_cells, every=1):
@@ -110,10 +106,11 @@ def _concat(fams):
     return cells, meta
 
 
-def test_tree_grandchildren_every_cell_bitwise(pvw):
+def test_tree_grandchildren_every_cell(pvw):
     """Grandchildren on every empty cell around parents at the corners, edges, next
     to each other and in the centre (parent and grandchild windows overlap, clip,
-    or are disjoint), under 3 roots: tree forward == full forward, bitwise."""
+    or are disjoint), under 3 roots: within DELTA_TOL of the full forward, roots
+    bitwise."""
     from gzero import device
     rng = np.random.default_rng(SEED + 2)
     corners = [0, 14, 210, 224]
@@ -129,15 +126,13 @@ def test_tree_grandchildren_every_cell_bitwise(pvw):
     full = device.pv_forward(pvw, rows, want_prior=True)
     tree = device.pv_forward_tree(pvw, rows, meta)
     assert tree[4] == [3, 3, n_kids, 0, n_grand, n_par], (tree[4], n_kids, n_grand, n_par)
-    for name, a, b in zip(("logits", "value", "probs", "prior"), full, tree[:4]):
-        bad = np.flatnonzero(~np.all(np.asarray(a).reshape(len(cells), -1) == np.asarray(b).reshape(len(cells), -1),
-                                     axis=1))
-        assert len(bad) == 0, (name, bad[:10], np.abs(np.asarray(a) - np.asarray(b)).max())
+    print("grandchildren vs full:", _close(full, tree, len(cells), np.flatnonzero(meta_a == -1)))
 
 
 def test_tree_patch_capacity_fallback(pvw):
     """More parents with grandchildren than patch slots (16 per map slot): the
-    grandchildren of parents without a slot take the full forward; results unchanged."""
+    grandchildren of parents without a slot take the full forward (bitwise), the
+    rest within DELTA_TOL."""
     from gzero import device
     rng = np.random.default_rng(SEED + 3)
     cells, meta = _concat([_grand_family(rng, 30, list(range(0, 225, 3)), every=60)])
@@ -149,12 +144,13 @@ def test_tree_patch_capacity_fallback(pvw):
     tree = device.pv_forward_tree(pvw, rows, meta, root_cap=1)
     st = tree[4]
     assert st[5] == n_par and 0 < st[4] < n_grand and st[3] == n_grand - st[4], st
-    assert _same(full, tree[:4])
+    _close(full, tree, len(cells))
+    assert _bitwise_rows(full, tree, len(cells)) >= st[1] + st[3]
 
 
 def test_tree_root_capacity_fallback(pvw):
     """root_cap smaller than the number of roots: the roots without a map slot and
-    their children take the full forward; results unchanged."""
+    their children take the full forward (bitwise), the rest within DELTA_TOL."""
     from gzero import device
     rng = np.random.default_rng(SEED + 1)
     cells, meta = [], []
@@ -168,63 +164,17 @@ def test_tree_root_capacity_fallback(pvw):
     rows = _rows(cells)
     full = device.pv_forward(pvw, rows, want_prior=True)
     tree = device.pv_forward_tree(pvw, rows, meta, root_cap=1)
-    assert tree[4][0] == 3 and tree[4][1] == 1
-    assert _same(full, tree[:4])
-
-
-def test_tree_forward_of_real_searches_bitwise(pvw):
-    """The leaves of 200-simulation searches of 256 self-play slots after a burn-in
-    (root children in the parallel phase, deeper nodes in the sequential phase):
-    the engine's tree forward equals the full forward of the same leaves, bitwise."""
-    from gzero import device
-    from gzero.selfplay import SelfPlayEngine
-    eng = SelfPlayEngine(n_slots=256, num_simulations=200, beta=0.0, seed=SEED, pv_weights=pvw, plies_per_step=1,
-                         pv_mode="tree")
-    eng.advance(60)
-    for _ in range(2):
-        eng.step()
-        c = eng.counters()
-        n = int(c["leaves"])
-        assert c["leaves_dropped"] == 0 and 0 < n <= eng.leaf_cap
-        st = eng.tree_stats()
-        assert st[1] == st[0] and st[1] + st[2] + st[3] + st[4] == n and st[2] > 0.5 * n
-        assert st[4] > 0  # grandchildren of parents with a patch slot
-        rows = eng.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
-        full = device.pv_forward(pvw, rows, want_prior=True)
-        got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),
-               eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225), eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225))
-        assert _same(full, got)
-
-
-def test_tree_forward_of_planner_searches_bitwise(pvw):
-    """Config-4 searches (BG-planner rollout plies, beta 0.2): the planner pipeline
-    tags its leaves like the fused search (root, root children, their children), and
-    the engine's tree forward equals the full forward of the same leaves, bitwise."""
-    from gzero import device, planner_nets
-    from gzero.selfplay import SelfPlayEngine
-    gnw = planner_nets.pack_planner_weights(planner_nets.init_graphnet_state(0), planner_nets.init_dqn_state(1))
-    eng = SelfPlayEngine(n_slots=64, num_simulations=200, beta=0.2, seed=SEED, pv_weights=pvw, plies_per_step=1,
-                         planner_steps=2, gn_weights=gnw, pv_mode="tree")
-    eng.advance(40)
-    for _ in range(2):
-        eng.step()
-        c = eng.counters()
-        n = int(c["leaves"])
-        assert c["leaves_dropped"] == 0 and 0 < n <= eng.leaf_cap
-        st = eng.tree_stats()
-        assert st[1] == st[0] > 0 and st[1] + st[2] + st[3] + st[4] == n and st[2] > 0.5 * n and st[4] > 0, st
-        rows = eng.d_leaves[: n * 16].cpu().numpy().view(np.uint32).reshape(n, 16)
-        full = device.pv_forward(pvw, rows, want_prior=True)
-        got = (eng.d_logits[: n * 225].cpu().numpy().reshape(n, 225), eng.d_value[:n].cpu().numpy(),
-               eng.d_probs[: n * 225].cpu().numpy().reshape(n, 225), eng.d_prior[: n * 225].cpu().numpy().reshape(n, 225))
-        assert _same(full, got)
+    st = tree[4]
+    assert st[0] == 3 and st[1] == 1 and st[2] > 0 and st[3] > 0, st
+    _close(full, tree, len(cells))
+    assert _bitwise_rows(full, tree, len(cells)) >= st[1] + st[3]
 
 
 def test_tree_wrong_tags_take_the_full_forward(pvw):
     """The tags are the caller's claim: a 'child' two stones from its root, a
     'grandchild' of such a node, and a node tagged with a non-root, non-child
-    parent take the full forward -- the outputs stay bitwise those of the full
-    forward; only the valid children are incremental."""
+    parent take the full forward -- their outputs stay bitwise those of the full
+    forward; only the valid children and grandchild are incremental (DELTA_TOL)."""
     from gzero import device
     rng = np.random.default_rng(SEED + 4)
     root, kids = _root_family(rng, 20)
@@ -257,4 +207,4 @@ def test_tree_wrong_tags_take_the_full_forward(pvw):
     tree = device.pv_forward_tree(pvw, rows, meta)
     st = tree[4]
     assert st[:5] == [1, 1, 40, 10 + 3 + 1, 1], st
-    assert _same(full, tree[:4])
+    _close(full, tree, len(cells), [0] + bad + list(range(len(cells) - 5, len(cells) - 2)) + [len(cells) - 1])

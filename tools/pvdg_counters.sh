@@ -5,7 +5,7 @@ set -e
 export TMPDIR=/tmp
 out=$1; shift
 mkdir -p "$out"
-args="--mode delta --iters 2 --check 0 --burn-in 300"
+args="--iters 2 --check 0 --burn-in 300"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- python3 tools/pvinc_bench.py $args > "$out/trace.txt" 2>&1
 run() { k=$1; shift; timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "$out/p$k" -o run -- python3 tools/pvinc_bench.py $args > "$out/p$k.txt" 2>&1; }
 run 1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE

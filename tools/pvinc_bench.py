@@ -5,8 +5,8 @@ Plays --burn-in plies on --slots self-play slots (200 sims, no PV), then one
 step with the leaves gathered and tagged, and runs the tree forward (and, with
 --full, the full forward) --iters times on those same leaves.  Prints the list
 sizes, ms per launch and the bitwise check of the last launch against the full
-forward (--check).  Used with rocprofv3 (--kernel-trace / --pmc) to isolate
-pv_child_kernel.
+forward (--check: within 2e-5).  Used with rocprofv3 (--kernel-trace / --pmc) to
+isolate pv_dg_kernel / pv_sib_kernel.
 """
 import argparse
 import os
@@ -31,8 +31,6 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--full", action="store_true", help="also time the full forward")
     ap.add_argument("--check", type=int, default=1)
-    ap.add_argument("--mode", default="exact", choices=["exact", "delta", "both"],
-                    help="tree mode(s) timed; delta is checked within 2e-5 of the full forward")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     w = PVWeights(weights.pack_pv_weights(weights.init_state_dict(0)), precision="f16x3")
@@ -48,15 +46,10 @@ def main():
     lib = eng.lib
     d_count = eng.d_counters[4:8]
 
-    def tree_of(mode):
-        def run():
-            _lib.check(lib.gz_pv_forward_tree_mode(ptr(w.tensor), ptr(eng.d_leaves), ptr(eng.d_meta), eng.leaf_cap,
-                                                   ptr(d_count), eng.root_cap, ptr(eng.d_logits), ptr(eng.d_value),
-                                                   ptr(eng.d_probs), ptr(eng.d_prior), ptr(eng.d_tree_ws), mode,
-                                                   stream()), "tree")
-        return run
-    modes = ["exact", "delta"] if a.mode == "both" else [a.mode]
-    tree = tree_of(_lib.GZ_TREE_DELTA if modes[-1] == "delta" else _lib.GZ_TREE_EXACT)
+    def tree():
+        _lib.check(lib.gz_pv_forward_tree(ptr(w.tensor), ptr(eng.d_leaves), ptr(eng.d_meta), eng.leaf_cap,
+                                          ptr(d_count), eng.root_cap, ptr(eng.d_logits), ptr(eng.d_value),
+                                          ptr(eng.d_probs), ptr(eng.d_prior), ptr(eng.d_tree_ws), stream()), "tree")
 
     def timed(fn, label):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -83,50 +76,42 @@ def main():
     dg_names = ["chunk start (units, conv0, y1 rows)", "rows of the next pass", "y1 k-loop", "x1 k-loop",
                 "y2 k-loop", "x2 k-loop", "barrier after the k-loop", "y1 epilogue", "x1 epilogue", "y2 epilogue",
                 "x2 epilogue + heads", "store drain + barrier", "records", "fill + barrier"]
-    outs = {}
     tiles = torch.zeros(2, dtype=torch.int32, device="cuda")
     sib_names = ["select nodes", "window fills (not overlapped)", "conv0", "y1 k-loop", "y1 barrier + next fill",
                  "y1 epilogue", "x1 k-loop", "x1 barrier + next fill", "x1 epilogue", "y2 k-loop",
                  "y2 barrier + next fill", "y2 epilogue", "x2 k-loop", "x2 barrier + next fill",
                  "x2 epilogue + heads", "record"]
-    delta_names = ["units", "im2col + conv0 + D(x0)", "exposed fills", "y1 k-loop", "x1 k-loop", "y2 k-loop",
-                   "x2 k-loop", "k-loop barrier", "y1 epilogue", "x1 epilogue", "y2 epilogue",
-                   "x2 epilogue + heads", "record", "end-of-pass barrier"]
-    for m in modes:
-        run = tree_of(_lib.GZ_TREE_DELTA if m == "delta" else _lib.GZ_TREE_EXACT)
-        timed(run, f"tree ({m})")
+    run = tree
+    timed(run, "tree")
+    torch.cuda.synchronize()
+    out = [t[: n * k].clone() for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225),
+                                           (eng.d_prior, 225))]
+    _lib.check(lib.gz_pv_tree_exec_tiles(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tiles), stream()), "tiles")
+    t2 = [int(x) for x in tiles.cpu()]
+    print(f"  executed 16-row tile-taps: children {t2[0]} ({t2[0] / max(1, st_kids):.1f} per child), "
+          f"grandchildren {t2[1]}", flush=True)
+    if dgst:
+        lib.gz_pvdg_stamps_read(dst.ctypes.data, 1)
+        run()
         torch.cuda.synchronize()
-        outs[m] = [t[: n * k].clone() for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225),
-                                                   (eng.d_prior, 225))]
-        _lib.check(lib.gz_pv_tree_exec_tiles(ptr(eng.d_tree_ws), eng.leaf_cap, ptr(tiles), stream()), "tiles")
-        t2 = [int(x) for x in tiles.cpu()]
-        print(f"  executed 16-row tile-taps: children {t2[0]} ({t2[0] / max(1, st_kids):.1f} per child), "
-              f"grandchildren {t2[1]}", flush=True)
-        if dgst and m == "delta":
-            lib.gz_pvdg_stamps_read(dst.ctypes.data, 1)
-            run()
-            torch.cuda.synchronize()
-            lib.gz_pvdg_stamps_read(dst.ctypes.data, 0)
-            kids = max(1, int(dst[16]))
-            vals = [int(x) for x in dst[: len(dg_names)]]
-            tot = sum(vals)
-            print(f"  stamps, workgroup 0 children (pv_dg_kernel): {kids} nodes, {tot / kids:.0f} ticks per node")
-            for i, x in enumerate(dg_names):
-                print(f"    {x:36s} {vals[i] / kids:9.0f}  {vals[i] / max(1, tot) * 100:5.1f}%")
-        if stamps:
-            lib.gz_pvinc_stamps_read(st.ctypes.data, 1)
-            run()
-            torch.cuda.synchronize()
-            lib.gz_pvinc_stamps_read(st.ctypes.data, 0)
-            for label, base, nm, cnt in (("children (pv_sib_kernel)" if m == "exact" else "children (pv_delta_kernel)",
-                                          0 if m == "exact" else 16, sib_names if m == "exact" else delta_names,
-                                          32 if m == "exact" else 33),):
-                kids = max(1, int(st[cnt]))
-                vals = [int(x) for x in st[base: base + len(nm)]]
-                tot = sum(vals)
-                print(f"  stamps, workgroup 0 {label}: {kids} nodes, {tot / kids:.0f} ticks per node")
-                for i, x in enumerate(nm):
-                    print(f"    {x:30s} {vals[i] / kids:9.0f}  {vals[i] / max(1, tot) * 100:5.1f}%")
+        lib.gz_pvdg_stamps_read(dst.ctypes.data, 0)
+        kids = max(1, int(dst[16]))
+        vals = [int(x) for x in dst[: len(dg_names)]]
+        tot = sum(vals)
+        print(f"  stamps, workgroup 0 children (pv_dg_kernel): {kids} nodes, {tot / kids:.0f} ticks per node")
+        for i, x in enumerate(dg_names):
+            print(f"    {x:36s} {vals[i] / kids:9.0f}  {vals[i] / max(1, tot) * 100:5.1f}%")
+    if stamps:
+        lib.gz_pvinc_stamps_read(st.ctypes.data, 1)
+        run()
+        torch.cuda.synchronize()
+        lib.gz_pvinc_stamps_read(st.ctypes.data, 0)
+        gk = max(1, int(st[32]))
+        vals = [int(x) for x in st[: len(sib_names)]]
+        tot = sum(vals)
+        print(f"  stamps, workgroup 0 grandchildren (pv_sib_kernel): {gk} nodes, {tot / gk:.0f} ticks per node")
+        for i, x in enumerate(sib_names):
+            print(f"    {x:30s} {vals[i] / gk:9.0f}  {vals[i] / max(1, tot) * 100:5.1f}%")
     if a.full or a.check:
         ws = w.workspace_for(eng.leaf_cap)
 
@@ -140,21 +125,12 @@ def main():
             full()
         torch.cuda.synchronize()
         ref = [t[: n * k] for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225), (eng.d_prior, 225))]
-        ok = True
-        for m, out in outs.items():
-            if m == "exact":
-                same = all(torch.equal(x, y) for x, y in zip(out, ref))
-                print(f"exact: bitwise equal to the full forward: {same}", flush=True)
-                ok &= same
-            else:
-                err = [float((x.double() - y.double()).abs().max()) for x, y in zip(out, ref)]
-                good = err[0] < 2e-5 and err[1] < 2e-5 and err[2] < 1e-6 and err[3] < 1e-6
-                print(f"delta: max |diff| vs the full forward: logits {err[0]:.2e} value {err[1]:.2e} "
-                      f"probs {err[2]:.2e} prior {err[3]:.2e} -> {'ok' if good else 'FAIL'}", flush=True)
-                ok &= good
-        if not ok:
+        err = [float((x.double() - y.double()).abs().max()) for x, y in zip(out, ref)]
+        good = err[0] < 2e-5 and err[1] < 2e-5 and err[2] < 1e-6 and err[3] < 1e-6
+        print(f"tree: max |diff| vs the full forward: logits {err[0]:.2e} value {err[1]:.2e} "
+              f"probs {err[2]:.2e} prior {err[3]:.2e} -> {'ok' if good else 'FAIL'}", flush=True)
+        if not good:
             sys.exit(1)
-
 
 if __name__ == "__main__":
     main()
