@@ -179,6 +179,64 @@ __device__ __forceinline__ int set_rank(int b) {
     return b == 7 ? 0 : (b == 3 ? 1 : (b == 1 ? 2 : (b == 6 ? 3 : (b == 2 ? 4 : 5))));
 }
 
+// Bank spreading inside the class buckets.  A tile's fragment read (ds_read_b128) is
+// conflict-free when its 16 rows' image slots are distinct mod 16 (16-B bank groups; the
+// 4 channel-group planes start at bank 0 and the lane groups mix rows of two planes), for
+// every tap at once, since a tap adds the same offset to every row's slot.  The counting
+// sort leaves a bucket in atomic order, so its 16-row windows repeat residues (a square
+// row of w interior positions is followed by the next one S = w + 2 slots on: 2-way
+// conflicts on every few rows).  Here each bucket of more than 16 rows is reordered by
+// (occurrence of the residue, residue): every 16-row window inside a level then holds
+// distinct residues.  One wave per pass; the order inside a bucket changes no tile's taps.
+__device__ __forceinline__ void dg_rows_spread(uint32_t* rt0, const uint32_t* starts, const uint32_t* mk0, int tid) {
+    const int w = tid >> 6, ln = tid & 63;
+    const uint64_t lt = (ln == 0) ? 0ull : (~0ull >> (64 - ln));
+    for (int p = w; p < K::NPASS; p += NTD / 64) {
+        const int L = p >= K::pb(3) ? 3 : (p >= K::pb(2) ? 2 : (p >= K::pb(1) ? 1 : 0));
+        const int S = dg_s(L), SS = dg_ss(L);
+        const int total = (int)mk0[p * 16 + 9];
+        uint32_t* rt = rt0 + p * K::ROWS;
+        for (int k = 0; k < K::NKEY; k++) {
+            const int b0 = (int)starts[p * K::NKEY + k];
+            const int b1 = k + 1 < K::NKEY ? (int)starts[p * K::NKEY + k + 1] : total;
+            if (b1 - b0 <= 16) continue;  // wave-uniform
+            constexpr int RND = (K::ROWS + 63) / 64;
+            uint32_t e[RND];
+            int r[RND], j[RND];
+#pragma unroll
+            for (int q = 0; q < RND; q++) {
+                const int idx = b0 + q * 64 + ln;
+                e[q] = idx < b1 ? rt[idx] : 0u;
+                const int base = (int)(e[q] & 15u) * SS + ((int)((e[q] >> 4) & 15u) - 1) * S + ((int)((e[q] >> 8) & 15u) - 1);
+                r[q] = idx < b1 ? ((base + 32) & 15) : -1;
+                j[q] = 0;
+            }
+            int cnt = 0;  // lane v < 16: the bucket's rows with residue v
+#pragma unroll
+            for (int v = 0; v < 16; v++) {
+                int acc = 0;
+#pragma unroll
+                for (int q = 0; q < RND; q++) {
+                    const uint64_t m = __ballot(r[q] == v);
+                    if (r[q] == v) j[q] = acc + __popcll(m & lt);
+                    acc += __popcll(m);
+                }
+                if (ln == v) cnt = acc;
+            }
+#pragma unroll
+            for (int q = 0; q < RND; q++) {
+                int pos = 0;
+#pragma unroll
+                for (int v = 0; v < 16; v++) {
+                    const int c = __shfl(cnt, v);
+                    pos += (c < j[q] ? c : j[q]) + (v < r[q] && c > j[q] ? 1 : 0);
+                }
+                if (r[q] >= 0) rt[b0 + pos] = e[q];
+            }
+        }
+    }
+}
+
 // The row tables of every pass of the chunk (nodes U[0, ng)), counting-sorted by class,
 // then per pass and tap the tiles that need it.  Ends with the tables written but NOT
 // published (the caller's next barrier does).
@@ -289,17 +347,11 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
-#ifdef GZ_PVDG_PROBE_W  // (wrong results) every weight load from one 4 KB, L1-resident
-        ks = 0;
-#endif
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     auto addr = [&](int tap, uint32_t r) -> int {
         const int toff = (tap / 3 - 1) * S + (tap - (tap / 3) * 3 - 1);
         const bool v = (r >> (16 + tap)) & 1u;
-#ifdef GZ_PVDG_PROBE_L  // (wrong results) conflict-free fragment reads: row li at slot li
-        return lb + ((lane & 15) + 16 * (tap & 3)) * 16 + 0 * v * toff;
-#endif
         return lb + (v ? (int)(r & 0xffffu) - 32 + toff : ZIDX) * 16;
     };
     // Units of two k-steps (a tap's channels 0-63 or 64-127): per tile 12 MFMAs behind one
@@ -363,11 +415,6 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
                 }
                 if (h == 1) ad[m] = addr(tap + 1, ri[m]);  // tile m is read for this tap: the next tap's address
                 if ((tm >> m) & 1u) {
-#ifdef GZ_PVDG_PROBE_M  // (wrong results) no MFMAs: the loop's skeleton (reads kept alive)
-#pragma unroll
-                    for (int k2 = 0; k2 < 2; k2++) c[0][m][0] += (float)fh[pm][k2][0] + (float)fl[pm][k2][0] + (float)b[2 * h + k2][0][0][0];
-                    continue;
-#endif
 #pragma unroll
                     for (int k2 = 0; k2 < 2; k2++) {
                         const int sl = 2 * h + k2;
@@ -423,12 +470,10 @@ __device__ __forceinline__ void put_hl_lds(_Float16* p, int plane_halves, const 
 //   child = relu(z + s * acc + D_skip),  root = relu(z),  D = child - root
 // into the node's D square of map L + 1 (its patch: the child value); x2 reduces the
 // child values into the 1x1 heads' partial sums (hpart, per wave) instead.  Rows in
-// groups of GB tiles, loads a group ahead; mid() (the next pass's fill, when it does
-// not read this pass's squares) runs once the first group's loads are issued, so
-// that only later loads queue behind its LDS-DMA.
-template <int L, class Mid>
-__device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const uint32_t* rt, const float* __restrict__ W,
-                                            int np, int lane, const f32x4 (&acc)[2][K::NMAX], int nt, Mid&& mid) {
+// groups of GB tiles, loads ST - 1 groups ahead.
+template <int L>
+__device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const uint32_t* rt, int np, int lane,
+                                            const f32x4 (&acc)[2][K::NMAX], int nt) {
     constexpr int RO = L + 2, SO = dg_so(L), SSO = SO * SO;
     constexpr bool SKIP = L == 1 || L == 3;
     constexpr int RS = L == 1 ? 1 : 3, SK = 2 * RS + 1, SSK = SK * SK;
@@ -475,8 +520,9 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
             }
         }
     };
-    loads(0, 0);
-    mid();
+#pragma unroll
+    for (int grp = 0; grp < ST - 1; grp++)
+        if (grp * GB < nt) loads(grp, grp);
 #pragma unroll
     for (int grp = 0; grp < NGRP; grp++) {
         if (grp * GB >= nt) break;
@@ -844,46 +890,48 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             st(2 + L);
             __syncthreads();  // every wave is past the k-loop: the image is free
             st(6);
-            // the next non-empty pass; its fill goes under this epilogue unless it reads
-            // squares this pass writes (the next layer over some of the same nodes)
+            // the next non-empty pass (its fill follows the epilogue: issued under it, the
+            // epilogue's loads would wait for the fill's LDS-DMA -- measured slower)
             int q = p + 1, L2 = 0, v0 = 0, g2 = 0;
             for (; q < K::NPASS; q++) {
                 dg_pass_of(q, ng, L2, v0, g2);
                 if (g2 > 0) break;
             }
             const bool more = q < K::NPASS;
-            // (issuing it under the epilogue, when it reads no square this pass writes, made
-            // the epilogue's later loads queue behind its LDS-DMA: measured slower)
-            const bool pre = false;
-            auto fill = [&]() {
+            if (L == 0) dg_epilogue<0>(lds, U + u0, rt, np, t & 63, acc, nt);
+            else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, np, t & 63, acc, nt);
+            else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, np, t & 63, acc, nt);
+            else dg_epilogue<3>(lds, U + u0, rt, np, t & 63, acc, nt);
+            st(7 + L);
+            // vmcnt counts loads, stores and LDS-DMA together in issue order, so each wait
+            // below also waits for every older store.  The next pass's fill reads, by
+            // LDS-DMA, squares that older passes stored -- and this pass's only when it is
+            // the next layer over some of the same nodes (y1 -> the first x1 pass): then
+            // every wave's stores complete before a barrier first.  x2: the barrier
+            // publishes hpart for the record.
+            const bool reads_mine = more && L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2;
+            if (reads_mine) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (reads_mine || L == 3) __syncthreads();
+            st(11);
+            // the fill goes out first; an x2 pass's record (the root's record loaded, the
+            // node's written) follows, its loads in flight with the fill's
+            if (more) {
                 if (L2 == 1) dg_fill<1>(lds, U + v0, g2, t);
                 else if (L2 == 2) dg_fill<2>(lds, U + v0, g2, t);
                 else if (L2 == 3) dg_fill<3>(lds, U + v0, g2, t);
-            };
-            auto mid = [&]() {
-                if (pre) fill();
-            };
-            if (L == 0) dg_epilogue<0>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
-            else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
-            else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
-            else dg_epilogue<3>(lds, U + u0, rt, Wp, np, t & 63, acc, nt, mid);
-            st(7 + L);
-            // every wave's square stores (and a prefetched fill) complete before the barrier:
-            // the next fill reads the squares by LDS-DMA, the next k-loop the image
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // the squares are stored; hpart is complete
-            st(11);
+            }
             if (L == 3) {  // (the root's record entries loaded here: held across the epilogue they were spilled)
                 float rec[REC_K];
                 dg_record_load(U[u0], A.hbuf, rec, t);
                 dg_record(U[u0], 0, (const float*)(lds + K::CST) + 896, A.hbuf, (const float*)(lds + K::HP), rec, t);
+                // every thread stores >= 2 record entries after the fill: all but the 2
+                // youngest operations done = the fill landed
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             st(12);
-            if (more && !pre) {
-                fill();
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();  // the image has landed
-            }
+            __syncthreads();  // the image has landed (and hpart is free again)
             st(13);
         }
     }

@@ -880,6 +880,145 @@ __global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, floa
     dw[((size_t)n * CH + c) * 9 + tap] = s;
 }
 
+// ---------------------------------------------------------------- FC heads and loss
+// training.py:292-297 over neural_network.py:150-159 (PolicyValueNet's FC heads):
+//   logits = policy_fc(pin),  h = relu(value_fc1(vin)),  val = tanh(value_fc2(h)),
+//   loss = CrossEntropy(logits, y) + MSE(val, v)     (both means over the batch)
+// and its backward down to dL/dpin, dL/dvin (the tower's backward takes it from there)
+// and the six FC parameter gradients.  fp32 throughout, sums in a fixed order.
+// Kernel 1, one workgroup per board: the forward, the board's loss terms, dlogits,
+// dL/d(value_fc1 pre-activation), dL/dpin, dL/dvin.  Kernel 2, one thread per
+// parameter: the FC weight / bias gradients as sums over the boards, and the loss.
+constexpr int FC_P_IN = 450, FC_P_OUT = 225, FC_V_IN = 225, FC_V_HID = 64;
+constexpr int FC_THREADS = 256;
+constexpr int FC_SAVE = FC_P_OUT + 2 * FC_V_HID + 4;  // dlogits, dpre1, h, dpre2, ce, se
+__device__ __forceinline__ float fc_wave_sum(float x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    return x;
+}
+__global__ __launch_bounds__(FC_THREADS) void sgd_fc_board_kernel(gz_sgd_fc fc, const float* __restrict__ pin,
+                                                                 const float* __restrict__ vin,
+                                                                 const int64_t* __restrict__ y,
+                                                                 const float* __restrict__ v, int B, float scale,
+                                                                 float* __restrict__ dpin, float* __restrict__ dvin,
+                                                                 float* __restrict__ save) {
+    __shared__ float sp[FC_P_IN], sv[FC_V_IN], lg[FC_P_OUT], hh[FC_V_HID], dl[FC_P_OUT], d1[FC_V_HID];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int k = tid; k < FC_P_IN; k += FC_THREADS) sp[k] = pin[(size_t)b * FC_P_IN + k];
+    for (int k = tid; k < FC_V_IN; k += FC_THREADS) sv[k] = vin[(size_t)b * FC_V_IN + k];
+    __syncthreads();
+    // logits and the value head's hidden layer: a wave per output, lanes over k
+    for (int i = wave; i < FC_P_OUT; i += 4) {
+        const float* w = fc.policy_weight + (size_t)i * FC_P_IN;
+        float a = 0.f;
+        for (int k = lane; k < FC_P_IN; k += 64) a = __builtin_fmaf(w[k], sp[k], a);
+        a = fc_wave_sum(a);
+        if (lane == 0) lg[i] = a + fc.policy_bias[i];
+    }
+    for (int j = wave; j < FC_V_HID; j += 4) {
+        const float* w = fc.value1_weight + (size_t)j * FC_V_IN;
+        float a = 0.f;
+        for (int k = lane; k < FC_V_IN; k += 64) a = __builtin_fmaf(w[k], sv[k], a);
+        a = fc_wave_sum(a);
+        if (lane == 0) hh[j] = fmaxf(a + fc.value1_bias[j], 0.f);
+    }
+    __syncthreads();
+    float* sb = save + (size_t)b * FC_SAVE;
+    if (wave == 0) {  // softmax cross-entropy (log-sum-exp about the max), dlogits
+        float m = -INFINITY;
+        for (int i = lane; i < FC_P_OUT; i += 64) m = fmaxf(m, lg[i]);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d));
+        float e = 0.f;
+        for (int i = lane; i < FC_P_OUT; i += 64) e += expf(lg[i] - m);
+        e = fc_wave_sum(e);
+        const int64_t yt = y[b];
+        const int t = yt >= 0 && yt < FC_P_OUT ? (int)yt : 0;  // (labels are checked by the caller)
+        const float lse = m + logf(e), g = scale / (float)B;
+        for (int i = lane; i < FC_P_OUT; i += 64) {
+            const float d = (expf(lg[i] - m) / e - (i == t ? 1.f : 0.f)) * g;
+            dl[i] = d;
+            sb[i] = d;
+        }
+        if (lane == 0) sb[FC_P_OUT + 2 * FC_V_HID + 1] = yt == t ? lse - lg[t] : NAN;
+    } else if (wave == 1) {  // value: tanh(value_fc2(h)), squared error, dpre2, dpre1
+        float a = lane < FC_V_HID ? fc.value2_weight[lane] * hh[lane] : 0.f;
+        a = fc_wave_sum(a) + fc.value2_bias[0];
+        const float val = tanhf(a), diff = val - v[b];
+        const float dpre2 = 2.f * diff * (scale / (float)B) * (1.f - val * val);
+        if (lane < FC_V_HID) {
+            const float d = hh[lane] > 0.f ? dpre2 * fc.value2_weight[lane] : 0.f;
+            d1[lane] = d;
+            sb[FC_P_OUT + lane] = d;
+            sb[FC_P_OUT + FC_V_HID + lane] = hh[lane];
+        }
+        if (lane == 0) {
+            sb[FC_P_OUT + 2 * FC_V_HID] = dpre2;
+            sb[FC_P_OUT + 2 * FC_V_HID + 2] = diff * diff;
+        }
+    }
+    __syncthreads();
+    // dL/dpin = dlogits . policy_fc.weight, dL/dvin = dpre1 . value_fc1.weight (coalesced over k)
+    for (int k = tid; k < FC_P_IN; k += FC_THREADS) {
+        float a = 0.f;
+        for (int i = 0; i < FC_P_OUT; i++) a = __builtin_fmaf(dl[i], fc.policy_weight[(size_t)i * FC_P_IN + k], a);
+        dpin[(size_t)b * FC_P_IN + k] = a;
+    }
+    for (int k = tid; k < FC_V_IN; k += FC_THREADS) {
+        float a = 0.f;
+        for (int j = 0; j < FC_V_HID; j++) a = __builtin_fmaf(d1[j], fc.value1_weight[(size_t)j * FC_V_IN + k], a);
+        dvin[(size_t)b * FC_V_IN + k] = a;
+    }
+}
+// one thread per gradient element (policy weight, policy bias, value1 weight, value1
+// bias, value2 weight, value2 bias), then one for the loss: sums over the boards in order
+constexpr int FC_NW = FC_P_OUT * FC_P_IN, FC_NB1 = FC_NW + FC_P_OUT, FC_NW1 = FC_NB1 + FC_V_HID * FC_V_IN,
+              FC_NV1B = FC_NW1 + FC_V_HID, FC_NV2 = FC_NV1B + FC_V_HID, FC_NALL = FC_NV2 + 2;
+__global__ __launch_bounds__(256) void sgd_fc_grad_kernel(const float* __restrict__ pin, const float* __restrict__ vin,
+                                                          const float* __restrict__ save, int B, gz_sgd_fc_grads gr,
+                                                          float* __restrict__ loss) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= FC_NALL) return;
+    float a = 0.f;
+    if (e < FC_NW) {
+        const int i = e / FC_P_IN, k = e - i * FC_P_IN;
+        for (int b = 0; b < B; b++) a = __builtin_fmaf(save[(size_t)b * FC_SAVE + i], pin[(size_t)b * FC_P_IN + k], a);
+        gr.policy_weight[e] = a;
+    } else if (e < FC_NB1) {
+        const int i = e - FC_NW;
+        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + i];
+        gr.policy_bias[i] = a;
+    } else if (e < FC_NW1) {
+        const int q = e - FC_NB1, j = q / FC_V_IN, k = q - j * FC_V_IN;
+        for (int b = 0; b < B; b++)
+            a = __builtin_fmaf(save[(size_t)b * FC_SAVE + FC_P_OUT + j], vin[(size_t)b * FC_V_IN + k], a);
+        gr.value1_weight[q] = a;
+    } else if (e < FC_NV1B) {
+        const int j = e - FC_NW1;
+        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + FC_P_OUT + j];
+        gr.value1_bias[j] = a;
+    } else if (e < FC_NV2) {
+        const int j = e - FC_NV1B;
+        for (int b = 0; b < B; b++)
+            a = __builtin_fmaf(save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID],
+                               save[(size_t)b * FC_SAVE + FC_P_OUT + FC_V_HID + j], a);
+        gr.value2_weight[j] = a;
+    } else if (e == FC_NV2) {
+        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID];
+        gr.value2_bias[0] = a;
+    } else {  // the loss: mean cross-entropy + mean squared error (of this batch, unscaled)
+        float ce = 0.f, se = 0.f;
+        for (int b = 0; b < B; b++) {
+            ce += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID + 1];
+            se += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID + 2];
+        }
+        loss[0] = ce / (float)B + se / (float)B;
+        loss[1] = ce / (float)B;
+        loss[2] = se / (float)B;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 struct Ws {
     _Float16* frag;
@@ -1079,4 +1218,25 @@ extern "C" int gz_sgd_backward(const gz_sgd_net* net, int32_t B, const float* d_
     sgd_conv0_reduce_kernel<<<(CH * (C0K + 1) + 255) / 256, 256, 0, s>>>(w.c0part, B, gr->conv0_weight,
                                                                          gr->conv0_bias);
     return sgd_check("gz_sgd_backward: conv0");
+}
+
+extern "C" size_t gz_sgd_fc_workspace_bytes(int32_t boards) {
+    return boards < 1 ? 0 : (size_t)boards * FC_SAVE * sizeof(float);
+}
+
+extern "C" int gz_sgd_fc_loss(const gz_sgd_fc* fc, int32_t B, const float* d_pin, const float* d_vin,
+                              const int64_t* d_y, const float* d_v, float scale, float* d_dpin, float* d_dvin,
+                              const gz_sgd_fc_grads* gr, float* d_loss, void* d_ws, void* stream) {
+    if (!fc || !gr || B < 1 || B > GZ_SGD_MAX_BOARDS || !d_pin || !d_vin || !d_y || !d_v || !d_dpin || !d_dvin ||
+        !d_loss || !d_ws)
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd_fc_loss: bad arguments");
+    if (!fc->policy_weight || !fc->policy_bias || !fc->value1_weight || !fc->value1_bias || !fc->value2_weight ||
+        !fc->value2_bias || !gr->policy_weight || !gr->policy_bias || !gr->value1_weight || !gr->value1_bias ||
+        !gr->value2_weight || !gr->value2_bias)
+        return sgd_fail(GZ_ERR_ARG, "gz_sgd_fc_loss: NULL parameter or gradient");
+    hipStream_t s = (hipStream_t)stream;
+    float* save = (float*)d_ws;
+    sgd_fc_board_kernel<<<B, FC_THREADS, 0, s>>>(*fc, d_pin, d_vin, d_y, d_v, B, scale, d_dpin, d_dvin, save);
+    sgd_fc_grad_kernel<<<(FC_NALL + 255) / 256, 256, 0, s>>>(d_pin, d_vin, save, B, *gr, d_loss);
+    return sgd_check("gz_sgd_fc_loss");
 }

@@ -94,6 +94,12 @@ class SgdGrads(ctypes.Structure):  # gz_sgd_grads
                 ("value_weight", ctypes.c_void_p), ("value_bias", ctypes.c_void_p)]
 
 
+class SgdFc(ctypes.Structure):  # gz_sgd_fc / gz_sgd_fc_grads
+    _fields_ = [("policy_weight", ctypes.c_void_p), ("policy_bias", ctypes.c_void_p),
+                ("value1_weight", ctypes.c_void_p), ("value1_bias", ctypes.c_void_p),
+                ("value2_weight", ctypes.c_void_p), ("value2_bias", ctypes.c_void_p)]
+
+
 GZ_SGD_MAX_BOARDS = 65535
 GZ_ADAM_MAX_TENSORS = 48
 
@@ -156,6 +162,9 @@ SIGNATURES = {
     "gz_sgd_forward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, _P, _P]),
     "gz_sgd_backward": (ctypes.c_int, [ctypes.POINTER(SgdNet), _I32, _P, _P, _P, ctypes.POINTER(SgdGrads), _P, _P]),
     "gz_sgd_saved": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "gz_sgd_fc_workspace_bytes": (_SZ, [_I32]),
+    "gz_sgd_fc_loss": (ctypes.c_int, [ctypes.POINTER(SgdFc), _I32, _P, _P, _P, _P, ctypes.c_float, _P, _P,
+                                      ctypes.POINTER(SgdFc), _P, _P, _P]),
 }
 
 _lib = None

@@ -7,8 +7,12 @@ BN0 + ReLU, the two residual blocks (neural_network.py:74-91), BatchNorm on batc
 statistics, and the 1x1 policy / value convs -- on the HIP kernels: f16x3 MFMA
 implicit-GEMM convolutions (forward, input and weight gradients), BatchNorm
 statistics and backward in the conv epilogues, conv0 and the 1x1 convs in fp32.
-The FC heads (policy_fc, value_fc1/2) stay torch ops; the loss, ``clip_grad_norm_``
-and Adam of ``training.train_epoch`` (training.py:277-311) are unchanged.  The
+In ``train_forward`` the FC heads (policy_fc, value_fc1/2) stay torch ops under
+autograd; ``NetStep`` runs the whole step without autograd: the tower forward, the
+FC heads + loss and their backward (gz_sgd_fc_loss) and the tower backward, the
+gradients written into every parameter's ``.grad`` (views of one flat buffer, which
+is also the data-parallel all-reduce bucket).  ``clip_grad_norm_`` and Adam of
+``training.train_epoch`` (training.py:277-311) follow (gzero.optim.DeviceAdam).  The
 BatchNorm running statistics and ``num_batches_tracked`` are updated as
 ``nn.BatchNorm2d.train()`` does.  There is no fallback: without the
 library this raises ``GzeroUnavailable``.
@@ -150,3 +154,102 @@ def train_forward(net, x):
     logits = net.policy_fc(pin)
     v = F.relu(net.value_fc1(vin))
     return logits, torch.tanh(net.value_fc2(v))
+
+
+class NetStep:
+    """One training step of PolicyValueNet (training.py:292-297: forward in training
+    mode, CrossEntropy + MSE, backward) on the device without autograd:
+    gz_sgd_forward -> gz_sgd_fc_loss -> gz_sgd_backward.  ``grads`` is one flat
+    buffer; every parameter's ``.grad`` is a view of it, overwritten by each step (no
+    zero_grad needed; gradients are never accumulated).  ``step(x, y, v, scale)``
+    returns the batch loss (a device scalar, unscaled); ``scale`` multiplies every
+    gradient (a data-parallel rank's share of the global batch)."""
+
+    def __init__(self, net):
+        _check_net(net)
+        self.net = net
+        self.lib = _lib.load()
+        self.params = list(net.parameters())
+        for p in self.params:
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                raise ValueError("gz_sgd: parameters must be contiguous float32 CUDA tensors")
+        dev = self.params[0].device
+        self.grads = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        off = 0
+        self._views = []
+        for p in self.params:
+            p.grad = self.grads[off:off + p.numel()].view_as(p)
+            self._views.append((p, p.grad))
+            off += p.numel()
+        tp = tower_params(net)
+        bns = _bns(net)
+        st, gr = _lib.SgdNet(), _lib.SgdGrads()
+        for i, bn in enumerate(bns):
+            st.bn_weight[i], st.bn_bias[i] = tp[2 * i].data_ptr(), tp[2 * i + 1].data_ptr()
+            st.bn_running_mean[i] = bn.running_mean.data_ptr() if bn.track_running_stats else None
+            st.bn_running_var[i] = bn.running_var.data_ptr() if bn.track_running_stats else None
+            gr.bn_weight[i], gr.bn_bias[i] = tp[2 * i].grad.data_ptr(), tp[2 * i + 1].grad.data_ptr()
+        for i in range(4):
+            st.conv_weight[i], st.conv_bias[i] = tp[10 + 2 * i].data_ptr(), tp[11 + 2 * i].data_ptr()
+            gr.conv_weight[i], gr.conv_bias[i] = tp[10 + 2 * i].grad.data_ptr(), tp[11 + 2 * i].grad.data_ptr()
+        for i, name in enumerate(_HEADS):
+            setattr(st, f"{name}_weight", tp[18 + 2 * i].data_ptr())
+            setattr(st, f"{name}_bias", tp[19 + 2 * i].data_ptr())
+            setattr(gr, f"{name}_weight", tp[18 + 2 * i].grad.data_ptr())
+            setattr(gr, f"{name}_bias", tp[19 + 2 * i].grad.data_ptr())
+        st.momentum = float(bns[0].momentum)
+        st.eps = float(bns[0].eps)
+        fcs = (net.policy_fc.weight, net.policy_fc.bias, net.value_fc1.weight, net.value_fc1.bias,
+               net.value_fc2.weight, net.value_fc2.bias)
+        if (tuple(fcs[0].shape) != (225, 450) or tuple(fcs[2].shape) != (64, 225)
+                or tuple(fcs[4].shape) != (1, 64)):
+            raise ValueError("gz_sgd: FC heads must be policy_fc 450 -> 225, value_fc1 225 -> 64, value_fc2 64 -> 1")
+        self.fc = _lib.SgdFc(*[t.data_ptr() for t in fcs])
+        self.fcg = _lib.SgdFc(*[t.grad.data_ptr() for t in fcs])
+        self.st, self.gr = st, gr
+        self.counts = [bn.num_batches_tracked for bn in bns if bn.track_running_stats]
+        self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
+        self._bufs = {}
+
+    def _buffers(self, B, dev):
+        b = self._bufs.get(B)
+        if b is None:
+            f32 = dict(dtype=torch.float32, device=dev)
+            b = (torch.empty(int(self.lib.gz_sgd_workspace_bytes(B)), dtype=torch.uint8, device=dev),
+                 torch.empty(int(self.lib.gz_sgd_fc_workspace_bytes(B)), dtype=torch.uint8, device=dev),
+                 torch.empty((B, 450), **f32), torch.empty((B, 225), **f32),
+                 torch.empty((B, 450), **f32), torch.empty((B, 225), **f32))
+            self._bufs[B] = b
+        return b
+
+    def _bind(self):
+        # the kernels write into the flat buffer: put the views back if something (a
+        # zero_grad(set_to_none=True)) replaced a parameter's .grad
+        for p, g in self._views:
+            if p.grad is not g:
+                p.grad = g
+
+    def zero(self):
+        self._bind()
+        self.grads.zero_()
+
+    def step(self, x, y, v, scale=1.0):
+        B = int(x.shape[0])
+        if not 1 <= B <= _lib.GZ_SGD_MAX_BOARDS or tuple(x.shape[1:]) != (3, 15, 15):
+            raise ValueError(f"gz_sgd: input of shape {tuple(x.shape)}")
+        xc = x.detach().float().contiguous()
+        yc = y.detach().to(torch.int64).contiguous()
+        vc = v.detach().float().reshape(B).contiguous()
+        ws, fws, pin, vin, dpin, dvin = self._buffers(B, xc.device)
+        self._bind()
+        s = _stream()
+        _lib.check(self.lib.gz_sgd_forward(ctypes.byref(self.st), B, _ptr(xc), _ptr(pin), _ptr(vin), _ptr(ws), s),
+                   "gz_sgd_forward")
+        if self.counts:
+            torch._foreach_add_(self.counts, 1)
+        _lib.check(self.lib.gz_sgd_fc_loss(ctypes.byref(self.fc), B, _ptr(pin), _ptr(vin), _ptr(yc), _ptr(vc),
+                                           float(scale), _ptr(dpin), _ptr(dvin), ctypes.byref(self.fcg),
+                                           _ptr(self.loss), _ptr(fws), s), "gz_sgd_fc_loss")
+        _lib.check(self.lib.gz_sgd_backward(ctypes.byref(self.st), B, _ptr(xc), _ptr(dpin), _ptr(dvin),
+                                            ctypes.byref(self.gr), _ptr(ws), s), "gz_sgd_backward")
+        return self.loss[0]

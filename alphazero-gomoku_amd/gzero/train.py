@@ -154,11 +154,13 @@ def _world(group):
 class DeviceTrainer:
     """Adam + StepLR policy-value SGD of training.main (training.py:379-388) on the device.
 
-    On a GPU the training forward/backward of the residual tower runs on the HIP
-    kernels of csrc/gz_sgd.hip (``gzero.sgd.train_forward``; ``native=False``: torch's
-    own convolutions, kept for comparison); on the CPU (gloo rehearsals of the
-    data-parallel loop) it is torch's.  With the native kernels, clip_grad_norm_ + Adam
-    are gzero.optim.DeviceAdam (csrc/gz_train.hip: two launches per step)."""
+    On a GPU the whole training step runs on the HIP kernels of csrc/gz_sgd.hip without
+    autograd (``gzero.sgd.NetStep``: tower forward, FC heads + loss and their backward,
+    tower backward, gradients into one flat buffer that is also the data-parallel
+    all-reduce bucket; ``native=False``: torch's own modules under autograd, kept for
+    comparison); on the CPU (gloo rehearsals of the data-parallel loop) it is torch's.
+    With the native kernels, clip_grad_norm_ + Adam are gzero.optim.DeviceAdam
+    (csrc/gz_train.hip: two launches per step)."""
 
     def __init__(self, model, lr=8e-4, weight_decay=1e-5, grad_clip=0.8, step_size=2, gamma=0.85, group=None,
                  device="cuda", native=None):
@@ -170,11 +172,11 @@ class DeviceTrainer:
             model.device = self.device
         self.grad_clip = grad_clip
         self.native = (self.device.type == "cuda") if native is None else bool(native)
+        self.step_fn = None
         if self.native:
             from . import sgd
-            self._forward = lambda x: sgd.train_forward(self.net, x)
-        else:
-            self._forward = self.net
+            self.step_fn = sgd.NetStep(self.net)
+        self._forward = self.net
         self.group = group
         self.world, self.rank = _world(group)
         self.params = [p for p in self.net.parameters()]
@@ -191,10 +193,15 @@ class DeviceTrainer:
             for t in list(self.net.state_dict().values()):
                 dist.broadcast(t, 0, group=group)
             n = sum(p.numel() for p in self.params)
-            self.flat = torch.zeros(n, dtype=torch.float32, device=self.device)
+            self.flat = self.step_fn.grads if self.step_fn is not None else \
+                torch.zeros(n, dtype=torch.float32, device=self.device)
 
     def _allreduce_grads(self):
-        """One bucket: the whole gradient (2.85 MB) in a single SUM all-reduce."""
+        """One bucket: the whole gradient (2.85 MB) in a single SUM all-reduce (native:
+        the gradients already live in that bucket)."""
+        if self.step_fn is not None:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            return
         off = 0
         views = []
         for p in self.params:
@@ -248,6 +255,21 @@ class DeviceTrainer:
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         batches = 0
         for mine, local, gcount in self._slices(ids_all, batch_size):
+            if self.step_fn is not None:  # every gradient is overwritten by the step
+                if local > 0:
+                    x, y, v = _gather(ds, mine)
+                    lval = self.step_fn.step(x, y, v, scale=local / gcount if self.world > 1 else 1.0)
+                else:
+                    self.step_fn.zero()
+                    lval = torch.zeros((), device=self.device)
+                if self.world > 1:
+                    self._allreduce_grads()
+                    lval = lval * (local / gcount)
+                    dist.all_reduce(lval, group=self.group)
+                self.clip_and_step()
+                total += lval.double()
+                batches += 1
+                continue
             # (torch's default, as training.py:292: fresh gradients are assigned, not added
             # into zero-filled ones -- about 60 fewer kernels per step)
             self.optimizer.zero_grad(set_to_none=True)

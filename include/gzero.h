@@ -370,6 +370,35 @@ int gz_sgd_forward(const gz_sgd_net* net, int32_t boards, const float* d_x, floa
  * forward's) */
 int gz_sgd_backward(const gz_sgd_net* net, int32_t boards, const float* d_x, const float* d_dpin,
                     const float* d_dvin, const gz_sgd_grads* grads, void* d_workspace, void* stream);
+/* The FC heads and the loss of the training step (training.py:292-297 over
+ * neural_network.py:150-159): logits = policy_fc(pin), val = tanh(value_fc2(relu(
+ * value_fc1(vin)))), loss = CrossEntropy(logits, y) + MSE(val, v) (batch means), and
+ * its backward: d_dpin [boards][450] and d_dvin [boards][225] for gz_sgd_backward and
+ * the six FC gradients (overwritten), all multiplied by `scale` (1, or this rank's
+ * share of a data-parallel global batch).  d_y int64 class labels [boards], d_v
+ * [boards] targets; d_loss float[3] = {loss, mean cross-entropy, mean squared error}
+ * (unscaled).  Weights in torch's layouts: policy_fc [225][450], value_fc1 [64][225],
+ * value_fc2 [1][64].  d_ws: gz_sgd_fc_workspace_bytes(boards) bytes. */
+typedef struct gz_sgd_fc {
+    const float* policy_weight;
+    const float* policy_bias;
+    const float* value1_weight;
+    const float* value1_bias;
+    const float* value2_weight;
+    const float* value2_bias;
+} gz_sgd_fc;
+typedef struct gz_sgd_fc_grads {
+    float* policy_weight;
+    float* policy_bias;
+    float* value1_weight;
+    float* value1_bias;
+    float* value2_weight;
+    float* value2_bias;
+} gz_sgd_fc_grads;
+size_t gz_sgd_fc_workspace_bytes(int32_t boards);
+int gz_sgd_fc_loss(const gz_sgd_fc* fc, int32_t boards, const float* d_pin, const float* d_vin, const int64_t* d_y,
+                   const float* d_v, float scale, float* d_dpin, float* d_dvin, const gz_sgd_fc_grads* grads,
+                   float* d_loss, void* d_ws, void* stream);
 /* checkers: a copy of a saved tensor of the last gz_sgd_forward on this workspace:
  * which 0..3 = the inputs of the four residual convs (a0, h1, a1, h2), 4..7 = their
  * outputs y1..y4, 8 = the tower output a2, 9 = y0 = conv0's output (fp32 NHWC) */

@@ -191,10 +191,14 @@ def test_sgd_tower_two_steps_match_torch_trainer():
         tr = DeviceTrainer(net, native=native)
         ls = []
         for _ in range(3):
-            tr.optimizer.zero_grad()
-            lg, val = tr._forward(x.cuda())
-            loss = nn.CrossEntropyLoss()(lg, y.cuda()) + nn.MSELoss()(val, v.cuda())
-            loss.backward()
+            if native:  # gzero.sgd.NetStep: tower, FC heads + loss and their backward on the device
+                loss = tr.step_fn.step(x.cuda(), y.cuda(), v.cuda())
+            else:
+                tr.net.train()
+                tr.optimizer.zero_grad()
+                lg, val = tr._forward(x.cuda())
+                loss = nn.CrossEntropyLoss()(lg, y.cuda()) + nn.MSELoss()(val, v.cuda())
+                loss.backward()
             tr.clip_and_step()  # (grad_clip 0.8: DeviceAdam on the native trainer, torch's on the other)
             ls.append(float(loss))
         losses.append(ls)
@@ -202,6 +206,75 @@ def test_sgd_tower_two_steps_match_torch_trainer():
     for (k, a), (_, b) in zip(nets[0].named_buffers(), nets[1].named_buffers()):
         assert torch.allclose(a.float(), b.float(), rtol=1e-2, atol=1e-2), k
 
+
+
+@pytest.mark.parametrize("B,scale", [(128, 1.0), (7, 0.25), (1, 1.0)])
+def test_sgd_fc_loss_vs_float64(B, scale):
+    """gz_sgd_fc_loss (the FC heads, CrossEntropy + MSE and their backward) against
+    torch autograd in float64 on the same pin / vin: the loss within 1e-6 relative,
+    dL/dpin, dL/dvin and the six FC gradients within 1e-5 of the float64 gradient's
+    norm (relative Frobenius error), all scaled by `scale` except the loss."""
+    import ctypes
+    from gzero import _lib
+    L = _lib.load()
+    torch.manual_seed(SEED + B)
+    net = _net(SEED + 3).cuda()
+    pin = torch.randn(B, 450, device="cuda") * 0.5
+    vin = torch.randn(B, 225, device="cuda") * 0.5
+    y = torch.randint(0, 225, (B,), device="cuda")
+    v = torch.rand(B, device="cuda") * 2 - 1
+    fcs = [net.policy_fc.weight, net.policy_fc.bias, net.value_fc1.weight, net.value_fc1.bias,
+           net.value_fc2.weight, net.value_fc2.bias]
+    grads = [torch.full_like(t, float("nan")) for t in fcs]
+    dpin, dvin = torch.empty_like(pin), torch.empty_like(vin)
+    loss = torch.empty(3, device="cuda")
+    ws = torch.empty(int(L.gz_sgd_fc_workspace_bytes(B)), dtype=torch.uint8, device="cuda")
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    fc, fcg = _lib.SgdFc(*[t.data_ptr() for t in fcs]), _lib.SgdFc(*[t.data_ptr() for t in grads])
+    _lib.check(L.gz_sgd_fc_loss(ctypes.byref(fc), B, ptr(pin), ptr(vin), ptr(y), ptr(v), scale, ptr(dpin),
+                                ptr(dvin), ctypes.byref(fcg), ptr(loss), ptr(ws),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "gz_sgd_fc_loss")
+    torch.cuda.synchronize()
+    ref = [t.detach().double().cpu().requires_grad_() for t in fcs]
+    p64 = pin.double().cpu().requires_grad_()
+    v64 = vin.double().cpu().requires_grad_()
+    lg = p64 @ ref[0].T + ref[1]
+    val = torch.tanh(torch.relu(v64 @ ref[2].T + ref[3]) @ ref[4].T + ref[5])
+    ce = nn.CrossEntropyLoss()(lg, y.cpu())
+    mse = nn.MSELoss()(val, v.double().cpu().view(B, 1))
+    ((ce + mse) * scale).backward()
+    got = loss.double().cpu()
+    for a, b in ((got[0], ce + mse), (got[1], ce), (got[2], mse)):
+        assert abs(float(a) - float(b)) <= 1e-6 * max(1.0, abs(float(b))), (float(a), float(b))
+    pairs = [(dpin, p64.grad), (dvin, v64.grad)] + list(zip(grads, [r.grad for r in ref]))
+    for k, (a, b) in enumerate(pairs):
+        err = float((a.double().cpu() - b).norm()) / max(float(b.norm()), 1e-30)
+        assert err < 1e-5, (k, err)
+
+
+def test_netstep_matches_the_autograd_path():
+    """gzero.sgd.NetStep (no autograd: tower, FC heads + loss, backward on the device)
+    against sgd.train_forward + torch's FC heads and loss under autograd, same weights
+    and batch: the same tower kernels, so every gradient within 1e-5 (relative
+    Frobenius) and the loss within 1e-6 relative; the BatchNorm running statistics
+    and num_batches_tracked identical."""
+    from gzero import sgd
+    x, y, v = _batch(128, SEED + 21)
+    nets = [_net(SEED + 4).cuda(), _net(SEED + 4).cuda()]
+    step = sgd.NetStep(nets[0])
+    nets[0].train()
+    l0 = float(step.step(x.cuda(), y.cuda(), v.cuda()))
+    nets[1].train()
+    lg, val = sgd.train_forward(nets[1], x.cuda())
+    loss = nn.CrossEntropyLoss()(lg, y.cuda()) + nn.MSELoss()(val, v.cuda())
+    loss.backward()
+    assert abs(l0 - float(loss)) <= 1e-6 * abs(float(loss))
+    for (k, a), (_, b) in zip(nets[0].named_parameters(), nets[1].named_parameters()):
+        err = float((a.grad - b.grad).norm()) / max(float(b.grad.norm()), 1e-30)
+        top = max(float(p.grad.norm()) for p in nets[1].parameters())
+        assert err < 1e-5 or float((a.grad - b.grad).norm()) < 1e-6 * top, (k, err)
+    for (k, a), (_, b) in zip(nets[0].named_buffers(), nets[1].named_buffers()):
+        assert torch.equal(a, b), k
 
 
 def test_device_adam_matches_torch_adam_with_clipping():

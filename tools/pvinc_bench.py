@@ -75,7 +75,8 @@ def main():
         dst = np.zeros(17, np.uint64)
     dg_names = ["chunk start (units, conv0, y1 rows)", "rows of the next pass", "y1 k-loop", "x1 k-loop",
                 "y2 k-loop", "x2 k-loop", "barrier after the k-loop", "y1 epilogue", "x1 epilogue", "y2 epilogue",
-                "x2 epilogue + heads", "store drain + barrier", "records", "fill + barrier"]
+                "x2 epilogue + heads", "drain + barrier (y1 -> x1, x2)", "fill issue (+ record) + wait",
+                "barrier (image landed)"]
     tiles = torch.zeros(2, dtype=torch.int32, device="cuda")
     sib_names = ["select nodes", "window fills (not overlapped)", "conv0", "y1 k-loop", "y1 barrier + next fill",
                  "y1 epilogue", "x1 k-loop", "x1 barrier + next fill", "x1 epilogue", "y2 k-loop",
