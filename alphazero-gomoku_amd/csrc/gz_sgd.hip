@@ -885,139 +885,168 @@ __global__ void sgd_wreduce_kernel(const float* __restrict__ wpart, int NG, floa
 //   logits = policy_fc(pin),  h = relu(value_fc1(vin)),  val = tanh(value_fc2(h)),
 //   loss = CrossEntropy(logits, y) + MSE(val, v)     (both means over the batch)
 // and its backward down to dL/dpin, dL/dvin (the tower's backward takes it from there)
-// and the six FC parameter gradients.  fp32 throughout, sums in a fixed order.
-// Kernel 1, one workgroup per board: the forward, the board's loss terms, dlogits,
-// dL/d(value_fc1 pre-activation), dL/dpin, dL/dvin.  Kernel 2, one thread per
-// parameter: the FC weight / bias gradients as sums over the boards, and the loss.
+// and the six FC parameter gradients.  fp32 throughout; every sum runs over its index
+// in order (deterministic).  Three launches: (1) the two forward products as tiled
+// jobs (logits, value_fc1's pre-activation), (2) one workgroup per board: softmax
+// cross-entropy, the value head, dlogits and dL/d(value_fc1 pre-activation), (3) the
+// four backward products (dWp, dW1, dpin, dvin) as tiled jobs plus the bias / value_fc2
+// gradients and the loss.
 constexpr int FC_P_IN = 450, FC_P_OUT = 225, FC_V_IN = 225, FC_V_HID = 64;
-constexpr int FC_THREADS = 256;
-constexpr int FC_SAVE = FC_P_OUT + 2 * FC_V_HID + 4;  // dlogits, dpre1, h, dpre2, ce, se
+// per board, in the workspace: logits / dlogits (in place), value_fc1 pre-activation /
+// dpre1 (in place), h, dpre2, ce, squared error
+constexpr int FC_SAVE = FC_P_OUT + 2 * FC_V_HID + 4;
+constexpr int FS_H = FC_P_OUT + FC_V_HID, FS_DP2 = FS_H + FC_V_HID;
+
+// One job: C[m][n] (+)= sum_k a(k, m) * b(k, n) (+ bias[n]), a(k, m) = A[k*sak + m*sam],
+// b(k, n) = Bm[k*sbk + n*sbn], C at m*ldc + n; tiles of 16 m x 32 n (enough workgroups
+// for these small products), K staged in chunks of 32 through LDS, the next chunk
+// loaded into registers meanwhile; 256 threads, 2 outputs each.
+struct FcJob {
+    const float* A;
+    const float* Bm;
+    const float* bias;
+    float* C;
+    int sak, sam, sbk, sbn, ldc, M, N, K, tiles_n, first;  // first: this job's first workgroup
+};
+constexpr int FC_MAXJOBS = 4, FC_TM = 16, FC_TN = 32, FC_TK = 32;
+struct FcJobs {
+    FcJob j[FC_MAXJOBS];
+    int n;
+};
+__global__ __launch_bounds__(256) void sgd_fc_gemm_kernel(FcJobs jobs) {
+    __shared__ float As[FC_TK][FC_TM + 1], Bs[FC_TK][FC_TN + 1];
+    int q = 0;
+    while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].first) q++;
+    const FcJob& J = jobs.j[q];
+    const int tile = blockIdx.x - J.first, m0 = (tile / J.tiles_n) * FC_TM, n0 = (tile % J.tiles_n) * FC_TN;
+    const int t = threadIdx.x, tm = t >> 4, tn = t & 15;
+    float acc[2] = {};
+    // staging: the contiguous index of each operand runs across the threads; the next
+    // chunk's elements are loaded into registers while the current one is multiplied
+    constexpr int NA = FC_TK * FC_TM / 256, NB = FC_TK * FC_TN / 256;
+    float ra[NA], rb[NB];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int r = 0; r < NA; r++) {
+            const int e = t + 256 * r;
+            int kk, mm;
+            if (J.sak == 1) kk = e % FC_TK, mm = e / FC_TK;
+            else mm = e % FC_TM, kk = e / FC_TM;
+            const int k = k0 + kk, m = m0 + mm;
+            ra[r] = k < J.K && m < J.M ? J.A[(size_t)k * J.sak + (size_t)m * J.sam] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < NB; r++) {
+            const int e = t + 256 * r;
+            int kk, nn;
+            if (J.sbk == 1) kk = e % FC_TK, nn = e / FC_TK;
+            else nn = e % FC_TN, kk = e / FC_TN;
+            const int k = k0 + kk, n = n0 + nn;
+            rb[r] = k < J.K && n < J.N ? J.Bm[(size_t)k * J.sbk + (size_t)n * J.sbn] : 0.f;
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int r = 0; r < NA; r++) {
+            const int e = t + 256 * r;
+            if (J.sak == 1) As[e % FC_TK][e / FC_TK] = ra[r];
+            else As[e / FC_TM][e % FC_TM] = ra[r];
+        }
+#pragma unroll
+        for (int r = 0; r < NB; r++) {
+            const int e = t + 256 * r;
+            if (J.sbk == 1) Bs[e % FC_TK][e / FC_TK] = rb[r];
+            else Bs[e / FC_TN][e % FC_TN] = rb[r];
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < J.K; k0 += FC_TK) {
+        __syncthreads();
+        put();
+        __syncthreads();
+        if (k0 + FC_TK < J.K) fetch(k0 + FC_TK);
+        const int kn = J.K - k0 < FC_TK ? J.K - k0 : FC_TK;
+#pragma unroll 8
+        for (int kk = 0; kk < kn; kk++) {
+            const float a0 = As[kk][tm];
+            acc[0] = __builtin_fmaf(a0, Bs[kk][tn], acc[0]);
+            acc[1] = __builtin_fmaf(a0, Bs[kk][tn + 16], acc[1]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int m = m0 + tm, n = n0 + tn + 16 * c;
+        if (m < J.M && n < J.N) J.C[(size_t)m * J.ldc + n] = acc[c] + (J.bias ? J.bias[n] : 0.f);
+    }
+}
+
 __device__ __forceinline__ float fc_wave_sum(float x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
     return x;
 }
-__global__ __launch_bounds__(FC_THREADS) void sgd_fc_board_kernel(gz_sgd_fc fc, const float* __restrict__ pin,
-                                                                 const float* __restrict__ vin,
-                                                                 const int64_t* __restrict__ y,
-                                                                 const float* __restrict__ v, int B, float scale,
-                                                                 float* __restrict__ dpin, float* __restrict__ dvin,
-                                                                 float* __restrict__ save) {
-    __shared__ float sp[FC_P_IN], sv[FC_V_IN], lg[FC_P_OUT], hh[FC_V_HID], dl[FC_P_OUT], d1[FC_V_HID];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int k = tid; k < FC_P_IN; k += FC_THREADS) sp[k] = pin[(size_t)b * FC_P_IN + k];
-    for (int k = tid; k < FC_V_IN; k += FC_THREADS) sv[k] = vin[(size_t)b * FC_V_IN + k];
-    __syncthreads();
-    // logits and the value head's hidden layer: a wave per output, lanes over k
-    for (int i = wave; i < FC_P_OUT; i += 4) {
-        const float* w = fc.policy_weight + (size_t)i * FC_P_IN;
-        float a = 0.f;
-        for (int k = lane; k < FC_P_IN; k += 64) a = __builtin_fmaf(w[k], sp[k], a);
-        a = fc_wave_sum(a);
-        if (lane == 0) lg[i] = a + fc.policy_bias[i];
-    }
-    for (int j = wave; j < FC_V_HID; j += 4) {
-        const float* w = fc.value1_weight + (size_t)j * FC_V_IN;
-        float a = 0.f;
-        for (int k = lane; k < FC_V_IN; k += 64) a = __builtin_fmaf(w[k], sv[k], a);
-        a = fc_wave_sum(a);
-        if (lane == 0) hh[j] = fmaxf(a + fc.value1_bias[j], 0.f);
-    }
-    __syncthreads();
+// one 64-thread workgroup per board: softmax cross-entropy about the max, the value
+// head, dlogits (in place of the logits) and dpre1 (in place of the pre-activation)
+__global__ __launch_bounds__(64) void sgd_fc_loss_kernel(gz_sgd_fc fc, const int64_t* __restrict__ y,
+                                                        const float* __restrict__ v, int B, float scale,
+                                                        float* __restrict__ save) {
+    const int b = blockIdx.x, lane = threadIdx.x;
     float* sb = save + (size_t)b * FC_SAVE;
-    if (wave == 0) {  // softmax cross-entropy (log-sum-exp about the max), dlogits
-        float m = -INFINITY;
-        for (int i = lane; i < FC_P_OUT; i += 64) m = fmaxf(m, lg[i]);
+    float m = -INFINITY;
+    for (int i = lane; i < FC_P_OUT; i += 64) m = fmaxf(m, sb[i]);
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d));
-        float e = 0.f;
-        for (int i = lane; i < FC_P_OUT; i += 64) e += expf(lg[i] - m);
-        e = fc_wave_sum(e);
-        const int64_t yt = y[b];
-        const int t = yt >= 0 && yt < FC_P_OUT ? (int)yt : 0;  // (labels are checked by the caller)
-        const float lse = m + logf(e), g = scale / (float)B;
-        for (int i = lane; i < FC_P_OUT; i += 64) {
-            const float d = (expf(lg[i] - m) / e - (i == t ? 1.f : 0.f)) * g;
-            dl[i] = d;
-            sb[i] = d;
-        }
-        if (lane == 0) sb[FC_P_OUT + 2 * FC_V_HID + 1] = yt == t ? lse - lg[t] : NAN;
-    } else if (wave == 1) {  // value: tanh(value_fc2(h)), squared error, dpre2, dpre1
-        float a = lane < FC_V_HID ? fc.value2_weight[lane] * hh[lane] : 0.f;
-        a = fc_wave_sum(a) + fc.value2_bias[0];
-        const float val = tanhf(a), diff = val - v[b];
-        const float dpre2 = 2.f * diff * (scale / (float)B) * (1.f - val * val);
-        if (lane < FC_V_HID) {
-            const float d = hh[lane] > 0.f ? dpre2 * fc.value2_weight[lane] : 0.f;
-            d1[lane] = d;
-            sb[FC_P_OUT + lane] = d;
-            sb[FC_P_OUT + FC_V_HID + lane] = hh[lane];
-        }
-        if (lane == 0) {
-            sb[FC_P_OUT + 2 * FC_V_HID] = dpre2;
-            sb[FC_P_OUT + 2 * FC_V_HID + 2] = diff * diff;
-        }
-    }
-    __syncthreads();
-    // dL/dpin = dlogits . policy_fc.weight, dL/dvin = dpre1 . value_fc1.weight (coalesced over k)
-    for (int k = tid; k < FC_P_IN; k += FC_THREADS) {
-        float a = 0.f;
-        for (int i = 0; i < FC_P_OUT; i++) a = __builtin_fmaf(dl[i], fc.policy_weight[(size_t)i * FC_P_IN + k], a);
-        dpin[(size_t)b * FC_P_IN + k] = a;
-    }
-    for (int k = tid; k < FC_V_IN; k += FC_THREADS) {
-        float a = 0.f;
-        for (int j = 0; j < FC_V_HID; j++) a = __builtin_fmaf(d1[j], fc.value1_weight[(size_t)j * FC_V_IN + k], a);
-        dvin[(size_t)b * FC_V_IN + k] = a;
+    for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d));
+    float e = 0.f;
+    for (int i = lane; i < FC_P_OUT; i += 64) e += expf(sb[i] - m);
+    e = fc_wave_sum(e);
+    const int64_t yt = y[b];
+    const int t = yt >= 0 && yt < FC_P_OUT ? (int)yt : 0;  // (labels are checked by the caller)
+    const float ce = m + logf(e) - sb[t], g = scale / (float)B;
+    // value: h = relu(pre1), val = tanh(w2 . h + b2)
+    const float pre1 = sb[FC_P_OUT + lane], h = fmaxf(pre1, 0.f);
+    const float val = tanhf(fc_wave_sum(fc.value2_weight[lane] * h) + fc.value2_bias[0]), diff = val - v[b];
+    const float dpre2 = 2.f * diff * g * (1.f - val * val);
+    __syncthreads();  // every lane has read the logits before they are overwritten
+    for (int i = lane; i < FC_P_OUT; i += 64) sb[i] = (expf(sb[i] - m) / e - (i == t ? 1.f : 0.f)) * g;
+    sb[FC_P_OUT + lane] = pre1 > 0.f ? dpre2 * fc.value2_weight[lane] : 0.f;
+    sb[FS_H + lane] = h;
+    if (lane == 0) {
+        sb[FS_DP2] = dpre2;
+        sb[FS_DP2 + 1] = yt == t ? ce : NAN;
+        sb[FS_DP2 + 2] = diff * diff;
     }
 }
-// one thread per gradient element (policy weight, policy bias, value1 weight, value1
-// bias, value2 weight, value2 bias), then one for the loss: sums over the boards in order
-constexpr int FC_NW = FC_P_OUT * FC_P_IN, FC_NB1 = FC_NW + FC_P_OUT, FC_NW1 = FC_NB1 + FC_V_HID * FC_V_IN,
-              FC_NV1B = FC_NW1 + FC_V_HID, FC_NV2 = FC_NV1B + FC_V_HID, FC_NALL = FC_NV2 + 2;
-__global__ __launch_bounds__(256) void sgd_fc_grad_kernel(const float* __restrict__ pin, const float* __restrict__ vin,
-                                                          const float* __restrict__ save, int B, gz_sgd_fc_grads gr,
-                                                          float* __restrict__ loss) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= FC_NALL) return;
-    float a = 0.f;
-    if (e < FC_NW) {
-        const int i = e / FC_P_IN, k = e - i * FC_P_IN;
-        for (int b = 0; b < B; b++) a = __builtin_fmaf(save[(size_t)b * FC_SAVE + i], pin[(size_t)b * FC_P_IN + k], a);
-        gr.policy_weight[e] = a;
-    } else if (e < FC_NB1) {
-        const int i = e - FC_NW;
-        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + i];
-        gr.policy_bias[i] = a;
-    } else if (e < FC_NW1) {
-        const int q = e - FC_NB1, j = q / FC_V_IN, k = q - j * FC_V_IN;
-        for (int b = 0; b < B; b++)
-            a = __builtin_fmaf(save[(size_t)b * FC_SAVE + FC_P_OUT + j], vin[(size_t)b * FC_V_IN + k], a);
-        gr.value1_weight[q] = a;
-    } else if (e < FC_NV1B) {
-        const int j = e - FC_NW1;
-        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + FC_P_OUT + j];
-        gr.value1_bias[j] = a;
-    } else if (e < FC_NV2) {
-        const int j = e - FC_NV1B;
-        for (int b = 0; b < B; b++)
-            a = __builtin_fmaf(save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID],
-                               save[(size_t)b * FC_SAVE + FC_P_OUT + FC_V_HID + j], a);
-        gr.value2_weight[j] = a;
-    } else if (e == FC_NV2) {
-        for (int b = 0; b < B; b++) a += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID];
-        gr.value2_bias[0] = a;
-    } else {  // the loss: mean cross-entropy + mean squared error (of this batch, unscaled)
-        float ce = 0.f, se = 0.f;
-        for (int b = 0; b < B; b++) {
-            ce += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID + 1];
-            se += save[(size_t)b * FC_SAVE + FC_P_OUT + 2 * FC_V_HID + 2];
+// the bias gradients, value_fc2's weight and bias gradients and the loss: one wave per
+// output, lanes over the boards (fixed lane order, then a fixed shuffle tree)
+__global__ __launch_bounds__(256) void sgd_fc_small_kernel(const float* __restrict__ save, int B, gz_sgd_fc_grads gr,
+                                                           float* __restrict__ loss) {
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    float a = 0.f, c = 0.f;
+    for (int b = lane; b < B; b += 64) {
+        const float* sb = save + (size_t)b * FC_SAVE;
+        if (e < FC_P_OUT) a += sb[e];
+        else if (e < FC_P_OUT + FC_V_HID) a += sb[e];  // dpre1 (in place of the pre-activation)
+        else if (e < FC_P_OUT + 2 * FC_V_HID) a = __builtin_fmaf(sb[FS_DP2], sb[FS_H + e - FC_P_OUT - FC_V_HID], a);
+        else if (e == FC_P_OUT + 2 * FC_V_HID) a += sb[FS_DP2];
+        else {
+            a += sb[FS_DP2 + 1];
+            c += sb[FS_DP2 + 2];
         }
-        loss[0] = ce / (float)B + se / (float)B;
-        loss[1] = ce / (float)B;
-        loss[2] = se / (float)B;
+    }
+    a = fc_wave_sum(a);
+    c = fc_wave_sum(c);
+    if (lane) return;
+    if (e < FC_P_OUT) gr.policy_bias[e] = a;
+    else if (e < FC_P_OUT + FC_V_HID) gr.value1_bias[e - FC_P_OUT] = a;
+    else if (e < FC_P_OUT + 2 * FC_V_HID) gr.value2_weight[e - FC_P_OUT - FC_V_HID] = a;
+    else if (e == FC_P_OUT + 2 * FC_V_HID) gr.value2_bias[0] = a;
+    else if (e == FC_P_OUT + 2 * FC_V_HID + 1) {  // the loss: mean cross-entropy + mean squared error
+        loss[0] = a / (float)B + c / (float)B;
+        loss[1] = a / (float)B;
+        loss[2] = c / (float)B;
     }
 }
+constexpr int FC_SMALL = FC_P_OUT + 2 * FC_V_HID + 2;
 
 // ---------------------------------------------------------------- host side
 struct Ws {
@@ -1236,7 +1265,40 @@ extern "C" int gz_sgd_fc_loss(const gz_sgd_fc* fc, int32_t B, const float* d_pin
         return sgd_fail(GZ_ERR_ARG, "gz_sgd_fc_loss: NULL parameter or gradient");
     hipStream_t s = (hipStream_t)stream;
     float* save = (float*)d_ws;
-    sgd_fc_board_kernel<<<B, FC_THREADS, 0, s>>>(*fc, d_pin, d_vin, d_y, d_v, B, scale, d_dpin, d_dvin, save);
-    sgd_fc_grad_kernel<<<(FC_NALL + 255) / 256, 256, 0, s>>>(d_pin, d_vin, save, B, *gr, d_loss);
+    auto job = [](const float* A, int sak, int sam, const float* Bm, int sbk, int sbn, const float* bias, float* C,
+                  int ldc, int M, int N, int K) {
+        FcJob j{A, Bm, bias, C, sak, sam, sbk, sbn, ldc, M, N, K, (N + FC_TN - 1) / FC_TN, 0};
+        return j;
+    };
+    auto launch = [&](FcJobs& js) {
+        int wg = 0;
+        for (int q = 0; q < js.n; q++) {
+            js.j[q].first = wg;
+            wg += ((js.j[q].M + FC_TM - 1) / FC_TM) * js.j[q].tiles_n;
+        }
+        sgd_fc_gemm_kernel<<<wg, 256, 0, s>>>(js);
+    };
+    // (1) logits[b][i] = sum_k pin[b][k] Wp[i][k] + bp[i];  pre1[b][j] = sum_k vin[b][k] W1[j][k] + b1[j]
+    FcJobs f{};
+    f.j[0] = job(d_pin, 1, FC_P_IN, fc->policy_weight, 1, FC_P_IN, fc->policy_bias, save, FC_SAVE, B, FC_P_OUT,
+                 FC_P_IN);
+    f.j[1] = job(d_vin, 1, FC_V_IN, fc->value1_weight, 1, FC_V_IN, fc->value1_bias, save + FC_P_OUT, FC_SAVE, B,
+                 FC_V_HID, FC_V_IN);
+    f.n = 2;
+    launch(f);
+    // (2) the loss terms, dlogits, dpre1
+    sgd_fc_loss_kernel<<<B, 64, 0, s>>>(*fc, d_y, d_v, B, scale, save);
+    // (3) dWp[i][k] = sum_b dl[b][i] pin[b][k];  dW1[j][k] = sum_b dpre1[b][j] vin[b][k];
+    //     dpin[b][k] = sum_i dl[b][i] Wp[i][k];  dvin[b][k] = sum_j dpre1[b][j] W1[j][k]
+    FcJobs g{};
+    g.j[0] = job(save, FC_SAVE, 1, d_pin, FC_P_IN, 1, nullptr, gr->policy_weight, FC_P_IN, FC_P_OUT, FC_P_IN, B);
+    g.j[1] = job(save + FC_P_OUT, FC_SAVE, 1, d_vin, FC_V_IN, 1, nullptr, gr->value1_weight, FC_V_IN, FC_V_HID,
+                 FC_V_IN, B);
+    g.j[2] = job(save, 1, FC_SAVE, fc->policy_weight, FC_P_IN, 1, nullptr, d_dpin, FC_P_IN, B, FC_P_IN, FC_P_OUT);
+    g.j[3] = job(save + FC_P_OUT, 1, FC_SAVE, fc->value1_weight, FC_V_IN, 1, nullptr, d_dvin, FC_V_IN, B, FC_V_IN,
+                 FC_V_HID);
+    g.n = 4;
+    launch(g);
+    sgd_fc_small_kernel<<<(FC_SMALL + 3) / 4, 256, 0, s>>>(save, B, *gr, d_loss);
     return sgd_check("gz_sgd_fc_loss");
 }

@@ -31,6 +31,7 @@ class DeviceAdam(torch.optim.Optimizer):
         dev = self.param_groups[0]["params"][0].device
         self._ws = torch.empty(int(self._lib.gz_adam_workspace_bytes()), dtype=torch.uint8, device=dev)
         self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._tables = {}  # per group: (the tensors' data pointers, the ctypes table built from them)
 
     @torch.no_grad()
     def step(self, closure=None, max_norm=None):
@@ -64,11 +65,16 @@ class DeviceAdam(torch.optim.Optimizer):
             if len(steps) != 1:
                 raise ValueError("DeviceAdam: the parameters of a group must share their step count")
             step = steps.pop() + 1
-            table = (_lib.AdamTensor * len(ps))()
-            for k, p in enumerate(ps):
-                st = self.state[p]
-                table[k] = _lib.AdamTensor(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
-                                           st["exp_avg_sq"].data_ptr(), p.numel())
+            # the table is rebuilt only when a tensor moved (a trainer that keeps its
+            # gradients in one buffer passes the same pointers every step)
+            key = tuple((p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                         self.state[p]["exp_avg_sq"].data_ptr(), p.numel()) for p in ps)
+            cached = self._tables.get(id(group))
+            if cached is not None and cached[0] == key:
+                table = cached[1]
+            else:
+                table = (_lib.AdamTensor * len(ps))(*[_lib.AdamTensor(*k) for k in key])
+                self._tables[id(group)] = (key, table)
             b1, b2 = group["betas"]
             _lib.check(self._lib.gz_adam_step(table, len(ps), float(group["lr"]), float(b1), float(b2),
                                               float(group["eps"]), float(group["weight_decay"]), step,
