@@ -512,16 +512,24 @@ def run_iteration(model, trainer, it: int, games_per_iteration: int = 10, num_si
     tr_idx = torch.tensor(idx[:split], dtype=torch.int64, device="cuda")
     va_idx = torch.tensor(idx[split:], dtype=torch.int64, device="cuda")
     tl, vl = [], []
+    t_tr = t_va = 0.0
+    t_ds = time.time() - t1
     for ep in range(epochs):
+        ta = time.time()
         tl.append(trainer.train_epoch(ds, batch_size, indices=tr_idx))
+        tb = time.time()
         vl.append(trainer.validate_epoch(ds, batch_size, indices=va_idx))
+        t_tr += tb - ta
+        t_va += time.time() - tb
         if verbose and rank == 0:
             print(f"    ├── 模型训练: {_render_bar((ep + 1) / epochs, 12)} epoch {ep + 1}/{epochs} "
                   f"train {tl[-1]:.3f} val {vl[-1]:.3f}")
     trainer.step_scheduler()
     model.eval_mode()
     t2 = time.time()
-    return dict(out, samples=n, train_loss=float(np.mean(tl)), val_loss=float(np.mean(vl)), sgd_s=t2 - t1)
+    return dict(out, samples=n, train_loss=float(np.mean(tl)), val_loss=float(np.mean(vl)), sgd_s=t2 - t1,
+                sgd_parts_s={"dataset_split": round(t_ds, 4), "train_epochs": round(t_tr, 4),
+                             "validation": round(t_va, 4)})
 
 
 def _rng_isolated(fn, *a, **k):

@@ -353,15 +353,18 @@ def config5(games, sims, seed, iterations=2):
                                "note": "the same iteration scaled linearly to 1,024 games (self-play, dataset and "
                                        "SGD all grow with the record count), for comparison with round 2"},
             "iteration_s": round(last["iteration_s"], 2), "selfplay_s": round(last["selfplay_s"], 2),
-            "sgd_s": round(last.get("sgd_s", 0.0), 2), "records": last["records"],
+            "sgd_s": round(last.get("sgd_s", 0.0), 2), "sgd_parts_s": last.get("sgd_parts_s"),
+            "records": last["records"],
             "samples": last.get("samples"), "moves_played": last["moves_played"],
             "first_iteration_s": round(its[0]["iteration_s"], 2),
             "workload": (f"BASELINE config 5 on 1 GPU: training.run_iteration with {games} self-play games per "
                          f"iteration ({sims} sims, medium, beta 0.2, planner_steps 5, tree PV forward on every node, "
                          "records through gzero.dist.RecordExchange; each game played once: slots idle past the "
                          "iteration's ids and are compacted), 35 % augmentation, 2 epochs of SGD "
-                         "(batch 128, Adam 8e-4, clip 0.8; conv0, residual tower and 1x1 head convs on "
-                         "gz_sgd_forward/backward, f16x3 MFMA tower; the FC heads torch), StepLR; games per iteration "
+                         "(batch 128, Adam 8e-4, clip 0.8: the whole step on the device without autograd -- conv0, "
+                         "residual tower and 1x1 head convs on gz_sgd_forward/backward (f16x3 MFMA tower), FC heads + "
+                         "loss and their backward on gz_sgd_fc_loss, clip + Adam on gz_adam_step), StepLR; games per "
+                         "iteration "
                          "fixed by the builder (BASELINE names none); "
                          "value from the last of "
                          f"{iterations} iterations")}

@@ -197,3 +197,18 @@ def test_data_parallel_step_equals_global_batch():
     np.testing.assert_allclose(l0, ref_losses, rtol=1e-5)
     for a, b in zip(p0, ref_params):
         np.testing.assert_allclose(np.frombuffer(a, np.float32), b.numpy().reshape(-1), atol=2e-6)
+
+
+@pytest.mark.parametrize("n", [1, 7, 128, 129, 5000])
+@pytest.mark.parametrize("shuffle", [True, False])
+def test_loader_order_matches_dataloader(n, shuffle):
+    """gzero.train.loader_order (no DataLoader iteration) yields DataLoader's batches and
+    leaves torch's global generator where iterating the DataLoader leaves it."""
+    import torch
+    from gzero.train import loader_order, loader_order_reference
+    torch.manual_seed(11)
+    a, ra = loader_order(n, 128, shuffle), torch.rand(4)
+    torch.manual_seed(11)
+    b, rb = loader_order_reference(n, 128, shuffle), torch.rand(4)
+    assert len(a) == len(b) and all(torch.equal(x, y) for x, y in zip(a, b))
+    assert torch.equal(ra, rb)
