@@ -311,14 +311,16 @@ class DeviceTrainer:
         return float(total.item()) / max(1, batches)
 
     @torch.no_grad()
-    def validate_epoch(self, ds, batch_size=128, indices=None, chunk=2048):
+    def validate_epoch(self, ds, batch_size=128, indices=None, chunk=512):
         """Mean per-batch validation loss (training.py:313-337).  Data parallel:
         batch k is evaluated by rank k mod N and the per-batch losses are
         SUM-all-reduced, so every rank returns the same global value (and each
         batch is evaluated once, not N times).  The batches are evaluated ``chunk``
         boards per forward (eval mode has no batch statistics, so the per-sample
-        outputs do not depend on the batching) and the per-sample losses are averaged
-        per batch of ``batch_size``, as the reference's loop over its DataLoader does."""
+        outputs do not depend on the batching; the last forward is padded to the same
+        shape, whose convolution algorithms MIOpen then finds once per process instead
+        of once per remainder size) and the per-sample losses are averaged per batch of
+        ``batch_size``, as the reference's loop over its DataLoader does."""
         self.net.eval()
         n = len(ds) if indices is None else int(indices.numel())
         # iterate an (unshuffled) DataLoader as the reference does: it draws one torch seed
@@ -333,8 +335,12 @@ class DeviceTrainer:
         for c in range(0, len(mine), per):
             bis = mine[c:c + per]
             ids = torch.cat([ids_all[bi * batch_size:(bi + 1) * batch_size] for bi in bis])
+            real = int(ids.numel())
+            if real < per * batch_size:
+                ids = torch.cat([ids, ids[:1].expand(per * batch_size - real)])
             x, y, v = _gather(ds, ids)
             logits, val = self.net(x)
+            logits, val, y, v = logits[:real], val[:real], y[:real], v[:real]
             ce = nn.functional.cross_entropy(logits, y, reduction="none")
             se = (val.reshape(-1) - v.reshape(-1).to(val.dtype)) ** 2
             ks = [min(batch_size, n - bi * batch_size) for bi in bis]
