@@ -16,8 +16,10 @@ def short(name):
     m = re.search(r"(\w+)(<[^(]*>)?\(", name)
     if m:
         return m.group(1)
-    m = re.match(r"_ZN12_GLOBAL__N_1\d+(\w+?)I", name)
-    return m.group(1) if m else name[:40]
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)  # <length><name> after the anonymous namespace
+    if m:
+        return name[m.end():m.end() + int(m.group(1))]
+    return name[:40]
 
 
 kernels = collections.defaultdict(list)
