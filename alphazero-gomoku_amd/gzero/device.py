@@ -165,10 +165,13 @@ class PVWeights:
             raise ValueError(f"unknown precision {precision!r}")
         self.precision = precision
         self.mode = _lib.GZ_PV_FP32 if precision == "fp32" else _lib.GZ_PV_F16X3
-        blob = np.ascontiguousarray(blob, np.float32)
-        if blob.size != lib.gz_pv_weight_floats():
-            raise ValueError(f"weight blob has {blob.size} floats, kernel expects {lib.gz_pv_weight_floats()}")
-        self.tensor = torch.from_numpy(blob).cuda()
+        if isinstance(blob, torch.Tensor):  # (weights.pack_pv_weights_torch: packed on the device)
+            blob = blob.detach().to(device="cuda", dtype=torch.float32).contiguous().reshape(-1)
+        else:
+            blob = torch.from_numpy(np.ascontiguousarray(blob, np.float32).reshape(-1))
+        if blob.numel() != lib.gz_pv_weight_floats():
+            raise ValueError(f"weight blob has {blob.numel()} floats, kernel expects {lib.gz_pv_weight_floats()}")
+        self.tensor = blob.cuda()
         self.workspace = torch.empty(0, dtype=torch.uint8, device="cuda")
 
     def workspace_for(self, n):

@@ -12,6 +12,7 @@ library this raises ``GzeroUnavailable``.
 import ctypes
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 
@@ -84,4 +85,8 @@ class DeviceAdam(torch.optim.Optimizer):
                        "gz_adam_step")
             for p in ps:
                 self.state[p]["step"] = step
+            # the kernel wrote the parameters through raw pointers: bump their version
+            # counters as an in-place torch op would, so that caches keyed on them (the
+            # model's packed inference weights, neural_network.GomokuModel) see the update
+            increment_version(ps)
         return loss

@@ -124,6 +124,19 @@ def check_ids(ds, d_ids):
             raise _lib.GzeroError(f"gz_dataset_gather: sample id out of range [{lo}, {hi}] for {len(ds)} samples")
 
 
+def rows_from_planes(x):
+    """[B, 3, 15, 15] network input planes (black, white, empty: boards.planes_from_cells)
+    -> [B, 16] int32 board rows (black words, then white: bit r * 16 + c), the input of
+    the inference kernel -- on the device, no host round trip."""
+    b = int(x.shape[0])
+    bits = (x[:, :2] > 0.5).to(torch.int64)                      # [B, 2, 15, 15]
+    bits = nn.functional.pad(bits, (0, 1)).reshape(b, 2, 240)    # column 15 empty
+    bits = nn.functional.pad(bits, (0, 16)).reshape(b, 2, 8, 32)
+    w = (bits << torch.arange(32, device=x.device, dtype=torch.int64)).sum(-1)
+    w = torch.where(w >= 2 ** 31, w - 2 ** 32, w)                  # the uint32 word's int32 bits
+    return w.to(torch.int32).reshape(b, 16)
+
+
 def _gather(ds, ids):
     """A batch of an epoch whose ids were checked once (check_ids)."""
     return ds.gather(ids, check=False) if isinstance(ds, DeviceDataset) else ds.gather(ids)
@@ -311,7 +324,7 @@ class DeviceTrainer:
         return float(total.item()) / max(1, batches)
 
     @torch.no_grad()
-    def validate_epoch(self, ds, batch_size=128, indices=None, chunk=512):
+    def validate_epoch(self, ds, batch_size=128, indices=None, chunk=512, kernel=None):
         """Mean per-batch validation loss (training.py:313-337).  Data parallel:
         batch k is evaluated by rank k mod N and the per-batch losses are
         SUM-all-reduced, so every rank returns the same global value (and each
@@ -320,8 +333,18 @@ class DeviceTrainer:
         outputs do not depend on the batching; the last forward is padded to the same
         shape, whose convolution algorithms MIOpen then finds once per process instead
         of once per remainder size) and the per-sample losses are averaged per batch of
-        ``batch_size``, as the reference's loop over its DataLoader does."""
+        ``batch_size``, as the reference's loop over its DataLoader does.
+
+        ``kernel`` (default: the native trainer): the eval-mode forward is the inference
+        kernel (gz_pv_forward, f16x3; logits within 3e-7 of fp32) on the
+        samples' board rows, with the weights packed on the device from the current
+        parameters and running statistics -- not the training graph's torch convolutions."""
         self.net.eval()
+        kernel = self.native if kernel is None else bool(kernel)
+        pvw = None
+        if kernel:
+            from . import device as _device, weights as _weights
+            pvw = _device.PVWeights(_weights.pack_pv_weights_torch(self.net.state_dict(), self.device))
         n = len(ds) if indices is None else int(indices.numel())
         # iterate an (unshuffled) DataLoader as the reference does: it draws one torch seed
         order = loader_order(n, batch_size, shuffle=False)
@@ -339,7 +362,12 @@ class DeviceTrainer:
             if real < per * batch_size:
                 ids = torch.cat([ids, ids[:1].expand(per * batch_size - real)])
             x, y, v = _gather(ds, ids)
-            logits, val = self.net(x)
+            if pvw is not None:
+                b = int(ids.numel())
+                lg, vl, _ = _device.pv_forward_dev(pvw, rows_from_planes(x), b)
+                logits, val = lg.view(b, -1), vl.view(b, 1)
+            else:
+                logits, val = self.net(x)
             logits, val, y, v = logits[:real], val[:real], y[:real], v[:real]
             ce = nn.functional.cross_entropy(logits, y, reduction="none")
             se = (val.reshape(-1) - v.reshape(-1).to(val.dtype)) ** 2

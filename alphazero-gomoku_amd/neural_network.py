@@ -54,7 +54,9 @@ class GomokuModel:
         from gzero.device import PVWeights
         key = self._param_key()
         if self._packed is None or key != self._packed_key:
-            self._packed = PVWeights(_w.pack_pv_weights(self.model.state_dict()), precision=self.precision)
+            # packed on the device (the host packer's numpy took ~0.5 s per repack)
+            self._packed = PVWeights(_w.pack_pv_weights_torch(self.model.state_dict(), "cuda"),
+                                     precision=self.precision)
             self._packed_key = key
         return self._packed
 

@@ -300,7 +300,11 @@ def test_device_adam_matches_torch_adam_with_clipping():
                 o.param_groups[0]["lr"] = 8e-4 * 0.85
         n_ref = float(nn.utils.clip_grad_norm_(ref, 0.8))
         opt_ref.step()
+        v0 = [p._version for p in mine]
         opt.step(max_norm=0.8)
+        # an update through raw pointers still bumps the version counters (the model's
+        # packed-weight cache keys on them)
+        assert all(p._version > v for p, v in zip(mine, v0))
         assert abs(float(opt.last_norm) - n_ref) <= 1e-6 * n_ref
         for a, b in zip(ref, mine):
             assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=0), k  # clipped in place

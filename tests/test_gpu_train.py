@@ -130,6 +130,13 @@ def test_device_trainer_follows_reference():
     for _ in range(2):
         tl.append(tr.train_epoch(ds, 128, indices=tr_idx))
         vl.append(tr.validate_epoch(ds, 128, indices=va_idx))
+        # the inference kernel's validation (the native trainer's default) against the
+        # eval-mode torch forward, same parameters and running statistics (the torch RNG
+        # state restored: each validation draws the DataLoader's base seed)
+        rng = torch.get_rng_state()
+        vt = tr.validate_epoch(ds, 128, indices=va_idx, kernel=False)
+        torch.set_rng_state(rng)
+        assert abs(vl[-1] - vt) <= 1e-5 * abs(vt), (vl[-1], vt)
     tr.step_scheduler()
     # tolerance: CPU torch at 8 vs 1 threads already differs by 1e-4 after these 12
     # steps; MIOpen's convolutions by 1.0-1.2e-3 (tools/sgd_numerics.py)

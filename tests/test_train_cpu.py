@@ -212,3 +212,20 @@ def test_loader_order_matches_dataloader(n, shuffle):
     b, rb = loader_order_reference(n, 128, shuffle), torch.rand(4)
     assert len(a) == len(b) and all(torch.equal(x, y) for x, y in zip(a, b))
     assert torch.equal(ra, rb)
+
+
+def test_rows_from_planes_matches_leaf_words():
+    """gzero.train.rows_from_planes (the kernel validation's input) = boards.leaf_words of
+    the same cells, every bit -- incl. the empty board, a full one and the corners."""
+    from gzero import boards
+    from gzero.train import rows_from_planes
+    rng = np.random.default_rng(3)
+    cells = rng.choice(3, size=(64, 225), p=[0.4, 0.3, 0.3]).astype(np.int8)
+    cells[0] = 0
+    cells[1] = rng.choice([1, 2], size=225)
+    cells[2] = 0
+    cells[2][[0, 14, 210, 224]] = [1, 2, 2, 1]
+    bl, wh = boards.cells_to_words(cells)
+    want = boards.leaf_words(bl, wh).view(np.int32)
+    got = rows_from_planes(torch.from_numpy(boards.planes_from_cells(cells))).numpy()
+    assert np.array_equal(got, want)
