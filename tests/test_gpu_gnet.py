@@ -179,3 +179,33 @@ def test_incremental_graphnet_chains_bitwise(nets):
             pr_ = ref[230400:230400 + 1800].view(np.float32)
             diag.append(("pol", int((pj.view(np.uint32) != pr_.view(np.uint32)).sum()), float(np.abs(pj - pr_).max())))
             assert not bad, (ply, bad[:8], float(np.abs(p - pf).max()), float(np.abs(q - qf).max()), c, diag)
+
+
+@pytest.mark.parametrize("n", [1, 17, 700, 5000])
+def test_small_launch_heads_bitwise(nets, n):
+    """gn_heads_small_kernel (16 boards, 8 waves per workgroup, dense fc0: the planner's
+    small sequential-round launches) against gn_heads_kernel (32 boards, 4 waves, fc0
+    over the stone-holding k-blocks) on the same records: p and q bit for bit.  A
+    launch that asks for logits takes gn_heads_kernel; one that does not, below 2 x 32
+    boards per CU, the small kernel.  Sparse and empty boards included."""
+    import torch
+    from gzero import device
+    _, gsd, dsd, w = nets
+    rng = np.random.default_rng(23)
+    cells = rng.choice(3, size=(n, 225), p=[0.6, 0.2, 0.2]).astype(np.int8)
+    cells[: min(n, 40) // 2] = 0
+    for i in range(min(n, 40) // 2, min(n, 40)):
+        cells[i] = 0
+        cells[i, rng.choice(225, size=1 + i % 3, replace=False)] = 1 + i % 2
+    bl, wh = boards.cells_to_words(cells)
+    d_b = torch.from_numpy(boards.leaf_words(bl, wh).view(np.int32).copy()).cuda()
+    d_lg = torch.empty(n * 225, dtype=torch.float32, device="cuda")
+    p_big, q_big, _ = device.gn_forward_dev(w, d_b, n, d_logits=d_lg)
+    p_big, q_big = p_big.clone(), q_big.clone()
+    p_sm, q_sm, _ = device.gn_forward_dev(w, d_b, n)
+    torch.cuda.synchronize()
+    assert torch.equal(p_sm.view(torch.int32), p_big.view(torch.int32))
+    assert torch.equal(q_sm.view(torch.int32), q_big.view(torch.int32))
+    _, pr, qr = planner_nets.reference_forward(gsd, dsd, boards.planes_from_cells(cells))
+    np.testing.assert_allclose(p_sm.cpu().numpy().reshape(n, 225), pr, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(q_sm.cpu().numpy().reshape(n, 225), qr, rtol=0, atol=1e-4)
