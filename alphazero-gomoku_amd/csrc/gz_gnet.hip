@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
                                                         const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ list_count,
                                                         const GnTag* __restrict__ tags, char* __restrict__ slots,
-                                                        float* __restrict__ rec) {
+                                                        float* __restrict__ rec, int per) {
     __shared__ __attribute__((aligned(16))) char lds[ILDS];
     GnUnit* U = (GnUnit*)(lds + IU);
     _Float16* col = (_Float16*)(lds + ICOL);
@@ -1208,9 +1208,12 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
     const int count = *list_count;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nt = wave & 3, mh = wave >> 2;
-    for (int pos0 = blockIdx.x * IG; pos0 < count; pos0 += gridDim.x * IG) {
+    // chunks of `per` (<= IG) boards: fewer than IG when the launch has too few rows to
+    // give every CU a chunk of IG (a workgroup's time is a chain of short phases whose
+    // k-loops scale with its tiles)
+    for (int pos0 = blockIdx.x * per; pos0 < count; pos0 += gridDim.x * per) {
         __syncthreads();  // the previous chunk is done with U
-        const int ng = count - pos0 < IG ? count - pos0 : IG;
+        const int ng = count - pos0 < per ? count - pos0 : per;
         if (tid < ng) {
             const int b = list[pos0 + tid];
             const GnTag tg = tags[b];
@@ -1443,9 +1446,16 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
     hipStream_t s = (hipStream_t)stream;
     gn_kernel<<<max_rows < 2 * cus ? max_rows : 2 * cus, NT, 0, s>>>(d_weights, d_rows, max_rows, d_full_count, d_rec,
                                                                      d_full_list, (char*)d_slots, (const GnTag*)d_tags);
-    const int chunks = (max_rows + IG - 1) / IG;
+    int per = (max_rows + IWG * cus - 1) / (IWG * cus);
+    per = per < 1 ? 1 : (per > IG ? IG : per);
+    static const int per_env = [] {  // GZ_GN_INC_PER: a fixed chunk size (A/B)
+        const char* e = getenv("GZ_GN_INC_PER");
+        return e ? atoi(e) : 0;
+    }();
+    if (per_env >= 1 && per_env <= IG) per = per_env;
+    const int chunks = (max_rows + per - 1) / per;
     gn_inc_kernel<<<chunks < IWG * cus ? chunks : IWG * cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
-                                                              (const GnTag*)d_tags, (char*)d_slots, d_rec);
+                                                              (const GnTag*)d_tags, (char*)d_slots, d_rec, per);
     gn_heads_launch(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr, cus, s);
     return gn_launch_check("gn_inc_kernel");
 }
