@@ -638,6 +638,171 @@ __global__ __launch_bounds__(NWS * 64) void gn_heads_small_kernel(const float* _
     }
 }
 
+// The heads split over output tiles, for the same small launches: three launches
+// (policy FC + DQN fc0; fc1; fc2 + the softmax), each workgroup 16 boards x 4 output
+// tiles (a wave per tile, the fragments 5 k-blocks ahead), the layers' outputs through
+// a scratch in global memory.  A launch of 512 rows then has 256 / 128 / 160
+// workgroups instead of 32, each with a quarter of a wave's MFMA chain per tile.
+// Products, their order and the epilogues are gn_heads_kernel's, so p and q are the
+// same bits.
+constexpr int HN_LD = 256;  // scratch row stride (logits 225, hidden 256)
+
+__device__ __forceinline__ void hn_tile(const float* __restrict__ Wp, int KB, int NTILES, int nt, int lane,
+                                        const float* __restrict__ arow, f32x4& acc) {
+    acc = zero4();
+    const int g = lane >> 4;
+    f32x4 a[PFS], b[PFS];
+    const float* bp = Wp + ((size_t)nt * 64 + lane) * 4;
+    const size_t bstep = (size_t)NTILES * 64 * 4;
+#pragma unroll
+    for (int k = 0; k < PFS - 1; k++)
+        if (k < KB) {
+            a[k] = *(const f32x4*)(arow + 16 * k + 4 * g);
+            b[k] = *(const f32x4*)(bp + k * bstep);
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = 0; k0 < KB; k0 += PFS) {
+#pragma unroll
+        for (int j = 0; j < PFS; j++) {
+            const int kb = k0 + j;
+            if (kb >= KB) break;
+            const int kn = kb + PFS - 1, sn = (j + PFS - 1) % PFS;
+            if (kn < KB) {
+                a[sn] = *(const f32x4*)(arow + 16 * kn + 4 * g);
+                b[sn] = *(const f32x4*)(bp + kn * bstep);
+            }
+            // (keeps the loads PFS - 1 blocks ahead: the scheduler would otherwise sink
+            // them next to their MFMAs, 1-2 blocks ahead)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 4; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][t], b[j][t], acc, 0, 0, 0);
+        }
+    }
+}
+
+// acc + bias (ReLU) -> out[b][o] for the tile's live rows and columns
+template <bool RELU>
+__device__ __forceinline__ void hn_put(const f32x4& acc, const float* __restrict__ bias, int nmax, int nt, int lane,
+                                       int b0, int count, float* __restrict__ out, int ld) {
+    const int li = lane & 15, g = lane >> 4, o = 16 * nt + li;
+    if (o >= nmax) return;
+    const float bv = bias[o];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int b = b0 + 4 * g + r;
+        float y = acc[r] + bv;
+        if (RELU) y = y > 0.f ? y : 0.f;
+        if (b < count) out[(size_t)b * ld + o] = y;
+    }
+}
+
+__device__ __forceinline__ int hn_count(int n, const int32_t* d_count) {
+    if (!d_count) return n;
+    const int c = *d_count;
+    return c < n ? c : n;
+}
+
+// stage 0: policy FC (y 0..3: tiles 4y + wave < 15) -> logits, DQN fc0 (y 4..7) -> h0
+__global__ __launch_bounds__(256) void gn_hn0_kernel(const float* __restrict__ W, const float* __restrict__ rec, int n,
+                                                     const int32_t* d_count, float* __restrict__ lg,
+                                                     float* __restrict__ h0) {
+    const int count = hn_count(n, d_count), b0 = blockIdx.x * HBS;
+    if (b0 >= count) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, y = blockIdx.y;
+    const float* arow = rec + (size_t)(b0 + li < count ? b0 + li : count - 1) * REC;
+    f32x4 acc;
+    if (y < 4) {
+        const int nt = 4 * y + wave;
+        if (nt >= 15) return;
+        hn_tile(W + GF_P, REC_X / 16, 15, nt, lane, arow, acc);
+        hn_put<false>(acc, W + GF_B, POS, nt, lane, b0, count, lg, HN_LD);
+    } else {
+        const int nt = 4 * (y - 4) + wave;
+        hn_tile(W + D0_P, (REC - REC_X) / 16, 16, nt, lane, arow + REC_X, acc);
+        hn_put<true>(acc, W + D0_BASE, DQH, nt, lane, b0, count, h0, HN_LD);
+    }
+}
+
+// stage 1: fc1 (y 0..3) h0 -> h1
+__global__ __launch_bounds__(256) void gn_hn1_kernel(const float* __restrict__ W, int n, const int32_t* d_count,
+                                                     const float* __restrict__ h0, float* __restrict__ h1) {
+    const int count = hn_count(n, d_count), b0 = blockIdx.x * HBS;
+    if (b0 >= count) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, nt = 4 * blockIdx.y + wave;
+    const float* arow = h0 + (size_t)(b0 + li < count ? b0 + li : count - 1) * HN_LD;
+    f32x4 acc;
+    hn_tile(W + D1_P, DQH / 16, 16, nt, lane, arow, acc);
+    hn_put<true>(acc, W + D1_B, DQH, nt, lane, b0, count, h1, HN_LD);
+}
+
+// stage 2: fc2 (y 0..3) h1 -> q; y 4: the softmax of the 16 boards' logits -> p
+__global__ __launch_bounds__(256) void gn_hn2_kernel(const float* __restrict__ W, int n, const int32_t* d_count,
+                                                     const float* __restrict__ lg, const float* __restrict__ h1,
+                                                     float* __restrict__ p_out, float* __restrict__ q_out) {
+    const int count = hn_count(n, d_count), b0 = blockIdx.x * HBS;
+    if (b0 >= count) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15;
+    if (blockIdx.y < 4) {
+        const int nt = 4 * blockIdx.y + wave;
+        if (nt >= 15) return;
+        const float* arow = h1 + (size_t)(b0 + li < count ? b0 + li : count - 1) * HN_LD;
+        f32x4 acc;
+        hn_tile(W + D2_P, DQH / 16, 15, nt, lane, arow, acc);
+        const int g = lane >> 4, o = 16 * nt + li;
+        if (o >= POS) return;
+        const float bv = W[D2_B + o];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int b = b0 + 4 * g + r;
+            if (b < count) q_out[(size_t)b * POS + o] = acc[r] + bv;
+        }
+        return;
+    }
+    for (int bb = wave; bb < HBS && b0 + bb < count; bb += 4) {  // gn_heads_kernel's softmax
+        const float* l = lg + (size_t)(b0 + bb) * HN_LD;
+        float x[4];
+        float mx = -3.0e38f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            x[u] = o < POS ? l[o] : -3.0e38f;
+            mx = fmaxf(mx, x[u]);
+        }
+        mx = wave_max(mx);
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            e[u] = o < POS ? __expf(x[u] - mx) : 0.f;
+            sum += e[u];
+        }
+        sum = wave_sum(sum);
+        const size_t base = (size_t)(b0 + bb) * POS;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int o = lane + 64 * u;
+            if (o < POS) p_out[base + o] = e[u] / sum;
+        }
+    }
+}
+
+// the split heads' scratch (logits, h0, h1: 3 x HN_LD floats per row), per device,
+// grown on demand
+static float* hn_scratch(size_t rows) {
+    static float* buf[16] = {};
+    static size_t cap[16] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+    if (rows > cap[dev]) {
+        if (buf[dev]) (void)hipFree(buf[dev]);
+        buf[dev] = nullptr;
+        cap[dev] = 0;
+        if (hipMalloc(&buf[dev], rows * 3 * HN_LD * sizeof(float)) != hipSuccess) return nullptr;
+        cap[dev] = rows;
+    }
+    return buf[dev];
+}
+
 // the heads over max_rows rows (d_count of them live): the small-launch kernel when
 // gn_heads_kernel would not give every CU 2 workgroups of 32 boards (and no logits
 // are asked for)
@@ -647,8 +812,19 @@ static void gn_heads_launch(const float* W, const float* rec, int max_rows, cons
         const char* e = getenv("GZ_GN_SMALL_HEADS");
         return e ? atoi(e) : -1;
     }();
+    static const int split = [] {  // GZ_GN_HEADS_SPLIT=0: one small-launch kernel instead (A/B)
+        const char* e = getenv("GZ_GN_HEADS_SPLIT");
+        return e ? atoi(e) : 1;
+    }();
     const int cap = small_cap >= 0 ? small_cap : 2 * HB * cus;
-    if (!d_logits && max_rows < cap)
+    float* sc = !d_logits && max_rows < cap && split ? hn_scratch((size_t)max_rows) : nullptr;
+    if (sc) {
+        const unsigned gx = (unsigned)((max_rows + HBS - 1) / HBS);
+        float *lg = sc, *h0 = sc + (size_t)max_rows * HN_LD, *h1 = sc + 2 * (size_t)max_rows * HN_LD;
+        gn_hn0_kernel<<<dim3(gx, 8), 256, 0, s>>>(W, rec, max_rows, d_count, lg, h0);
+        gn_hn1_kernel<<<dim3(gx, 4), 256, 0, s>>>(W, max_rows, d_count, h0, h1);
+        gn_hn2_kernel<<<dim3(gx, 5), 256, 0, s>>>(W, max_rows, d_count, lg, h1, d_p, d_q);
+    } else if (!d_logits && max_rows < cap)
         gn_heads_small_kernel<<<(max_rows + HBS - 1) / HBS, NWS * 64, 0, s>>>(W, rec, max_rows, d_count, d_p, d_q);
     else
         gn_heads_kernel<<<(max_rows + HB - 1) / HB, NTH_H, 0, s>>>(W, rec, max_rows, d_count, d_p, d_q, d_logits);
