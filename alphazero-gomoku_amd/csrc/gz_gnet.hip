@@ -646,6 +646,7 @@ __global__ __launch_bounds__(NWS * 64) void gn_heads_small_kernel(const float* _
 // Products, their order and the epilogues are gn_heads_kernel's, so p and q are the
 // same bits.
 constexpr int HN_LD = 256;  // scratch row stride (logits 225, hidden 256)
+constexpr int HN_ROW = 3 * HN_LD;  // scratch floats per row: logits, h0, h1 (in the caller's workspace)
 
 __device__ __forceinline__ void hn_tile(const float* __restrict__ Wp, int KB, int NTILES, int nt, int lane,
                                         const float* __restrict__ arow, f32x4& acc) {
@@ -786,28 +787,11 @@ __global__ __launch_bounds__(256) void gn_hn2_kernel(const float* __restrict__ W
     }
 }
 
-// the split heads' scratch (logits, h0, h1: 3 x HN_LD floats per row), per device,
-// grown on demand
-static float* hn_scratch(size_t rows) {
-    static float* buf[16] = {};
-    static size_t cap[16] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-    if (rows > cap[dev]) {
-        if (buf[dev]) (void)hipFree(buf[dev]);
-        buf[dev] = nullptr;
-        cap[dev] = 0;
-        if (hipMalloc(&buf[dev], rows * 3 * HN_LD * sizeof(float)) != hipSuccess) return nullptr;
-        cap[dev] = rows;
-    }
-    return buf[dev];
-}
-
-// the heads over max_rows rows (d_count of them live): the small-launch kernel when
-// gn_heads_kernel would not give every CU 2 workgroups of 32 boards (and no logits
-// are asked for)
+// the heads over max_rows rows (d_count of them live): split over output tiles when
+// gn_heads_kernel would not give every CU 2 workgroups of 32 boards, no logits are asked
+// for and the caller's workspace holds the scratch (sc: max_rows x HN_ROW floats)
 static void gn_heads_launch(const float* W, const float* rec, int max_rows, const int32_t* d_count, float* d_p,
-                            float* d_q, float* d_logits, int cus, hipStream_t s) {
+                            float* d_q, float* d_logits, int cus, hipStream_t s, float* sc) {
     static const int small_cap = [] {  // GZ_GN_SMALL_HEADS: rows below which the small kernel runs (A/B)
         const char* e = getenv("GZ_GN_SMALL_HEADS");
         return e ? atoi(e) : -1;
@@ -817,8 +801,7 @@ static void gn_heads_launch(const float* W, const float* rec, int max_rows, cons
         return e ? atoi(e) : 1;
     }();
     const int cap = small_cap >= 0 ? small_cap : 2 * HB * cus;
-    float* sc = !d_logits && max_rows < cap && split ? hn_scratch((size_t)max_rows) : nullptr;
-    if (sc) {
+    if (sc && !d_logits && max_rows < cap && split) {
         const unsigned gx = (unsigned)((max_rows + HBS - 1) / HBS);
         float *lg = sc, *h0 = sc + (size_t)max_rows * HN_LD, *h1 = sc + 2 * (size_t)max_rows * HN_LD;
         gn_hn0_kernel<<<dim3(gx, 8), 256, 0, s>>>(W, rec, max_rows, d_count, lg, h0);
@@ -1580,7 +1563,8 @@ extern "C" void gz_internal_set_error(const char* msg);
 
 extern "C" size_t gz_gn_weight_floats(void) { return (size_t)TOTAL; }
 
-extern "C" size_t gz_gn_workspace_bytes(int32_t n) { return (size_t)(n < 1 ? 1 : n) * REC * sizeof(float); }
+// n records, then the split heads' scratch for n rows
+extern "C" size_t gz_gn_workspace_bytes(int32_t n) { return (size_t)(n < 1 ? 1 : n) * (REC + HN_ROW) * sizeof(float); }
 
 static int gn_cus() {
     int dev = 0, cus = 256;
@@ -1616,7 +1600,8 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
                                              const int32_t* d_count, const int32_t* d_full_list,
                                              const int32_t* d_full_count, const int32_t* d_inc_list,
                                              const int32_t* d_inc_count, const void* d_tags, void* d_slots,
-                                             float* d_p, float* d_q, float* d_rec, void* stream) {
+                                             float* d_p, float* d_q, float* d_rec, float* d_hscratch,
+                                             void* stream) {
     if (max_rows <= 0) return GZ_OK;
     const int cus = gn_cus();
     hipStream_t s = (hipStream_t)stream;
@@ -1632,7 +1617,7 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
     const int chunks = (max_rows + per - 1) / per;
     gn_inc_kernel<<<chunks < IWG * cus ? chunks : IWG * cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
                                                               (const GnTag*)d_tags, (char*)d_slots, d_rec, per);
-    gn_heads_launch(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr, cus, s);
+    gn_heads_launch(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr, cus, s, d_hscratch);
     return gn_launch_check("gn_inc_kernel");
 }
 
@@ -1649,7 +1634,7 @@ extern "C" size_t gz_gn_slot_bytes(void) { return SLOT_BYTES; }
 
 extern "C" size_t gz_gn_chain_workspace_bytes(int32_t n) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
-    return m * REC * 4 + 2 * m * 4 + 256;
+    return m * (REC + HN_ROW) * 4 + 2 * m * 4 + 256;
 }
 
 extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boards, int32_t n, const void* d_tags,
@@ -1661,7 +1646,8 @@ extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boa
     if (n == 0) return GZ_OK;
     hipStream_t s = (hipStream_t)stream;
     float* rec = (float*)d_workspace;
-    int32_t* lists = (int32_t*)(rec + (size_t)n * REC);
+    float* hsc = rec + (size_t)n * REC;
+    int32_t* lists = (int32_t*)(hsc + (size_t)n * HN_ROW);
     int32_t* counts = lists + 2 * (size_t)n;
     if (hipMemsetAsync(counts, 0, 8, s) != hipSuccess) {
         gz_internal_set_error("gz_gn_forward_chain: memset");
@@ -1671,7 +1657,7 @@ extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boa
     int rc = gn_launch_check("gn_split_kernel");
     if (rc) return rc;
     return gz_internal_gn_forward_tagged(d_weights, d_boards, n, nullptr, lists, counts, lists + n, counts + 1,
-                                         d_tags, d_slots, d_p, d_q, rec, stream);
+                                         d_tags, d_slots, d_p, d_q, rec, hsc, stream);
 }
 
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
@@ -1687,7 +1673,8 @@ extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, i
     int grid = n < 2 * cus ? n : 2 * cus;
     hipStream_t s = (hipStream_t)stream;
     gn_kernel<<<grid, NT, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace, nullptr, nullptr, nullptr);
-    gn_heads_launch(d_weights, (const float*)d_workspace, n, d_count, d_p, d_q, d_logits, cus, s);
+    gn_heads_launch(d_weights, (const float*)d_workspace, n, d_count, d_p, d_q, d_logits, cus, s,
+                    (float*)d_workspace + (size_t)n * REC);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gz_internal_set_error((std::string("gn_kernel: ") + hipGetErrorString(e)).c_str());

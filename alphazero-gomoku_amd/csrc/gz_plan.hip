@@ -88,7 +88,9 @@ struct GnStats {
 
 __host__ __device__ inline size_t ctx_stride(int S) { return sizeof(PlanCtx) + tree_bytes_for(S); }
 
-constexpr size_t GN_REC_BYTES = 928 * 4;  // = gz_gn_workspace_bytes(1) (gz_gnet.h REC), checked at run time
+constexpr size_t GN_REC_BYTES = 928 * 4;  // a net record (gz_gnet.h REC)
+// gz_gn_workspace_bytes(1): the record + the split heads' scratch (3 x 256 floats), checked at run time
+constexpr size_t GN_WS_BYTES = GN_REC_BYTES + 3 * 256 * 4;
 
 struct Workspace {
     char* ctx;
@@ -96,7 +98,7 @@ struct Workspace {
     uint32_t* gn_in;   // [C][16] (C = chunk_rows: the GN rows of one planner step)
     float* gn_p;       // [C][225]
     float* gn_q;
-    float* gn_rec;     // gz_gn_forward's workspace for C rows
+    float* gn_rec;     // gz_gn_forward's workspace for C rows (records, then the heads' scratch)
     int32_t* rows;     // row -> job
     Counters* ctr;
     GnStats* stats;
@@ -138,7 +140,7 @@ __host__ __device__ inline Workspace carve(void* base, int n, int S) {
     w.gn_q = (float*)p;
     p += align256(C * 225 * 4);
     w.gn_rec = (float*)p;
-    p += align256(C * GN_REC_BYTES);
+    p += align256(C * GN_WS_BYTES);
     w.rows = (int32_t*)p;
     p += align256(C * 4);
     w.tags = (GnTag*)p;
@@ -152,7 +154,7 @@ __host__ __device__ inline Workspace carve(void* base, int n, int S) {
     w.chk_q = (float*)p;
     p += align256(C * 225 * 4);
     w.chk_rec = (float*)p;
-    p += align256(C * GN_REC_BYTES);
+    p += align256(C * GN_WS_BYTES);
     w.slots = p;
     p += align256(((size_t)n + C) * gzgn::SLOT_BYTES);
     w.end = (size_t)(p - (char*)base);
@@ -982,7 +984,8 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
                                              const int32_t* d_count, const int32_t* d_full_list,
                                              const int32_t* d_full_count, const int32_t* d_inc_list,
                                              const int32_t* d_inc_count, const void* d_tags, void* d_slots,
-                                             float* d_p, float* d_q, float* d_rec, void* stream);
+                                             float* d_p, float* d_q, float* d_rec, float* d_hscratch,
+                                             void* stream);
 
 static int plan_fail(int code, const char* msg) {
     gz_internal_set_error(msg);
@@ -1016,7 +1019,7 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
     if (gather && (!d_leaves || !d_leaf_count || leaf_cap < 0))
         return plan_fail(GZ_ERR_ARG, "gz_plan_search: leaf gathering needs d_leaves and d_leaf_count");
     if (n == 0) return GZ_OK;
-    if (gz_gn_workspace_bytes(1) != GN_REC_BYTES)
+    if (gz_gn_workspace_bytes(1) != GN_WS_BYTES)
         return plan_fail(GZ_ERR_INTERNAL, "gz_plan_search: planner-net record size mismatch");
     hipStream_t s = (hipStream_t)stream;
     const int S = p->num_simulations;
@@ -1058,7 +1061,7 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         } else {
             if ((r = gz_internal_gn_forward_tagged(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.full_list,
                                                    &w.ctr->nfull, w.inc_list, &w.ctr->ninc, w.tags, w.slots, w.gn_p,
-                                                   w.gn_q, w.gn_rec, stream)))
+                                                   w.gn_q, w.gn_rec, w.gn_rec + (size_t)max_rows * 928, stream)))
                 return r;
             plan_gn_count_kernel<<<1, 1, 0, s>>>(w);
             if ((r = plan_check("plan_gn_count_kernel"))) return r;

@@ -234,8 +234,13 @@ int gz_pv_tree_exec_tiles(const void* d_workspace, int32_t n, int32_t* d_out2, v
  * gzero/planner_nets.py).  Boards [n][16] uint32 bit planes (d_count as above).
  * Outputs: p = softmax(GraphNet(planes)) [n][225], q = OpponentDQN(planes)
  * [n][225], logits [n][225] or NULL.  GraphNet convs in f16x3 (as GZ_PV_F16X3);
- * the policy FC and the DQN run batched over 64 boards (fp32 MFMA).
- * d_workspace: gz_gn_workspace_bytes(n) bytes, required. */
+ * the policy FC and the DQN run batched over 32 boards per workgroup (fp32 MFMA);
+ * a launch of fewer than 64 boards per CU without logits runs them split over output
+ * tiles instead (16 boards x 4 tiles per workgroup, three launches, p and q the same
+ * bits), the layers' outputs through the workspace.  GZ_GN_SMALL_HEADS=<rows> moves
+ * that threshold, GZ_GN_HEADS_SPLIT=0 runs a one-kernel variant instead (A/B knobs).
+ * d_workspace: gz_gn_workspace_bytes(n) bytes, required (per row a 3.6 KB net record,
+ * then 3 KB of the split heads' scratch). */
 size_t gz_gn_weight_floats(void);
 size_t gz_gn_workspace_bytes(int32_t n);
 int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
@@ -249,10 +254,11 @@ int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, c
  * gz_plan_workspace_bytes(n, num_simulations) bytes.  d_trees (optional) gets
  * gz_tree_bytes(num_simulations) bytes per game in gz_search's layout.
  * Footprint (C = max(n, 65536) GN rows per planner step, capped at n*S): per game
- * its context + tree and S 128-B jobs; per row 0.9 KB of p / q, a 3.6 KB net record
- * and, always reserved, the same again for GZ_FLAG_GN_CHECK's full-forward copy
- * (0.36 GB at C = 65536); and n + C incremental-GraphNet map slots of 232 KB
- * (16.2 GB at n = 4096, S = 200 -- 16.9 GB in all). */
+ * its context + tree and S 128-B jobs; per row 0.9 KB of p / q, a 6.6 KB net
+ * workspace (gz_gn_workspace_bytes(1)) and, always reserved, the same again for
+ * GZ_FLAG_GN_CHECK's full-forward copy (0.56 GB each at C = 65536); and n + C
+ * incremental-GraphNet map slots of 232 KB (16.2 GB at n = 4096, S = 200 -- 17.4 GB
+ * in all). */
 size_t gz_plan_workspace_bytes(int32_t n, int32_t num_simulations);
 int gz_plan_search(const gz_board_state* d_boards, const int64_t* d_game_ids, int32_t n,
                    const gz_search_params* p, const gz_planner_params* pp, const float* d_gn_weights,
