@@ -201,6 +201,13 @@ struct PlanShared {
     uint8_t grid[GRID_BYTES];
     int32_t base;
 };
+// plan_step_kernel's workgroup of PW waves: the cells' scores and the waves' pattern parts
+constexpr int PW = 4;
+struct PlanShared4 {
+    PlanShared s;
+    double sc[PW * WAVE];
+    int32_t part[PW];
+};
 
 __device__ inline int pow3(int i) {
     const int P3[8] = {1, 3, 9, 27, 81, 243, 729, 2187};
@@ -240,7 +247,100 @@ __device__ inline bool new_five_through(const uint8_t* grid, int g0, int who) {
     return false;
 }
 
-// KnowledgeSearch.score_move(board, m, P) (bg_planner.py:90-106) of every cell,
+// window codes (wrt P) of `cell` into sh->code; returns its pattern(board, P) part
+__device__ __forceinline__ int cell_codes(PlanShared* sh, int cell, const BB& Pst, int P) {
+    const int DR[4] = {1, 0, 1, 1}, DC[4] = {0, 1, 1, -1};  // bg_planner.py:147
+    const int r = cell / GZ_N, c = cell % GZ_N;
+    const int g0 = (r + 4) * GRID_W + (c + 4);
+    const bool isP = bb_test(Pst, r * 16 + c);
+    int part = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int step = DR[d] * GRID_W + DC[d];
+        int code = 0, pw = 1;
+#pragma unroll
+        for (int k = -4; k <= 4; k++) {
+            if (k == 0) continue;
+            const int v = sh->grid[g0 + k * step];
+            code += (v == P ? 0 : (v == 0 ? 1 : 2)) * pw;
+            pw *= 3;
+        }
+        sh->code[cell][d] = (uint16_t)code;
+        if (isP) part += GZ_PATTERN_LUT[code];
+    }
+    return part;
+}
+
+// KnowledgeSearch.score_move(board, m, P) (bg_planner.py:90-106) of one cell (-inf
+// for occupied / off-board cells), given the codes of every cell and pattern(board, P)
+struct KsCtx {
+    BB E, Wm, Fo, Pst;
+    int mover, P, oppP, n_moves, ne;
+};
+__device__ __forceinline__ KsCtx ks_ctx(const BB& black, const BB& white, int mover, int n_moves, int P) {
+    KsCtx k;
+    k.E = empties(black, white);
+    k.ne = bb_count(k.E);
+    const BB mine = mover == 1 ? black : white;
+    k.Pst = P == 1 ? black : white;
+    k.oppP = 3 - P;
+    const BB Ost = k.oppP == 1 ? black : white;
+    k.Wm = threats(mine).win & k.E;  // cells where the mover completes five
+    k.Fo = threats(Ost).win & k.E;   // cells where P's opponent completes five
+    k.mover = mover;
+    k.P = P;
+    k.n_moves = n_moves;
+    return k;
+}
+__device__ __forceinline__ double cell_score(const PlanShared* sh, int cell, const KsCtx& k, int base) {
+    const int DR[4] = {1, 0, 1, 1}, DC[4] = {0, 1, 1, -1};
+    if (cell >= GZ_CELLS) return -__builtin_inf();
+    const int r = cell / GZ_N, c = cell % GZ_N, bit = r * 16 + c;
+    if (!bb_test(k.E, bit)) return -__builtin_inf();
+    const bool win = bb_test(k.Wm, bit);
+    if (win && k.mover == k.P) return 1e6;
+    bool opp_wins;
+    if (win || k.n_moves + 1 >= 200 || k.ne == 1) {
+        // the move ends the game: make_move fails on the copies, which keep
+        // the old winner -- P's opponent iff it just won (and a cell is left)
+        opp_wins = win && k.ne > 1;
+    } else if (k.mover == k.P) {
+        BB f = k.Fo;
+        f.w[bit >> 5] &= ~(1u << (bit & 31));
+        opp_wins = bb_any(f);
+    } else {
+        // the mover is P's opponent: after m it completes five at a cell f != m
+        // iff f already did (Fo) or a five-window through m holds 3 of its
+        // stones, m and the empty f (new_five_through)
+        BB f = k.Fo;
+        f.w[bit >> 5] &= ~(1u << (bit & 31));
+        opp_wins = bb_any(f) || new_five_through(sh->grid, (r + 4) * GRID_W + (c + 4), k.oppP);
+    }
+    if (opp_wins) return -1e5;
+    const int nd = k.mover == k.P ? 0 : 2;  // digit of the new stone wrt P
+    int delta = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+#pragma unroll
+        for (int q = -4; q <= 4; q++) {
+            if (q == 0) continue;
+            const int rr = r + q * DR[d], cc = c + q * DC[d];
+            if (rr < 0 || rr >= GZ_N || cc < 0 || cc >= GZ_N) continue;
+            if (!bb_test(k.Pst, rr * 16 + cc)) continue;
+            const int code = sh->code[rr * GZ_N + cc][d];
+            const int j = 4 - q;  // m's slot in the window of the stone at offset q
+            const int i = j < 4 ? j : j - 1;
+            delta += GZ_PATTERN_LUT[code + (nd - 1) * pow3(i)] - GZ_PATTERN_LUT[code];
+        }
+        if (k.mover == k.P) delta += GZ_PATTERN_LUT[sh->code[cell][d]];
+    }
+    const int dist = (r > 7 ? r - 7 : 7 - r) + (c > 7 ? c - 7 : 7 - c);
+    const double cb = (6 - dist) * 0.5;
+    return (double)(base + delta) + (cb > 0.0 ? cb : 0.0);
+}
+
+// KnowledgeSearch.score_move(board, m, P) (bg_planner.py:90-106) of every cell, one wave
+// (cell_codes / cell_score's work, kept as one body: split, the one-wave kernel spilled more),
 // lane-strided: sc[s] is cell lane + 64 s (-inf for occupied / off-board cells);
 // returns the number of empty cells.
 __device__ __forceinline__ int knowledge_scores(PlanShared* sh, const BB& black, const BB& white, int mover,
@@ -380,6 +480,79 @@ __device__ int planner_pick(PlanShared* sh, const BB& black, const BB& white, in
     int best = sh->top[ci];
     if (to_unit(draw(key, (*cnt)++)) < pp.explore) best = sh->top[below(draw(key, (*cnt)++), (uint32_t)m)];
     __syncthreads();
+    return best;
+}
+
+// planner_pick with PW waves: the window codes and the cells' scores one cell per
+// thread (the heavy part, 4 cells per lane with one wave), then wave 0 alone as
+// planner_pick: top-k, compose, explore -- the same scores, so the same move and draws.
+// Returns the move in wave 0 (-1 elsewhere).
+__device__ int planner_pick4(PlanShared4* sh4, const BB& black, const BB& white, int mover, int n_moves, int P,
+                             const gz_planner_params& pp, const float* __restrict__ pv, const float* __restrict__ qv,
+                             uint64_t key, uint32_t* cnt) {
+    PlanShared* sh = &sh4->s;
+    const int lane = lane_id(), wave = threadIdx.x / WAVE, t = threadIdx.x;
+    const KsCtx k = ks_ctx(black, white, mover, n_moves, P);
+    for (int idx = t; idx < GRID_CELLS; idx += PW * WAVE) {
+        const int r = idx / GRID_W - 4, c = idx % GRID_W - 4;
+        uint8_t v = 3;
+        if (r >= 0 && r < GZ_N && c >= 0 && c < GZ_N) {
+            const int b = r * 16 + c;
+            v = bb_test(black, b) ? 1 : (bb_test(white, b) ? 2 : 0);
+        }
+        sh->grid[idx] = v;
+    }
+    __syncthreads();
+    const int part = t < GZ_CELLS ? cell_codes(sh, t, k.Pst, P) : 0;
+    const long long wp = wave_sum_ll(part);
+    if (lane == 0) sh4->part[wave] = (int)wp;
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int w = 0; w < PW; w++) base += sh4->part[w];
+    sh4->sc[t] = cell_score(sh, t, k, base);
+    __syncthreads();
+    int best = -1;
+    if (wave == 0) {
+        double sc[4];
+        int cl[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            cl[s] = lane + 64 * s;
+            sc[s] = sh4->sc[cl[s]];
+        }
+        // top-k: Python's stable sort, descending (score desc, row-major asc)
+        const int m = k.ne < pp.k ? k.ne : pp.k;
+        for (int rnk = 0; rnk < m; rnk++) {
+            double bv = -__builtin_inf();
+            int bi = INT_MAX;
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+                if (sc[s] > bv || (sc[s] == bv && cl[s] < bi && sc[s] != -__builtin_inf())) {
+                    bv = sc[s];
+                    bi = cl[s];
+                }
+            wave_argmax(bv, bi);
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+                if (cl[s] == bi) sc[s] = -__builtin_inf();
+            if (lane == 0) sh->top[rnk] = bi;
+        }
+        // (the top-k list is this wave's: its LDS writes are visible to it)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        // compose: first strict maximum of alpha*p - (1-alpha)*q in top-k order (fp64)
+        double cv = -__builtin_inf();
+        int ci = INT_MAX;
+        if (lane < m) {
+            const int cell = sh->top[lane];
+            cv = pp.alpha * (double)pv[cell] - (1 - pp.alpha) * (double)qv[cell];
+            ci = lane;
+        }
+        wave_argmax(cv, ci);
+        best = sh->top[ci];
+        if (to_unit(draw(key, (*cnt)++)) < pp.explore) best = sh->top[below(draw(key, (*cnt)++), (uint32_t)m)];
+    }
     return best;
 }
 
@@ -644,27 +817,39 @@ __global__ void plan_gn_check_kernel(Workspace w) {
     }
 }
 
+// one planner ply (BGPlannerAI.get_move + make_move) per collected row
+// (at least 3 waves per SIMD: 178 -> 168 VGPRs, config 4 +4.5 %)
 __global__ void plan_gn_count_kernel(Workspace w) {
     atomicAdd((unsigned long long*)&w.stats->full, (unsigned long long)w.ctr->nfull);
     atomicAdd((unsigned long long*)&w.stats->inc, (unsigned long long)w.ctr->ninc);
 }
 
-// one planner ply (BGPlannerAI.get_move + make_move) per collected row
-// (at least 3 waves per SIMD: 178 -> 168 VGPRs, config 4 +4.5 %)
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3, 8))) void plan_step_kernel(Workspace w, gz_planner_params pp) {
-    __shared__ PlanShared sh;
+// one planner ply of row blockIdx.x; with PW waves (count_rows) it also adds the
+// incremental planner nets' row counts to the search statistics (the GN forward of this
+// step is complete): plan_gn_count_kernel without a launch (in the one-wave kernel the
+// atomics cost it 30 more spilled registers)
+template <int NWV, class SH>
+__device__ __forceinline__ void plan_step_row(Workspace& w, const gz_planner_params& pp, int count_rows, SH* sh) {
     const int row = blockIdx.x;
+    if (NWV > 1 && count_rows && row == 0 && threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&w.stats->full, (unsigned long long)w.ctr->nfull);
+        atomicAdd((unsigned long long*)&w.stats->inc, (unsigned long long)w.ctr->ninc);
+    }
     if (row >= w.ctr->rows) return;
-    const int lane = lane_id();
     PlanJob& j = w.jobs[w.rows[row]];
     BB black, white;
     load_bb(black, j.black);
     load_bb(white, j.white);
     const int mover = j.mover, n_moves = j.n_moves, P = j.ai;
     uint32_t cnt = j.cnt;
-    const int mv = planner_pick(&sh, black, white, mover, n_moves, P, pp, w.gn_p + (size_t)row * 225,
-                                w.gn_q + (size_t)row * 225, j.key, &cnt);
-    if (lane == 0) {  // make_move (gomoku_board.py:84-113)
+    int mv;
+    if constexpr (NWV == 1)
+        mv = planner_pick(sh, black, white, mover, n_moves, P, pp, w.gn_p + (size_t)row * 225,
+                          w.gn_q + (size_t)row * 225, j.key, &cnt);
+    else
+        mv = planner_pick4(sh, black, white, mover, n_moves, P, pp, w.gn_p + (size_t)row * 225,
+                           w.gn_q + (size_t)row * 225, j.key, &cnt);
+    if (threadIdx.x == 0) {  // make_move (gomoku_board.py:84-113)
         const int bit = cell_to_bit(mv);
         BB& mine = mover == 1 ? black : white;
         const BB E = empties(black, white);
@@ -684,6 +869,18 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
         }
         j.row = -1;
     }
+}
+// large launches (round 0): a wave per row, at least 3 waves per SIMD (178 -> 168
+// VGPRs, config 4 +4.5 %)
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3, 8))) void plan_step_kernel(
+    Workspace w, gz_planner_params pp, int count_rows) {
+    __shared__ PlanShared sh;
+    plan_step_row<1>(w, pp, count_rows, &sh);
+}
+// small launches (the sequential rounds: a row per game): PW waves per row
+__global__ __launch_bounds__(PW * WAVE) void plan_step4_kernel(Workspace w, gz_planner_params pp, int count_rows) {
+    __shared__ PlanShared4 sh;
+    plan_step_row<PW>(w, pp, count_rows, &sh);
 }
 
 // offensive rollout (_simulate :276-285) of every job past its planner plies
@@ -1063,8 +1260,6 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
                                                    &w.ctr->nfull, w.inc_list, &w.ctr->ninc, w.tags, w.slots, w.gn_p,
                                                    w.gn_q, w.gn_rec, w.gn_rec + (size_t)max_rows * 928, stream)))
                 return r;
-            plan_gn_count_kernel<<<1, 1, 0, s>>>(w);
-            if ((r = plan_check("plan_gn_count_kernel"))) return r;
             if (check) {
                 if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.chk_p, w.chk_q, nullptr,
                                        w.chk_rec, stream)))
@@ -1073,7 +1268,17 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
                 if ((r = plan_check("plan_gn_check_kernel"))) return r;
             }
         }
-        plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp);
+        // PW waves per row when the launch leaves CUs idle (GZ_PLAN_STEP4: that row cap, A/B)
+        static const int cap4 = [] {
+            const char* e = getenv("GZ_PLAN_STEP4");
+            return e ? atoi(e) : 4096;
+        }();
+        if (max_rows <= cap4) {
+            plan_step4_kernel<<<max_rows, PW * WAVE, 0, s>>>(w, *pp, inc ? 1 : 0);
+        } else {
+            if (inc) plan_gn_count_kernel<<<1, 1, 0, s>>>(w);
+            plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp, 0);
+        }
         return plan_check("plan_step_kernel");
     };
     for (int round = 0;; round++) {
