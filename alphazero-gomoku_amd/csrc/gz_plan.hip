@@ -1281,13 +1281,23 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         }
         return plan_check("plan_step_kernel");
     };
+    // The pending count is read (one host synchronisation) every `every` rounds only: a
+    // round after the last is a no-op (no job is collected, rolled out or resumed when no
+    // game has a pending simulation), so the rounds in between are launched unread.
+    static const int every = [] {
+        const char* e = getenv("GZ_PLAN_SYNC_EVERY");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : v;
+    }();
     for (int round = 0;; round++) {
-        int32_t pending = 0;
-        if (hipMemcpyAsync(&pending, &w.ctr->pending, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return plan_fail(GZ_ERR_HIP, "gz_plan_search: reading the pending count");
-        if (pending == 0) break;
-        if (round > S + 1) return plan_fail(GZ_ERR_INTERNAL, "gz_plan_search: search did not terminate");
+        if (round % every == 0) {
+            int32_t pending = 0;
+            if (hipMemcpyAsync(&pending, &w.ctr->pending, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return plan_fail(GZ_ERR_HIP, "gz_plan_search: reading the pending count");
+            if (pending == 0) break;
+        }
+        if (round > S + 1 + every) return plan_fail(GZ_ERR_INTERNAL, "gz_plan_search: search did not terminate");
         if (round == 0) {  // every job of the parallel phase, C at a time
             for (int j0 = 0; j0 < n_jobs; j0 += C) {
                 const int j1 = j0 + C < n_jobs ? j0 + C : n_jobs;
