@@ -101,6 +101,7 @@ struct Workspace {
     float* gn_rec;     // gz_gn_forward's workspace for C rows (records, then the heads' scratch)
     int32_t* rows;     // row -> job
     Counters* ctr;
+    Counters* ctr2;    // a planner step's rows / nfull / ninc alternate between ctr and ctr2
     GnStats* stats;
     GnTag* tags;       // [C] incremental tags of the rows
     int32_t* full_list, *inc_list;  // [C] rows by kind
@@ -126,7 +127,8 @@ __host__ __device__ inline Workspace carve(void* base, int n, int S) {
     const size_t nj = (size_t)n * (S > 0 ? S : 1), C = chunk_rows(n, S);
     Workspace w;
     w.ctr = (Counters*)p;
-    p += align256(sizeof(Counters));
+    w.ctr2 = w.ctr + 1;
+    p += align256(2 * sizeof(Counters));
     w.stats = (GnStats*)p;
     p += align256(sizeof(GnStats));
     w.ctx = p;
@@ -878,8 +880,12 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
     plan_step_row<1>(w, pp, count_rows, &sh);
 }
 // small launches (the sequential rounds: a row per game): PW waves per row
-__global__ __launch_bounds__(PW * WAVE) void plan_step4_kernel(Workspace w, gz_planner_params pp, int count_rows) {
+__global__ __launch_bounds__(PW * WAVE) void plan_step4_kernel(Workspace w, gz_planner_params pp, int count_rows,
+                                                               Counters* next) {
     __shared__ PlanShared4 sh;
+    // the next planner step's counters (the other set: every kernel of the step that used
+    // it is done) -- hipMemsetAsync's work, without a launch
+    if (blockIdx.x == 0 && threadIdx.x < 4) (&next->rows)[threadIdx.x] = 0;
     plan_step_row<PW>(w, pp, count_rows, &sh);
 }
 
@@ -1230,7 +1236,7 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
     const bool inc = p->planner_steps > 0 && !(env && env[0] == '0');
     const bool check = inc && (p->flags & GZ_FLAG_GN_CHECK) != 0;
     int rc;
-    if (hipMemsetAsync(w.ctr, 0, sizeof(Counters), s) != hipSuccess)
+    if (hipMemsetAsync(w.ctr, 0, 2 * sizeof(Counters), s) != hipSuccess)
         return plan_fail(GZ_ERR_HIP, "gz_plan_search: memset");
     if (hipMemsetAsync(w.jobs, 0, sizeof(PlanJob) * (size_t)n_jobs, s) != hipSuccess)
         return plan_fail(GZ_ERR_HIP, "gz_plan_search: memset");
@@ -1242,29 +1248,38 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         if ((rc = gz_internal_gn_roots(d_gn_weights, w.gn_in, n, w.slots, w.gn_rec, stream))) return rc;
     }
     // one planner step over jobs [j0, j1): collect -> GraphNet + DQN -> planner move
+    // planner step k uses counter set k & 1 (rows, nfull, ninc; pending is w.ctr's, read
+    // only around resume); the set is zeroed by the previous step's plan_step4_kernel, or
+    // here when that step ran the one-wave kernel
+    int step_no = 0;
+    bool zeroed = true;  // (both sets cleared above)
     auto planner_step = [&](int j0, int j1, int max_rows, int slot_game) -> int {
         int r;
+        Workspace wk = w;
+        wk.ctr = (step_no & 1) ? w.ctr2 : w.ctr;
+        Counters* next = (step_no & 1) ? w.ctr : w.ctr2;
+        step_no++;
         // rows, pending (recomputed by the next resume), nfull, ninc
-        if (hipMemsetAsync(&w.ctr->rows, 0, 16, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
+        if (!zeroed && hipMemsetAsync(&wk.ctr->rows, 0, 16, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
         // jobs j0 .. j1-1 (round 0's chunk), or (slot_game) the one job per game at g * S
         const int cnt = slot_game ? n : j1 - j0, stride = slot_game ? S : 1;
-        plan_collect_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(w, S, n, j0, cnt, stride, p->planner_steps, 0,
+        plan_collect_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(wk, S, n, j0, cnt, stride, p->planner_steps, 0,
                                                                inc ? 1 : 0, slot_game);
         if ((r = plan_check("plan_collect_kernel"))) return r;
         if (!inc) {
-            if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
+            if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &wk.ctr->rows, w.gn_p, w.gn_q, nullptr, w.gn_rec,
                                    stream)))
                 return r;
         } else {
-            if ((r = gz_internal_gn_forward_tagged(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.full_list,
-                                                   &w.ctr->nfull, w.inc_list, &w.ctr->ninc, w.tags, w.slots, w.gn_p,
+            if ((r = gz_internal_gn_forward_tagged(d_gn_weights, w.gn_in, max_rows, &wk.ctr->rows, w.full_list,
+                                                   &wk.ctr->nfull, w.inc_list, &wk.ctr->ninc, w.tags, w.slots, w.gn_p,
                                                    w.gn_q, w.gn_rec, w.gn_rec + (size_t)max_rows * 928, stream)))
                 return r;
             if (check) {
-                if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &w.ctr->rows, w.chk_p, w.chk_q, nullptr,
+                if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &wk.ctr->rows, w.chk_p, w.chk_q, nullptr,
                                        w.chk_rec, stream)))
                     return r;
-                plan_gn_check_kernel<<<max_rows, 256, 0, s>>>(w);
+                plan_gn_check_kernel<<<max_rows, 256, 0, s>>>(wk);
                 if ((r = plan_check("plan_gn_check_kernel"))) return r;
             }
         }
@@ -1274,10 +1289,12 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
             return e ? atoi(e) : 4096;
         }();
         if (max_rows <= cap4) {
-            plan_step4_kernel<<<max_rows, PW * WAVE, 0, s>>>(w, *pp, inc ? 1 : 0);
+            plan_step4_kernel<<<max_rows, PW * WAVE, 0, s>>>(wk, *pp, inc ? 1 : 0, next);
+            zeroed = true;
         } else {
-            if (inc) plan_gn_count_kernel<<<1, 1, 0, s>>>(w);
-            plan_step_kernel<<<max_rows, WAVE, 0, s>>>(w, *pp, 0);
+            if (inc) plan_gn_count_kernel<<<1, 1, 0, s>>>(wk);
+            plan_step_kernel<<<max_rows, WAVE, 0, s>>>(wk, *pp, 0);
+            zeroed = false;
         }
         return plan_check("plan_step_kernel");
     };
