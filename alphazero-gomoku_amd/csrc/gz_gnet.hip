@@ -503,142 +503,12 @@ __global__ __launch_bounds__(NTH_H, 64 / HB) void gn_heads_kernel(const float* _
 }
 
 
-// The same heads for small launches (the planner's sequential rounds: one row per
-// game, 512 rows in config 5): gn_heads_kernel's 32 boards and 4 waves per workgroup
-// give such a launch 16 workgroups whose fp32-MFMA chains (90 k-blocks x 32 MFMAs per
-// wave) set its time.  Here 16 boards (one M tile) and 8 waves (n-tiles w, w + 8) per
-// workgroup -- 4x the workgroups, a quarter of the chain -- and the A / B fragments 5
-// k-blocks ahead (the chain is too short to hide an L2 round trip one block ahead).
-// Every output element takes the same products in the same order (k-block ascending,
-// t = 0..3); DQN fc0 runs over all 29 k-blocks (the skipped blocks of gn_heads_kernel
-// add +-0 products only, so both are bitwise the dense GEMM).
-constexpr int HBS = 16, NWS = 8, NQS = 16 / NWS, PFS = 6;
+// Small launches (the planner's sequential rounds: one row per game, 512 rows in config
+// 5): gn_heads_kernel's 32 boards and 4 waves per workgroup give such a launch 16
+// workgroups whose fp32-MFMA chains (90 k-blocks x 32 MFMAs per wave) set its time.
+constexpr int HBS = 16, PFS = 6;  // boards per workgroup; k-blocks of fragments in flight
 
-template <int KB, int NTILES>
-__device__ __forceinline__ void heads_gemm_s(const float* __restrict__ Wp, int lane, const int (&nt)[NQS], int ntn,
-                                             f32x4 (&acc)[NQS], const float* __restrict__ arow) {
-#pragma unroll
-    for (int q = 0; q < NQS; q++) acc[q] = zero4();
-    const int g = lane >> 4;
-    f32x4 a[PFS], b[PFS][NQS];
-    auto load = [&](int kb, int st) {
-        a[st] = *(const f32x4*)(arow + 16 * kb + 4 * g);
-#pragma unroll
-        for (int q = 0; q < NQS; q++)
-            b[st][q] = q < ntn ? *(const f32x4*)(Wp + (((size_t)kb * NTILES + nt[q]) * 64 + lane) * 4) : zero4();
-    };
-#pragma unroll
-    for (int kb = 0; kb < PFS - 1 && kb < KB; kb++) load(kb, kb);
-#pragma unroll
-    for (int kb = 0; kb < KB; kb++) {
-        if (kb + PFS - 1 < KB) load(kb + PFS - 1, (kb + PFS - 1) % PFS);
-        const int st = kb % PFS;
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int q = 0; q < NQS; q++)
-                if (q < ntn) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st][t], b[st][q][t], acc[q], 0, 0, 0);
-    }
-}
-
-template <bool RELU>
-__device__ __forceinline__ void heads_put_s(const f32x4 (&acc)[NQS], const float* __restrict__ bias, int nmax,
-                                            const int (&nt)[NQS], int ntn, int lane, float* dst, int stride) {
-    const int li = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int q = 0; q < NQS; q++) {
-        if (q >= ntn) continue;
-        const int o = 16 * nt[q] + li;
-        if (o >= nmax) continue;
-        const float bv = bias[o];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            float y = acc[q][r] + bv;
-            if (RELU) y = y > 0.f ? y : 0.f;
-            dst[(4 * g + r) * stride + o] = y;
-        }
-    }
-}
-
-__global__ __launch_bounds__(NWS * 64) void gn_heads_small_kernel(const float* __restrict__ W,
-                                                                 const float* __restrict__ rec, int n,
-                                                                 const int32_t* d_count, float* __restrict__ p_out,
-                                                                 float* __restrict__ q_out) {
-    __shared__ __attribute__((aligned(16))) float ra[HBS * H_STRIDE];
-    __shared__ __attribute__((aligned(16))) float rb[HBS * H_STRIDE];
-    int count = n;
-    if (d_count) {
-        const int c = *d_count;
-        count = c < n ? c : n;
-    }
-    const int b0 = blockIdx.x * HBS;
-    if (b0 >= count) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int li = lane & 15, g = lane >> 4;
-    const float* arow = rec + (size_t)(b0 + li < count ? b0 + li : count - 1) * REC;
-    int nt[NQS];
-    int ntn_p = 0;
-#pragma unroll
-    for (int q = 0; q < NQS; q++) {
-        nt[q] = wave + NWS * q;
-        ntn_p += nt[q] < 15;
-    }
-    f32x4 acc[NQS];
-    // ---- policy FC 450 -> 225 (+ bias) into ra, then softmax per board
-    heads_gemm_s<REC_X / 16, 15>(W + GF_P, lane, nt, ntn_p, acc, arow);
-    heads_put_s<false>(acc, W + GF_B, POS, nt, ntn_p, lane, ra, LG_STRIDE);
-    __syncthreads();
-    for (int bb = wave; bb < HBS && b0 + bb < count; bb += NWS) {
-        const float* l = ra + bb * LG_STRIDE;
-        float x[4];
-        float mx = -3.0e38f;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int o = lane + 64 * u;
-            x[u] = o < POS ? l[o] : -3.0e38f;
-            mx = fmaxf(mx, x[u]);
-        }
-        mx = wave_max(mx);
-        float e[4], sum = 0.f;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int o = lane + 64 * u;
-            e[u] = o < POS ? __expf(x[u] - mx) : 0.f;
-            sum += e[u];
-        }
-        sum = wave_sum(sum);
-        const size_t base = (size_t)(b0 + bb) * POS;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int o = lane + 64 * u;
-            if (o < POS) p_out[base + o] = e[u] / sum;
-        }
-    }
-    // ---- DQN fc0 (one-hot planes -> 256, all 29 k-blocks) + ReLU into rb
-    heads_gemm_s<(REC - REC_X) / 16, 16>(W + D0_P, lane, nt, NQS, acc, arow + REC_X);
-    heads_put_s<true>(acc, W + D0_BASE, DQH, nt, NQS, lane, rb, H_STRIDE);
-    __syncthreads();  // rb complete; ra (logits) no longer read
-    // ---- fc1 256 -> 256 + ReLU into ra
-    heads_gemm_s<DQH / 16, 16>(W + D1_P, lane, nt, NQS, acc, rb + li * H_STRIDE);
-    heads_put_s<true>(acc, W + D1_B, DQH, nt, NQS, lane, ra, H_STRIDE);
-    __syncthreads();
-    // ---- fc2 256 -> 225: q
-    heads_gemm_s<DQH / 16, 15>(W + D2_P, lane, nt, ntn_p, acc, ra + li * H_STRIDE);
-#pragma unroll
-    for (int q = 0; q < NQS; q++) {
-        if (q >= ntn_p) continue;
-        const int o = 16 * nt[q] + li;
-        if (o >= POS) continue;
-        const float bv = W[D2_B + o];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int b = b0 + 4 * g + r;
-            if (b < count) q_out[(size_t)b * POS + o] = acc[q][r] + bv;
-        }
-    }
-}
-
-// The heads split over output tiles, for the same small launches: three launches
+// The heads split over output tiles for them: three launches
 // (policy FC + DQN fc0; fc1; fc2 + the softmax), each workgroup 16 boards x 4 output
 // tiles (a wave per tile, the fragments 5 k-blocks ahead), the layers' outputs through
 // a scratch in global memory.  A launch of 512 rows then has 256 / 128 / 160
@@ -796,20 +666,14 @@ static void gn_heads_launch(const float* W, const float* rec, int max_rows, cons
         const char* e = getenv("GZ_GN_SMALL_HEADS");
         return e ? atoi(e) : -1;
     }();
-    static const int split = [] {  // GZ_GN_HEADS_SPLIT=0: one small-launch kernel instead (A/B)
-        const char* e = getenv("GZ_GN_HEADS_SPLIT");
-        return e ? atoi(e) : 1;
-    }();
     const int cap = small_cap >= 0 ? small_cap : 2 * HB * cus;
-    if (sc && !d_logits && max_rows < cap && split) {
+    if (sc && !d_logits && max_rows < cap) {
         const unsigned gx = (unsigned)((max_rows + HBS - 1) / HBS);
         float *lg = sc, *h0 = sc + (size_t)max_rows * HN_LD, *h1 = sc + 2 * (size_t)max_rows * HN_LD;
         gn_hn0_kernel<<<dim3(gx, 8), 256, 0, s>>>(W, rec, max_rows, d_count, lg, h0);
         gn_hn1_kernel<<<dim3(gx, 4), 256, 0, s>>>(W, max_rows, d_count, h0, h1);
         gn_hn2_kernel<<<dim3(gx, 5), 256, 0, s>>>(W, max_rows, d_count, lg, h1, d_p, d_q);
-    } else if (!d_logits && max_rows < cap)
-        gn_heads_small_kernel<<<(max_rows + HBS - 1) / HBS, NWS * 64, 0, s>>>(W, rec, max_rows, d_count, d_p, d_q);
-    else
+    } else
         gn_heads_kernel<<<(max_rows + HB - 1) / HB, NTH_H, 0, s>>>(W, rec, max_rows, d_count, d_p, d_q, d_logits);
 }
 

@@ -238,7 +238,7 @@ int gz_pv_tree_exec_tiles(const void* d_workspace, int32_t n, int32_t* d_out2, v
  * a launch of fewer than 64 boards per CU without logits runs them split over output
  * tiles instead (16 boards x 4 tiles per workgroup, three launches, p and q the same
  * bits), the layers' outputs through the workspace.  GZ_GN_SMALL_HEADS=<rows> moves
- * that threshold, GZ_GN_HEADS_SPLIT=0 runs a one-kernel variant instead (A/B knobs).
+ * that threshold (A/B knob).
  * d_workspace: gz_gn_workspace_bytes(n) bytes, required (per row a 3.6 KB net record,
  * then 3 KB of the split heads' scratch). */
 size_t gz_gn_weight_floats(void);

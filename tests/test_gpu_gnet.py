@@ -183,11 +183,12 @@ def test_incremental_graphnet_chains_bitwise(nets):
 
 @pytest.mark.parametrize("n", [1, 17, 700, 5000])
 def test_small_launch_heads_bitwise(nets, n):
-    """gn_heads_small_kernel (16 boards, 8 waves per workgroup, dense fc0: the planner's
-    small sequential-round launches) against gn_heads_kernel (32 boards, 4 waves, fc0
-    over the stone-holding k-blocks) on the same records: p and q bit for bit.  A
-    launch that asks for logits takes gn_heads_kernel; one that does not, below 2 x 32
-    boards per CU, the small kernel.  Sparse and empty boards included."""
+    """The heads split over output tiles (gn_hn0/1/2_kernel: 16 boards x 4 tiles per
+    workgroup, dense fc0 -- the planner's small sequential-round launches) against
+    gn_heads_kernel (32 boards, 4 waves, fc0 over the stone-holding k-blocks) on the same
+    records: p and q bit for bit.  A launch that asks for logits takes gn_heads_kernel;
+    one that does not, below 2 x 32 boards per CU, the split.  Sparse and empty boards
+    included."""
     import torch
     from gzero import device
     _, gsd, dsd, w = nets
