@@ -75,9 +75,11 @@ struct PlanJob {  // 128 bytes
 static_assert(sizeof(PlanJob) == 128, "job");
 
 struct Counters {
-    int32_t rows;     // GN rows collected this round
-    int32_t pending;  // games with a job after resume
+    int32_t rows;         // GN rows collected this round
     int32_t nfull, ninc;  // this planner step's full-forward / incremental rows
+    // games with a job after resume: only w.ctr's is used, cleared by the host right
+    // before plan_resume_kernel and never by the per-step resets of (rows, nfull, ninc)
+    int32_t pending;
     int32_t pad[60];
 };
 // never cleared by a search: gz_plan_gn_stats reads (and resets) them
@@ -885,7 +887,7 @@ __global__ __launch_bounds__(PW * WAVE) void plan_step4_kernel(Workspace w, gz_p
     __shared__ PlanShared4 sh;
     // the next planner step's counters (the other set: every kernel of the step that used
     // it is done) -- hipMemsetAsync's work, without a launch
-    if (blockIdx.x == 0 && threadIdx.x < 4) (&next->rows)[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 3) (&next->rows)[threadIdx.x] = 0;  // rows, nfull, ninc (not pending)
     plan_step_row<PW>(w, pp, count_rows, &sh);
 }
 
@@ -1259,8 +1261,9 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         wk.ctr = (step_no & 1) ? w.ctr2 : w.ctr;
         Counters* next = (step_no & 1) ? w.ctr : w.ctr2;
         step_no++;
-        // rows, pending (recomputed by the next resume), nfull, ninc
-        if (!zeroed && hipMemsetAsync(&wk.ctr->rows, 0, 16, s) != hipSuccess) return plan_fail(GZ_ERR_HIP, "memset");
+        // rows, nfull, ninc (pending is left alone: the resume's own memset clears it)
+        if (!zeroed && hipMemsetAsync(&wk.ctr->rows, 0, 3 * sizeof(int32_t), s) != hipSuccess)
+            return plan_fail(GZ_ERR_HIP, "memset");
         // jobs j0 .. j1-1 (round 0's chunk), or (slot_game) the one job per game at g * S
         const int cnt = slot_game ? n : j1 - j0, stride = slot_game ? S : 1;
         plan_collect_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(wk, S, n, j0, cnt, stride, p->planner_steps, 0,

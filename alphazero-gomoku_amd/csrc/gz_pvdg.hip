@@ -54,8 +54,18 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ uint4 gz_dg_zero16[1];  // zero source of the LDS-DMA fills
 
+#ifndef GZ_DG_N4
+#define GZ_DG_N4 0  // 1: 4 n-tiles per wave over half the tiles (dg_kloop4)
+#endif
+#ifndef GZ_DG_RING
+#define GZ_DG_RING 2  // dg_kloop4's weight ring, k-steps (2 or 3)
+#endif
+#ifndef GZ_DG_EST
+#define GZ_DG_EST 2  // dg_epilogue4's load stages
+#endif
+
 constexpr int NTD = 256;  // 4 waves
-constexpr int PATCH_HALVES = 164 * 256;
+constexpr int PATCH_HALVES = PV_PATCH_HALVES;
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // x0 r1, y1 r2, x1 r3, y2 r4 (halves)
 __host__ __device__ constexpr int dg_s(int L) { return 2 * L + 3; }  // D-square width (radius L+1)
 __host__ __device__ constexpr int dg_ss(int L) { return dg_s(L) * dg_s(L); }
@@ -82,6 +92,8 @@ struct K {
     __host__ __device__ static constexpr int npos(int L) { return dgk_npos(L); }
     static constexpr int MAXNPOS = 112;            // npos(2) = max over the layers (static_assert below)
     static constexpr int NMAX = 12;                // output tiles of a pass at most (y2: 2 x 81 rows in 11)
+    static constexpr int NTW = NMAX / 2;           // tiles of a wave (4-n-tile ownership)
+    static constexpr int HPW = GZ_DG_N4 ? 2 : 4;   // head partial slots per node (channel groups of the waves)
     static constexpr int ROWS = NMAX * 16;         // row-table entries per pass
     static constexpr int GB = 2;                   // epilogue: tiles per load group
     static constexpr int WPS = 2;                  // workgroups per CU
@@ -161,13 +173,30 @@ struct DgStamp {
 // global-memory accesses through the unit table's pointers as global (not flat)
 // instructions: flat ones count against lgkmcnt too and would hold the LDS waits
 #define GZ_GLB __attribute__((address_space(1)))
+#ifdef GZ_DG_CHK
+// debug builds (tools only): every global access of the kernel checked against the tree
+// workspace's bounds; an access outside is counted and redirected to the workspace start
+__device__ unsigned long long gz_dg_chk[8];
+__device__ const char* gz_dg_lo;
+__device__ const char* gz_dg_hi;
+__device__ __forceinline__ const void* dg_chk(const void* p, int code) {
+    if ((const char*)p < gz_dg_lo || (const char*)p >= gz_dg_hi) {
+        atomicAdd(&gz_dg_chk[code], 1ull);
+        return gz_dg_lo;
+    }
+    return p;
+}
+#define DG_CHK(p, code) dg_chk((p), (code))
+#else
+#define DG_CHK(p, code) (p)
+#endif
 template <class T>
 __device__ __forceinline__ T gld(const void* p) {
-    return *(const GZ_GLB T*)p;
+    return *(const GZ_GLB T*)DG_CHK(p, 0);
 }
 template <class T>
 __device__ __forceinline__ void gst(void* p, const T& v) {
-    *(GZ_GLB T*)p = v;
+    *(GZ_GLB T*)DG_CHK(p, 1) = v;
 }
 
 // ------------------------------------------------------------------ rows of a pass
@@ -436,6 +465,107 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
         for (int m = 0; m < NT; m++) acc[n][m] = c[n][m];
 }
 
+// ------------------------------------------------------------------ the k-loop, 4 n-tiles per wave
+// Wave (ng, mh) = (wave & 1, wave >> 1) owns the n-tiles 4 ng .. 4 ng + 3 over the pass's
+// tiles m = 2 j + mh: each activation fragment read from LDS feeds 12 MFMAs (4 n-tiles x
+// 3 products) instead of 6, halving the LDS reads of the 2-n-tile ownership; each weight
+// fragment is read by the two waves of an n-half.  One k-step per unit (12 MFMAs per tile
+// behind one tap-mask test); weights in a RING-deep ring of k-steps, refilled RING - 1
+// k-steps ahead (the tap loop unrolled so that a k-step's ring slot is static).
+template <int NT, int L, int RING>
+__device__ __forceinline__ void dg_kloop4(const char* lds, const uint32_t (&ri)[K::NTW], const uint32_t* mk,
+                                          const _Float16* __restrict__ Wf, int nt0, int mh, int lane,
+                                          f32x4 (&acc)[4][K::NTW]) {
+    static_assert(NT % 2 == 0 && NT <= K::NTW, "tile parity");
+    constexpr int S = dg_s(L), NPOS = K::npos(L), CQ = 4, KS = 9 * CQ;
+    constexpr int CQB = 4 * NPOS * 16, PLB = 16 * NPOS * 16, ZIDX = NPOS - 1;
+    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
+    constexpr int TU = RING == 3 ? 3 : 1;  // taps per loop iteration: TU * CQ k-steps, a multiple of RING
+    static_assert((TU * CQ) % RING == 0 && 9 % TU == 0, "ring");
+    const int lb = K::IN + (lane >> 4) * NPOS * 16;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+    const int wo = (nt0 * 64 + lane) * 16;
+    auto wload = [&](int ks, int n, int lo) -> h8 {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
+    };
+    auto addr = [&](int tap, uint32_t r) -> int {
+        const int toff = (tap / 3 - 1) * S + (tap - (tap / 3) * 3 - 1);
+        const bool v = (r >> (16 + tap)) & 1u;
+        return lb + (v ? (int)(r & 0xffffu) - 32 + toff : ZIDX) * 16;
+    };
+    h8 b[RING][4][2];
+#pragma unroll
+    for (int s = 0; s < RING - 1; s++)
+#pragma unroll
+        for (int n = 0; n < 4; n++) {
+            b[s][n][0] = wload(s, n, 0);
+            b[s][n][1] = wload(s, n, 1);
+        }
+    f32x4 c[4][NT];
+#pragma unroll
+    for (int n = 0; n < 4; n++)
+#pragma unroll
+        for (int m = 0; m < NT; m++) c[n][m] = acc[n][m];
+    int ad[NT];
+#pragma unroll
+    for (int m = 0; m < NT; m++) ad[m] = addr(0, ri[m]);
+    h8 fh[2], fl[2];  // [fragment parity]: NT even, so tile m's parity is m & 1 in every k-step
+    fh[0] = *(const h8*)(lds + ad[0]);
+    fl[0] = *(const h8*)(lds + ad[0] + PLB);
+#pragma unroll 1
+    for (int tap0 = 0; tap0 < 9; tap0 += TU) {
+#pragma unroll
+        for (int tu = 0; tu < TU; tu++) {
+            const int tap = tap0 + tu;
+            const uint32_t tm = (uint32_t)__builtin_amdgcn_readfirstlane((int)mk[tap]) >> mh;
+#pragma unroll
+            for (int k4 = 0; k4 < CQ; k4++) {
+                const int kl = tu * CQ + k4;  // k-step inside the iteration: its ring slot is kl % RING
+                {  // k-step + RING - 1 into the slot the previous k-step released (past the end: unused)
+                    const int ksr = tap * CQ + k4 + RING - 1;
+                    const int kn = ksr < KS ? ksr : ksr - KS;
+                    const int sr = (kl + RING - 1) % RING;
+#pragma unroll
+                    for (int n = 0; n < 4; n++) {
+                        b[sr][n][0] = wload(kn, n, 0);
+                        b[sr][n][1] = wload(kn, n, 1);
+                    }
+                }
+                const int sl = kl % RING;
+#pragma unroll
+                for (int m = 0; m < NT; m++) {
+                    const int pm = m & 1, pn = (m + 1) & 1;
+                    int na;
+                    if (m + 1 < NT) na = ad[m + 1] + k4 * CQB;
+                    else na = k4 + 1 < CQ ? ad[0] + (k4 + 1) * CQB : ad[0];
+#ifdef GZ_DG_CHK
+                    if (na < 0 || na + PLB + 16 > K::IN_BYTES) {
+                        atomicAdd(&gz_dg_chk[5], 1ull);
+                        na = 0;
+                    }
+#endif
+                    fh[pn] = *(const h8*)(lds + na);
+                    fl[pn] = *(const h8*)(lds + na + PLB);
+                    if (k4 == CQ - 1) ad[m] = addr(tap + 1, ri[m]);  // tile m's reads of this tap are issued
+                    if ((tm >> (2 * m)) & 1u) {
+                        const h8 ah = fh[pm], al = fl[pm];
+#pragma unroll
+                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah, c[n][m], 0, 0, 0);
+#pragma unroll
+                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah, c[n][m], 0, 0, 0);
+#pragma unroll
+                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al, c[n][m], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; n++)
+#pragma unroll
+        for (int m = 0; m < NT; m++) acc[n][m] = c[n][m];
+}
+
 // ------------------------------------------------------------------ epilogue
 struct H4x2 {
     h4 h, l;
@@ -582,13 +712,119 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
     }
 }
 
+// The same epilogue for the 4-n-tile ownership (dg_kloop4): the wave's tiles m = 2 j + mh
+// (ntw of them), its 64 channels; one tile per load group, loads ST - 1 tiles ahead.  x2:
+// the head partial sums of its 64 channels into hpart slot ng.
+template <int L, int ST>
+__device__ __forceinline__ void dg_epilogue4(char* lds, const DgUnit* U, const uint32_t* rt, int ng, int mh,
+                                             int lane, const f32x4 (&acc)[4][K::NTW], int ntw) {
+    constexpr int RO = L + 2, SO = dg_so(L), SSO = SO * SO;
+    constexpr bool SKIP = L == 1 || L == 3;
+    constexpr int RS = L == 1 ? 1 : 3, SK = 2 * RS + 1, SSK = SK * SK;
+    float* hpart = (float*)(lds + K::HP);
+    const int q = lane >> 4, li = lane & 15;
+    const float* cst = (const float*)(lds + K::CST);  // staged at kernel start
+    f32x4 es[4];
+#pragma unroll
+    for (int n = 0; n < 4; n++) es[n] = *(const f32x4*)(cst + L * 128 + (4 * ng + n) * 16 + 4 * q);
+    f32x4 z[ST][4];
+    H4x2 dk[ST][4];
+    uint32_t ent[ST];
+    auto loads = [&](int j, int st) {
+        uint32_t e = rt[(2 * j + mh) * 16 + li];
+#ifdef GZ_DG_CHK
+        if ((e & 15) >= (uint32_t)K::C) {
+            atomicAdd(&gz_dg_chk[6], 1ull);
+            e = 0;
+        }
+#endif
+        ent[st] = e;
+        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
+        const DgUnit& u = U[gi];
+        const int cell = u.cell, cr = cell / BN, cc = cell - (cell / BN) * BN;
+        const bool v = (e >> 21) & 1u;
+        const int pos = v ? (cr + dy) * BN + (cc + dx) : 0;
+        const bool near = SKIP && v && iabs(dy) <= RS && iabs(dx) <= RS;
+        const int sidx = near ? (dy + RS) * SK + (dx + RS) : 0;
+#pragma unroll
+        for (int n = 0; n < 4; n++) {
+            const int ch0 = (4 * ng + n) * 16 + 4 * q;
+            z[st][n] = gld<f32x4>(u.pre + L * PV_PRE_FLOATS + pos * CH + ch0);
+            if (SKIP) {
+                const _Float16* p = u.own + PATCH_OFF[L - 1] + ((ch0 >> 3) * SSK + sidx) * 8 + (ch0 & 7);
+                dk[st][n] = H4x2{gld<h4>(p), gld<h4>(p + 16 * SSK * 8)};
+            }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < ST - 1; j++)
+        if (j < ntw) loads(j, j);
+#pragma unroll
+    for (int j = 0; j < K::NTW; j++) {
+        if (j >= ntw) break;
+        const int st = j % ST;
+        if (j + ST - 1 < ntw) loads(j + ST - 1, (j + ST - 1) % ST);
+        const uint32_t e = ent[st];
+        const bool v = (e >> 21) & 1u;
+        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
+        const bool near = SKIP && iabs(dy) <= RS && iabs(dx) <= RS;
+        const int oidx = (dy + RO) * SO + (dx + RO);
+        float s0 = 0.f, s1 = 0.f, sv = 0.f;
+#pragma unroll
+        for (int n = 0; n < 4; n++) {
+            const int ch0 = (4 * ng + n) * 16 + 4 * q;
+            f32x4 y, d, h0, h1, hv;
+            if (L == 3) {
+                h0 = *(const f32x4*)(cst + 512 + ch0);
+                h1 = *(const f32x4*)(cst + 640 + ch0);
+                hv = *(const f32x4*)(cst + 768 + ch0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float zr = z[st][n][r];
+                float tc = __builtin_fmaf(acc[n][j][r], es[n][r], zr);
+                if (SKIP) tc += near ? h2f(dk[st][n], r) : 0.f;
+                tc = tc > 0.f ? tc : 0.f;
+                if (L == 3) {
+                    s0 = __builtin_fmaf(h0[r], tc, s0);
+                    s1 = __builtin_fmaf(h1[r], tc, s1);
+                    sv = __builtin_fmaf(hv[r], tc, sv);
+                } else {
+                    y[r] = tc;
+                    d[r] = tc - (zr > 0.f ? zr : 0.f);
+                }
+            }
+            if (L < 3 && v) {
+                const DgUnit& u = U[gi];
+                const int o = PATCH_OFF[L + 1] + ((ch0 >> 3) * SSO + oidx) * 8 + (ch0 & 7);
+                put_hl(u.own + o, 16 * SSO * 8, d);
+                if (u.patch) put_hl(u.patch + o, 16 * SSO * 8, y);
+            }
+        }
+        if (L == 3) {
+            s0 += __shfl_xor(s0, 16);
+            s1 += __shfl_xor(s1, 16);
+            sv += __shfl_xor(sv, 16);
+            s0 += __shfl_xor(s0, 32);
+            s1 += __shfl_xor(s1, 32);
+            sv += __shfl_xor(sv, 32);
+            if (lane < 16 && v) {
+                float* h = hpart + ((gi * 4 + ng) * 3) * 121 + oidx;
+                h[0] = s0;
+                h[121] = s1;
+                h[242] = sv;
+            }
+        }
+    }
+}
+
 // a node's head-conv record: the radius-5 square from the partials (bias + the 4
 // waves' sums), everything else the root's record (rec: this thread's entries of the
 // root's record, dg_record_load)
 constexpr int REC_K = (HSTRIDE + NTD - 1) / NTD;
 __device__ __forceinline__ void dg_record_load(const DgUnit& u, const float* __restrict__ hbuf, float (&rec)[REC_K],
                                                int tid) {
-    const float* src = hbuf + (size_t)u.base * HSTRIDE;
+    const float* src = (const float*)DG_CHK(hbuf + (size_t)u.base * HSTRIDE, 3);
 #pragma unroll
     for (int k = 0; k < REC_K; k++) {
         const int j = tid + k * NTD;
@@ -598,7 +834,7 @@ __device__ __forceinline__ void dg_record_load(const DgUnit& u, const float* __r
 __device__ __forceinline__ void dg_record(const DgUnit& u, int g, const float* bias, float* __restrict__ hbuf,
                                           const float* hpart, const float (&rec)[REC_K], int tid) {
     const int cr = u.cell / BN, cc = u.cell - (u.cell / BN) * BN;
-    float* h = hbuf + (size_t)u.leaf * HSTRIDE;
+    float* h = (float*)DG_CHK(hbuf + (size_t)u.leaf * HSTRIDE, 4);
 #pragma unroll
     for (int k = 0; k < REC_K; k++) {
         const int j = tid + k * NTD;
@@ -620,7 +856,7 @@ __device__ __forceinline__ void dg_record(const DgUnit& u, int g, const float* b
                 const int idx = (dy + 5) * 11 + (dx + 5);
                 float a = bias[which];
 #pragma unroll
-                for (int w = 0; w < 4; w++) a += hpart[((g * 4 + w) * 3 + which) * 121 + idx];
+                for (int w = 0; w < K::HPW; w++) a += hpart[((g * 4 + w) * 3 + which) * 121 + idx];
                 v = a;
             }
         }
@@ -652,7 +888,7 @@ __device__ __forceinline__ void dg_fill(char* lds, const DgUnit* U, int g, int t
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const int pc = wave * 8 + k;
-                __builtin_amdgcn_global_load_lds((glb_void_t*)(src + pc * stride), (lds_void_t*)(dst + pc * NPOS * 16),
+                __builtin_amdgcn_global_load_lds((glb_void_t*)DG_CHK(src + pc * stride, 2), (lds_void_t*)(dst + pc * NPOS * 16),
                                                  16, 0, 0);
             }
         }
@@ -786,6 +1022,35 @@ __device__ __forceinline__ void dg_pass(const char* lds, const uint32_t* rt, con
         dg_kloop<K::NMAX, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
 }
 
+// the same for the 4-n-tile ownership: the wave's tiles m = 2 j + mh
+template <int L>
+__device__ __forceinline__ void dg_pass4(const char* lds, const uint32_t* rt, const uint32_t* mk,
+                                         const float* __restrict__ W, int ng, int mh, int lane,
+                                         f32x4 (&acc)[4][K::NTW], int nt) {
+    constexpr int RIN = L + 1, RO = L + 2, S = dg_s(L), SS = dg_ss(L);
+    const int li = lane & 15;
+    uint32_t ri[K::NTW];
+#pragma unroll
+    for (int j = 0; j < K::NTW; j++) {
+        const uint32_t e = rt[(2 * j + mh) * 16 + li];
+        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
+        const int base = gi * SS + (dy + RIN) * S + (dx + RIN) + 32;
+        ri[j] = (e >> 21) & 1u ? ((uint32_t)base & 0xffffu) | (((e >> 12) & 0x1ffu) << 16) : 0u;
+    }
+#pragma unroll
+    for (int n = 0; n < 4; n++)
+#pragma unroll
+        for (int j = 0; j < K::NTW; j++) acc[n][j] = zero4();
+    const _Float16* Wf = (const _Float16*)(W + F16_RES0 + L * F16_STRIDE);
+    // tiles per wave rounded up to even (both waves of an n-half run the same instantiation)
+    if (nt <= 4)
+        dg_kloop4<2, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
+    else if (nt <= 8)
+        dg_kloop4<4, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
+    else
+        dg_kloop4<K::NTW, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
+}
+
 // pass p of a chunk of ng nodes: its layer L, first node u0 and node count g (0: empty)
 __device__ __forceinline__ void dg_pass_of(int p, int ng, int& L, int& u0, int& g) {
     L = p >= K::pb(3) ? 3 : (p >= K::pb(2) ? 2 : (p >= K::pb(1) ? 1 : 0));
@@ -882,11 +1147,20 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             const float* Wp = W;
             int t = tid;
             asm volatile("" : "+s"(Wp), "+v"(t));
+#if GZ_DG_N4
+            const int ng = wave & 1, mh = wave >> 1, ntw = (nt - mh + 1) >> 1;
+            f32x4 acc[4][K::NTW];
+            if (L == 0) dg_pass4<0>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
+            else if (L == 1) dg_pass4<1>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
+            else if (L == 2) dg_pass4<2>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
+            else dg_pass4<3>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
+#else
             f32x4 acc[2][K::NMAX];
             if (L == 0) dg_pass<0>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else if (L == 1) dg_pass<1>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else if (L == 2) dg_pass<2>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else dg_pass<3>(lds, rt, mk, Wp, np, t & 63, acc, nt);
+#endif
             st(2 + L);
             __syncthreads();  // every wave is past the k-loop: the image is free
             st(6);
@@ -898,10 +1172,17 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
                 if (g2 > 0) break;
             }
             const bool more = q < K::NPASS;
+#if GZ_DG_N4
+            if (L == 0) dg_epilogue4<0, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
+            else if (L == 1) dg_epilogue4<1, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
+            else if (L == 2) dg_epilogue4<2, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
+            else dg_epilogue4<3, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
+#else
             if (L == 0) dg_epilogue<0>(lds, U + u0, rt, np, t & 63, acc, nt);
             else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, np, t & 63, acc, nt);
             else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, np, t & 63, acc, nt);
             else dg_epilogue<3>(lds, U + u0, rt, np, t & 63, acc, nt);
+#endif
             st(7 + L);
             // vmcnt counts loads, stores and LDS-DMA together in issue order, so each wait
             // below also waits for every older store.  The next pass's fill reads, by
@@ -949,13 +1230,21 @@ extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_
                                       int32_t* d_tiles, const int32_t* d_children, const int32_t* d_nchildren,
                                       int grid, void* stream) {
     DgArgs A{d_cinfo, d_weights, d_boards, d_meta, d_pslot, d_maps, d_pres, d_patches, d_hbuf, d_tiles};
-    // K::WPS workgroups per CU; the scratch holds 12 patches per CU = K::C per workgroup
-    static_assert(K::C * K::WPS <= 12, "scratch");
+    // K::WPS workgroups per grid entry (CU), K::C patch-sized scratch areas each
+    static_assert(K::C * K::WPS <= PV_SCRATCH_PATCHES, "scratch");
 #ifdef GZ_PVDG_STAMPS
     // stamp builds: GZ_PVDG_WPS=1 runs one workgroup per CU (the k-loop without a co-resident one)
     static const int wps = std::getenv("GZ_PVDG_WPS") && std::getenv("GZ_PVDG_WPS")[0] == '1' ? 1 : K::WPS;
 #else
     constexpr int wps = K::WPS;
+#endif
+#ifdef GZ_DG_CHK
+    {
+        const char* lo = (const char*)d_hbuf;
+        const char* hi = (const char*)(d_scratch + (size_t)grid * PV_SCRATCH_PATCHES * PATCH_HALVES);
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(gz_dg_lo), &lo, sizeof(lo), 0, hipMemcpyHostToDevice, (hipStream_t)stream);
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(gz_dg_hi), &hi, sizeof(hi), 0, hipMemcpyHostToDevice, (hipStream_t)stream);
+    }
 #endif
     pv_dg_kernel<<<grid * wps, NTD, 0, (hipStream_t)stream>>>(A, d_scratch, d_children, d_nchildren);
     hipError_t e = hipGetLastError();
@@ -978,5 +1267,13 @@ extern "C" int gz_pvdg_stamps_read(unsigned long long* out, int reset) {
         if (hipMemcpyToSymbol(HIP_SYMBOL(gz_pvdg_stamps_n), z, sizeof(z[0])) != hipSuccess) return -1;
     }
     return 0;
+}
+#endif
+
+#ifdef GZ_DG_CHK
+// out-of-workspace global accesses per code (loads, stores, fills, record reads, record writes)
+extern "C" int gz_pvdg_chk_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_dg_chk), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -107,7 +107,7 @@ __device__ inline int bit_of_board(int r, int c) { return r * 16 + c; }
 // A parent's patch for its grandchildren: the recomputed squares of its maps
 // (x0 r1, y1 r2, x1 r3, y2 r4), [plane][16 cg][(2r+1)^2][8] each, in that order
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // halves
-constexpr int PATCH_HALVES = 164 * 256;
+constexpr int PATCH_HALVES = PV_PATCH_HALVES;
 
 
 struct TreeArgs {
@@ -148,6 +148,7 @@ struct TreeArgs {
 constexpr int NTS = 256, SIB_MH = 1;  // 4 waves; SIB_MH: M halves per n-tile pair
 constexpr int sib_tiles(int t) { return t; }
 constexpr int SIB_G = 6;
+static_assert(SIB_G <= PV_SCRATCH_PATCHES, "tree scratch: one workgroup per grid entry");
 constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
 static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
 constexpr int SIB_HP = SIB_WIN;                     // head partials [4 pairs][3][HP_ROWS]

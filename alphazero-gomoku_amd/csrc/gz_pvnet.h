@@ -59,6 +59,13 @@ constexpr int PV_MAP_HALVES = 2 * PV_MAP_PLANE;
 // of the 4 residual layers (y1, x1, y2, x2: z = BN(conv) [+ skip input]), fp32
 // position-major [256 positions][128 channels] -- PV_PRE_FLOATS floats per layer
 constexpr int PV_PRE_FLOATS = 256 * CH;
+// a root child's recomputed squares / D squares (x0 r1, y1 r2, x1 r3, y2 r4: 164
+// positions x 256 halves), the unit of the patch slots and of the tree scratch
+constexpr int PV_PATCH_HALVES = 164 * 256;
+// tree scratch per grid entry (one per CU): PV_SCRATCH_PATCHES patch-sized areas,
+// shared by the workgroups of pv_sib_kernel / pv_dg_kernel on that entry (each kernel
+// static_asserts its workgroups x nodes per chunk against it)
+constexpr int PV_SCRATCH_PATCHES = 12;
 // per-board record of the 1x1 head convs' outputs between the tower and the FC heads
 // (gz_pvnet.hip / gz_pvinc.hip -> pv_heads_kernel): hp [0, 450) channel-major, zero to
 // HP_K; hv [HV_OFF, HV_OFF + 225), zero to HSTRIDE

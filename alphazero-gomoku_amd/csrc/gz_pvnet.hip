@@ -974,8 +974,8 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-constexpr int PV_PATCH_HALVES = 164 * 256;  // a root child's recomputed squares (gz_pvinc.hip)
-constexpr size_t SIB_SCRATCH_HALVES = 12 * (size_t)PV_PATCH_HALVES;  // per workgroup: pv_sib_kernel 6, pv_dg_kernel 12
+// per grid entry (gz_pvnet.h): pv_sib_kernel's workgroup x 6 nodes, pv_dg_kernel's 2 x 6
+constexpr size_t SIB_SCRATCH_HALVES = PV_SCRATCH_PATCHES * (size_t)PV_PATCH_HALVES;
 inline int32_t patch_cap_of(int32_t root_cap) { return 16 * (root_cap < 0 ? 0 : root_cap); }
 struct TreeWs {
     float* hbuf;

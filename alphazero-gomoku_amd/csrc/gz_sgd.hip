@@ -1000,8 +1000,11 @@ __global__ __launch_bounds__(64) void sgd_fc_loss_kernel(gz_sgd_fc fc, const int
     for (int i = lane; i < FC_P_OUT; i += 64) e += expf(sb[i] - m);
     e = fc_wave_sum(e);
     const int64_t yt = y[b];
-    const int t = yt >= 0 && yt < FC_P_OUT ? (int)yt : 0;  // (labels are checked by the caller)
-    const float ce = m + logf(e) - sb[t], g = scale / (float)B;
+    // a label outside [0, 225) (torch's CrossEntropyLoss raises) poisons the loss and every
+    // gradient of the step with NaN instead of training on a substituted class
+    const bool bad = !(yt >= 0 && yt < FC_P_OUT);
+    const int t = bad ? 0 : (int)yt;
+    const float ce = m + logf(e) - sb[t], g = bad ? NAN : scale / (float)B;
     // value: h = relu(pre1), val = tanh(w2 . h + b2)
     const float pre1 = sb[FC_P_OUT + lane], h = fmaxf(pre1, 0.f);
     const float val = tanhf(fc_wave_sum(fc.value2_weight[lane] * h) + fc.value2_bias[0]), diff = val - v[b];

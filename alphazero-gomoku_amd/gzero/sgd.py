@@ -252,4 +252,6 @@ class NetStep:
                                            _ptr(self.loss), _ptr(fws), s), "gz_sgd_fc_loss")
         _lib.check(self.lib.gz_sgd_backward(ctypes.byref(self.st), B, _ptr(xc), _ptr(dpin), _ptr(dvin),
                                             ctypes.byref(self.gr), _ptr(ws), s), "gz_sgd_backward")
-        return self.loss[0]
+        # a copy: the loss buffer is overwritten by the next step (a label outside
+        # [0, 225) makes it NaN, and every gradient with it)
+        return self.loss[0].clone()

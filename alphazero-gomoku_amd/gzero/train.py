@@ -338,7 +338,11 @@ class DeviceTrainer:
         ``kernel`` (default: the native trainer): the eval-mode forward is the inference
         kernel (gz_pv_forward, f16x3; logits within 3e-7 of fp32) on the
         samples' board rows, with the weights packed on the device from the current
-        parameters and running statistics -- not the training graph's torch convolutions."""
+        parameters and running statistics -- not the training graph's torch convolutions.
+        This is a deliberate numeric difference from the reference, whose validation loss
+        (and so training.main's improvement / early-stop decision) comes from the fp32
+        eval-mode torch forward: the two agree within 1e-5 (checked every epoch in
+        tests/test_gpu_train.py); kernel=False evaluates with the torch forward."""
         self.net.eval()
         kernel = self.native if kernel is None else bool(kernel)
         pvw = None

@@ -439,6 +439,9 @@ def stub_main(args):
     bracketed by barriers, max over ranks, rank 0's JSON line."""
     rank, ws = gdist.init_from_env(backend=os.environ.get("GZ_DIST_BACKEND", "gloo"))
     info = distributed_info(ws, stub=True)
+    if rank == args.stub_fail_rank:  # (tests: a rank that dies after the rendezvous fails the whole run)
+        log(f"rank {rank}: failing on purpose (--stub-fail-rank)")
+        sys.exit(3)
     x = torch.ones(1024)
 
     def step():
@@ -574,6 +577,7 @@ def main():
                     help="N = 1 secondary: the exact-fp32 PV forward timed over this many steps (0 = skip)")
     ap.add_argument("--stub", action="store_true",
                     help="multi-rank plumbing only (rendezvous, device report, timing, JSON line) without a GPU")
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # CPU test: a failing rank
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -670,10 +674,17 @@ def main():
                                    "plies 0-5 that _opening_move plays without one (ai_agent.py:138-166)"},
             "distributed": dinfo,
         }
-    if ex is not None and rank == 0:
-        out["record_exchange"] = {"chunk_records": ex.chunk, "bytes_per_rank_per_step": ex.chunk * ex.item,
-                                  "pending_after": int(ex.pending().item()), "overflow": int(ex.overflow.item()),
-                                  "note": "fixed-size RCCL all_gather_into_tensor per step, counts on the device"}
+    if ex is not None:  # every rank's leftover / lost records (a collective: all ranks take part)
+        mine = torch.stack([ex.pending().reshape(()).to(torch.int64), ex.overflow.reshape(()).to(torch.int64)])
+        every = torch.zeros(ws * 2, dtype=torch.int64, device=mine.device)
+        dist.all_gather_into_tensor(every, mine)
+        every = every.view(ws, 2).cpu().tolist()
+        if rank == 0:
+            out["record_exchange"] = {
+                "chunk_records": ex.chunk, "bytes_per_rank_per_step": ex.chunk * ex.item,
+                "pending_after": [p for p, _ in every], "overflow": [o for _, o in every],
+                "note": "per rank (index = rank): records still queued after the window and records lost to "
+                        "a full outbox; fixed-size RCCL all_gather_into_tensor per step, counts on the device"}
     boards0, gids0 = m["boards0"], m["gids0"]
     del eng
 

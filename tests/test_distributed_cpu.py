@@ -286,6 +286,22 @@ def test_bench_self_launches_n_ranks_stub():
     assert [x["rank"] for x in d["ranks"]] == [0, 1] and [x["local_rank"] for x in d["ranks"]] == [0, 1]
 
 
+def test_bench_self_launch_fails_when_a_rank_fails():
+    """A rank that exits non-zero after the rendezvous makes the self-launched
+    `bench.py --gpus 2` exit non-zero and print no JSON line (the driver must never
+    read a partial run as a result)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GZ_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--stub", "--steps", "3",
+                        "--warmup", "1", "--stub-fail-rank", "1"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode != 0, (r.returncode, r.stderr[-2000:])
+    assert not [s for s in r.stdout.splitlines() if s.startswith("{")], r.stdout
+
+
 def _loss_worker(rank, ws, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

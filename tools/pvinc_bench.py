@@ -83,6 +83,13 @@ def main():
                  "y2 barrier + next fill", "y2 epilogue", "x2 k-loop", "x2 barrier + next fill",
                  "x2 epilogue + heads", "record"]
     run = tree
+    if hasattr(lib, "gz_pvdg_chk_read"):  # -DGZ_DG_CHK build: global accesses outside the workspace
+        import ctypes
+        lib.gz_pvdg_chk_read.argtypes = [ctypes.c_void_p]
+        chk = np.zeros(8, np.uint64)
+        tree()
+        lib.gz_pvdg_chk_read(chk.ctypes.data)
+        print("pv_dg_kernel out-of-workspace accesses (load, store, fill, record r/w):", chk[:5].tolist(), flush=True)
     timed(run, "tree")
     torch.cuda.synchronize()
     out = [t[: n * k].clone() for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225),
