@@ -13,18 +13,18 @@
 // a full forward (tests/test_gpu_pvdelta.py: 2e-5 of the full forward, 1e-4 of the
 // reference), not bitwise.
 //
-// Schedule: a workgroup (4 waves, one per SIMD, the whole LDS) takes a chunk of 12
-// consecutive root children and runs the tower layer-major: y1 over all 12 nodes, x1 in
-// passes of 6, y2 of 4, x2 + the 1x1 heads of 3 -- 10 passes per 12 nodes, each pass one
-// stream of a layer's 576 KB of hi/lo weight fragments for 200-360 output rows
-// (480 KB of weights per node; pv_sib_kernel streamed 1.15 MB).
+// Schedule (K below): two workgroups per CU, each (4 waves, one per SIMD) taking chunks
+// of 6 consecutive root children (a root's children are adjacent in the list): y1 over
+// the 6 nodes, x1 over 3 + 3, then per node pair y2 over the pair and x2 + the 1x1 heads
+// over each node -- 12 passes per 6 nodes, each pass one stream of a layer's 576 KB of
+// hi/lo weight fragments for up to 12 16-row tiles.
 //
 // Gather with tap skipping: a pass's output rows (every on-board position of each
 // node's radius-(L+2) square) are MFMA M rows; row p needs tap t only if p + t lies in
 // the D square (and on the board) -- a set TY x TX.  The rows are counting-sorted by
 // that class, so a 16-row tile's tap set (the union of its rows') is small, and a
-// tile runs only its taps: 86 tile-taps per node in the simulation of real chunks,
-// against 122 for the exact recomputation of the squares (pv_sib_kernel) -- the delta
+// tile runs only its taps: 102 tile-taps per node on real searches (92 for the
+// unclipped ideal), against 124 for the exact recomputation of the squares -- the delta
 // form's saving without pv_delta_kernel's scatter (an LDS read-add-write of the
 // accumulators per tap).  Accumulators stay in registers for the whole pass; the D
 // squares of the pass's nodes sit in LDS ([plane][16 cg][position][8], a node's square
@@ -33,8 +33,10 @@
 //
 // Between layers each node's D squares (x0 r1, y1 r2, x1 r3, y2 r4: the patch layout)
 // go to the workgroup's scratch in global memory and come back by LDS-DMA for the
-// passes that read them; a node with grandchildren also writes its CHILD values into
-// its patch slot for pv_sib_kernel<true> (gz_pvinc.hip).
+// passes that read them -- except where the next pass is the next layer of the same
+// first nodes (y1 -> x1 of nodes 0-2, y2 -> x2 of node 2k): those squares go from the
+// epilogue straight into the next pass's LDS image.  A node with grandchildren also
+// writes its CHILD values into its patch slot for pv_sib_kernel<true> (gz_pvinc.hip).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -54,16 +56,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ uint4 gz_dg_zero16[1];  // zero source of the LDS-DMA fills
 
-#ifndef GZ_DG_N4
-#define GZ_DG_N4 0  // 1: 4 n-tiles per wave over half the tiles (dg_kloop4)
-#endif
-#ifndef GZ_DG_RING
-#define GZ_DG_RING 2  // dg_kloop4's weight ring, k-steps (2 or 3)
-#endif
-#ifndef GZ_DG_EST
-#define GZ_DG_EST 2  // dg_epilogue4's load stages
-#endif
-
 constexpr int NTD = 256;  // 4 waves
 constexpr int PATCH_HALVES = PV_PATCH_HALVES;
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // x0 r1, y1 r2, x1 r3, y2 r4 (halves)
@@ -82,18 +74,18 @@ __host__ __device__ constexpr int dgk_npos(int L) { return (dgk_g(L) * dg_ss(L) 
 struct K {
     static constexpr int C = 6;  // nodes per chunk
     __host__ __device__ static constexpr int g(int L) { return dgk_g(L); }
-    // first pass of layer L in a full chunk; NPASS passes in all
-    __host__ __device__ static constexpr int pb(int L) {
-        return L == 0 ? 0 : (L == 1 ? 1 : (L == 2 ? 1 + C / 3 : 1 + C / 3 + C / 2));
-    }
     static constexpr int NPASS = 1 + C / 3 + C / 2 + C;
+    // the pass of layer L that takes node gi: y1, x1 x 2, then per node pair k: y2(2k, 2k+1),
+    // x2(2k), x2(2k+1) -- so that node 2k's D(y2) goes from the y2 epilogue straight into
+    // the x2 pass's LDS image (layer-major y2 x 3, x2 x 6: 1.8 % slower, profiles/r06/ab.md)
+    __host__ __device__ static constexpr int pass_of(int L, int gi) {
+        return L == 0 ? 0 : (L == 1 ? 1 + gi / 3 : (L == 2 ? 3 + 3 * (gi / 2) : 4 + 3 * (gi / 2) + (gi & 1)));
+    }
     // positions of a pass's LDS image: the nodes' squares back to back, then at least one
     // zero slot (the last), rounded to 16 so that a channel group's plane starts at bank 0
     __host__ __device__ static constexpr int npos(int L) { return dgk_npos(L); }
     static constexpr int MAXNPOS = 112;            // npos(2) = max over the layers (static_assert below)
     static constexpr int NMAX = 12;                // output tiles of a pass at most (y2: 2 x 81 rows in 11)
-    static constexpr int NTW = NMAX / 2;           // tiles of a wave (4-n-tile ownership)
-    static constexpr int HPW = GZ_DG_N4 ? 2 : 4;   // head partial slots per node (channel groups of the waves)
     static constexpr int ROWS = NMAX * 16;         // row-table entries per pass
     static constexpr int GB = 2;                   // epilogue: tiles per load group
     static constexpr int WPS = 2;                  // workgroups per CU
@@ -119,6 +111,7 @@ static_assert(K::COL + K::C * 1024 <= K::IN_BYTES, "im2col behind the y1 image")
 static_assert(dgk_g(0) * dg_so(0) * dg_so(0) <= K::ROWS && dgk_g(1) * dg_so(1) * dg_so(1) <= K::ROWS &&
                   dgk_g(2) * dg_so(2) * dg_so(2) <= K::ROWS && dgk_g(3) * dg_so(3) * dg_so(3) <= K::ROWS, "rows");
 static_assert(K::C % 6 == 0 && dgk_g(3) == 1, "passes; one x2 node per pass (the record prefetch)");
+static_assert(K::C == 6 && dgk_g(1) == 3 && dgk_g(2) == 2, "pass order (K::pass_of, dg_pass_of): 2 x1 triples, 3 y2 pairs");
 
 struct DgUnit {
     const _Float16* gm;  // the root's maps x0, y1, x1, y2 (hi / lo)
@@ -176,7 +169,7 @@ struct DgStamp {
 #ifdef GZ_DG_CHK
 // debug builds (tools only): every global access of the kernel checked against the tree
 // workspace's bounds; an access outside is counted and redirected to the workspace start
-__device__ unsigned long long gz_dg_chk[8];
+__device__ unsigned long long gz_dg_chk[16];
 __device__ const char* gz_dg_lo;
 __device__ const char* gz_dg_hi;
 __device__ __forceinline__ const void* dg_chk(const void* p, int code) {
@@ -206,64 +199,6 @@ __device__ __forceinline__ void gst(void* p, const T& v) {
 // {-1,0}, {-1}, {0,1}, {0}, {1}: neighbouring classes share taps
 __device__ __forceinline__ int set_rank(int b) {
     return b == 7 ? 0 : (b == 3 ? 1 : (b == 1 ? 2 : (b == 6 ? 3 : (b == 2 ? 4 : 5))));
-}
-
-// Bank spreading inside the class buckets.  A tile's fragment read (ds_read_b128) is
-// conflict-free when its 16 rows' image slots are distinct mod 16 (16-B bank groups; the
-// 4 channel-group planes start at bank 0 and the lane groups mix rows of two planes), for
-// every tap at once, since a tap adds the same offset to every row's slot.  The counting
-// sort leaves a bucket in atomic order, so its 16-row windows repeat residues (a square
-// row of w interior positions is followed by the next one S = w + 2 slots on: 2-way
-// conflicts on every few rows).  Here each bucket of more than 16 rows is reordered by
-// (occurrence of the residue, residue): every 16-row window inside a level then holds
-// distinct residues.  One wave per pass; the order inside a bucket changes no tile's taps.
-__device__ __forceinline__ void dg_rows_spread(uint32_t* rt0, const uint32_t* starts, const uint32_t* mk0, int tid) {
-    const int w = tid >> 6, ln = tid & 63;
-    const uint64_t lt = (ln == 0) ? 0ull : (~0ull >> (64 - ln));
-    for (int p = w; p < K::NPASS; p += NTD / 64) {
-        const int L = p >= K::pb(3) ? 3 : (p >= K::pb(2) ? 2 : (p >= K::pb(1) ? 1 : 0));
-        const int S = dg_s(L), SS = dg_ss(L);
-        const int total = (int)mk0[p * 16 + 9];
-        uint32_t* rt = rt0 + p * K::ROWS;
-        for (int k = 0; k < K::NKEY; k++) {
-            const int b0 = (int)starts[p * K::NKEY + k];
-            const int b1 = k + 1 < K::NKEY ? (int)starts[p * K::NKEY + k + 1] : total;
-            if (b1 - b0 <= 16) continue;  // wave-uniform
-            constexpr int RND = (K::ROWS + 63) / 64;
-            uint32_t e[RND];
-            int r[RND], j[RND];
-#pragma unroll
-            for (int q = 0; q < RND; q++) {
-                const int idx = b0 + q * 64 + ln;
-                e[q] = idx < b1 ? rt[idx] : 0u;
-                const int base = (int)(e[q] & 15u) * SS + ((int)((e[q] >> 4) & 15u) - 1) * S + ((int)((e[q] >> 8) & 15u) - 1);
-                r[q] = idx < b1 ? ((base + 32) & 15) : -1;
-                j[q] = 0;
-            }
-            int cnt = 0;  // lane v < 16: the bucket's rows with residue v
-#pragma unroll
-            for (int v = 0; v < 16; v++) {
-                int acc = 0;
-#pragma unroll
-                for (int q = 0; q < RND; q++) {
-                    const uint64_t m = __ballot(r[q] == v);
-                    if (r[q] == v) j[q] = acc + __popcll(m & lt);
-                    acc += __popcll(m);
-                }
-                if (ln == v) cnt = acc;
-            }
-#pragma unroll
-            for (int q = 0; q < RND; q++) {
-                int pos = 0;
-#pragma unroll
-                for (int v = 0; v < 16; v++) {
-                    const int c = __shfl(cnt, v);
-                    pos += (c < j[q] ? c : j[q]) + (v < r[q] && c > j[q] ? 1 : 0);
-                }
-                if (r[q] >= 0) rt[b0 + pos] = e[q];
-            }
-        }
-    }
 }
 
 // The row tables of every pass of the chunk (nodes U[0, ng)), counting-sorted by class,
@@ -307,7 +242,7 @@ __device__ __forceinline__ void dg_rows_all(char* lds, const DgUnit* U, int ng, 
         for (int a = 0; a < 3; a++)
             if ((ty >> a) & 1) m |= (uint32_t)tx << (3 * a);
         const int gl = L == 0 ? 0 : (L == 1 ? 3 : (L == 2 ? 2 : 1));  // nodes per pass of layer L (g(L))
-        const int p = K::pb(L) + (L == 0 ? 0 : gi / gl), u0 = L == 0 ? 0 : (gi / gl) * gl;
+        const int p = K::pass_of(L, gi), u0 = L == 0 ? 0 : (gi / gl) * gl;
         kk[i] = p * K::NKEY + set_rank(ty) * 6 + set_rank(tx);
         ent[i] = (uint32_t)(gi - u0) | ((uint32_t)(dy + RO) << 4) | ((uint32_t)(dx + RO) << 8) | (m << 12) | (1u << 21);
         rank[i] = (int)atomicAdd(&hist[kk[i]], 1u);
@@ -465,107 +400,6 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
         for (int m = 0; m < NT; m++) acc[n][m] = c[n][m];
 }
 
-// ------------------------------------------------------------------ the k-loop, 4 n-tiles per wave
-// Wave (ng, mh) = (wave & 1, wave >> 1) owns the n-tiles 4 ng .. 4 ng + 3 over the pass's
-// tiles m = 2 j + mh: each activation fragment read from LDS feeds 12 MFMAs (4 n-tiles x
-// 3 products) instead of 6, halving the LDS reads of the 2-n-tile ownership; each weight
-// fragment is read by the two waves of an n-half.  One k-step per unit (12 MFMAs per tile
-// behind one tap-mask test); weights in a RING-deep ring of k-steps, refilled RING - 1
-// k-steps ahead (the tap loop unrolled so that a k-step's ring slot is static).
-template <int NT, int L, int RING>
-__device__ __forceinline__ void dg_kloop4(const char* lds, const uint32_t (&ri)[K::NTW], const uint32_t* mk,
-                                          const _Float16* __restrict__ Wf, int nt0, int mh, int lane,
-                                          f32x4 (&acc)[4][K::NTW]) {
-    static_assert(NT % 2 == 0 && NT <= K::NTW, "tile parity");
-    constexpr int S = dg_s(L), NPOS = K::npos(L), CQ = 4, KS = 9 * CQ;
-    constexpr int CQB = 4 * NPOS * 16, PLB = 16 * NPOS * 16, ZIDX = NPOS - 1;
-    constexpr int KS_BYTES = 8 * 64 * 8 * 2, LO_BYTES = KS * KS_BYTES;
-    constexpr int TU = RING == 3 ? 3 : 1;  // taps per loop iteration: TU * CQ k-steps, a multiple of RING
-    static_assert((TU * CQ) % RING == 0 && 9 % TU == 0, "ring");
-    const int lb = K::IN + (lane >> 4) * NPOS * 16;
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
-    const int wo = (nt0 * 64 + lane) * 16;
-    auto wload = [&](int ks, int n, int lo) -> h8 {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
-    };
-    auto addr = [&](int tap, uint32_t r) -> int {
-        const int toff = (tap / 3 - 1) * S + (tap - (tap / 3) * 3 - 1);
-        const bool v = (r >> (16 + tap)) & 1u;
-        return lb + (v ? (int)(r & 0xffffu) - 32 + toff : ZIDX) * 16;
-    };
-    h8 b[RING][4][2];
-#pragma unroll
-    for (int s = 0; s < RING - 1; s++)
-#pragma unroll
-        for (int n = 0; n < 4; n++) {
-            b[s][n][0] = wload(s, n, 0);
-            b[s][n][1] = wload(s, n, 1);
-        }
-    f32x4 c[4][NT];
-#pragma unroll
-    for (int n = 0; n < 4; n++)
-#pragma unroll
-        for (int m = 0; m < NT; m++) c[n][m] = acc[n][m];
-    int ad[NT];
-#pragma unroll
-    for (int m = 0; m < NT; m++) ad[m] = addr(0, ri[m]);
-    h8 fh[2], fl[2];  // [fragment parity]: NT even, so tile m's parity is m & 1 in every k-step
-    fh[0] = *(const h8*)(lds + ad[0]);
-    fl[0] = *(const h8*)(lds + ad[0] + PLB);
-#pragma unroll 1
-    for (int tap0 = 0; tap0 < 9; tap0 += TU) {
-#pragma unroll
-        for (int tu = 0; tu < TU; tu++) {
-            const int tap = tap0 + tu;
-            const uint32_t tm = (uint32_t)__builtin_amdgcn_readfirstlane((int)mk[tap]) >> mh;
-#pragma unroll
-            for (int k4 = 0; k4 < CQ; k4++) {
-                const int kl = tu * CQ + k4;  // k-step inside the iteration: its ring slot is kl % RING
-                {  // k-step + RING - 1 into the slot the previous k-step released (past the end: unused)
-                    const int ksr = tap * CQ + k4 + RING - 1;
-                    const int kn = ksr < KS ? ksr : ksr - KS;
-                    const int sr = (kl + RING - 1) % RING;
-#pragma unroll
-                    for (int n = 0; n < 4; n++) {
-                        b[sr][n][0] = wload(kn, n, 0);
-                        b[sr][n][1] = wload(kn, n, 1);
-                    }
-                }
-                const int sl = kl % RING;
-#pragma unroll
-                for (int m = 0; m < NT; m++) {
-                    const int pm = m & 1, pn = (m + 1) & 1;
-                    int na;
-                    if (m + 1 < NT) na = ad[m + 1] + k4 * CQB;
-                    else na = k4 + 1 < CQ ? ad[0] + (k4 + 1) * CQB : ad[0];
-#ifdef GZ_DG_CHK
-                    if (na < 0 || na + PLB + 16 > K::IN_BYTES) {
-                        atomicAdd(&gz_dg_chk[5], 1ull);
-                        na = 0;
-                    }
-#endif
-                    fh[pn] = *(const h8*)(lds + na);
-                    fl[pn] = *(const h8*)(lds + na + PLB);
-                    if (k4 == CQ - 1) ad[m] = addr(tap + 1, ri[m]);  // tile m's reads of this tap are issued
-                    if ((tm >> (2 * m)) & 1u) {
-                        const h8 ah = fh[pm], al = fl[pm];
-#pragma unroll
-                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], ah, c[n][m], 0, 0, 0);
-#pragma unroll
-                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][1], ah, c[n][m], 0, 0, 0);
-#pragma unroll
-                        for (int n = 0; n < 4; n++) c[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[sl][n][0], al, c[n][m], 0, 0, 0);
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < 4; n++)
-#pragma unroll
-        for (int m = 0; m < NT; m++) acc[n][m] = c[n][m];
-}
-
 // ------------------------------------------------------------------ epilogue
 struct H4x2 {
     h4 h, l;
@@ -603,7 +437,7 @@ __device__ __forceinline__ void put_hl_lds(_Float16* p, int plane_halves, const 
 // groups of GB tiles, loads ST - 1 groups ahead.
 template <int L>
 __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const uint32_t* rt, int np, int lane,
-                                            const f32x4 (&acc)[2][K::NMAX], int nt) {
+                                            const f32x4 (&acc)[2][K::NMAX], int nt, int ldsg) {
     constexpr int RO = L + 2, SO = dg_so(L), SSO = SO * SO;
     constexpr bool SKIP = L == 1 || L == 3;
     constexpr int RS = L == 1 ? 1 : 3, SK = 2 * RS + 1, SSK = SK * SK;
@@ -690,7 +524,13 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
                 if (L < 3 && v) {
                     const DgUnit& u = U[gi];
                     const int o = PATCH_OFF[L + 1] + ((ch0 >> 3) * SSO + oidx) * 8 + (ch0 & 7);
-                    put_hl(u.own + o, 16 * SSO * 8, d);
+                    if (gi < ldsg) {  // the next pass's image (dg_fill<L + 1>'s layout)
+                        constexpr int NPN = K::npos(L + 1 < 4 ? L + 1 : 3), SSN = SSO;
+                        put_hl_lds((_Float16*)(lds + K::IN) + ((ch0 >> 3) * NPN + gi * SSN + oidx) * 8 + (ch0 & 7),
+                                   16 * NPN * 8, d);
+                    } else {
+                        put_hl(u.own + o, 16 * SSO * 8, d);
+                    }
                     if (u.patch) put_hl(u.patch + o, 16 * SSO * 8, y);
                 }
             }
@@ -707,112 +547,6 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
                     h[121] = s1;
                     h[242] = sv;
                 }
-            }
-        }
-    }
-}
-
-// The same epilogue for the 4-n-tile ownership (dg_kloop4): the wave's tiles m = 2 j + mh
-// (ntw of them), its 64 channels; one tile per load group, loads ST - 1 tiles ahead.  x2:
-// the head partial sums of its 64 channels into hpart slot ng.
-template <int L, int ST>
-__device__ __forceinline__ void dg_epilogue4(char* lds, const DgUnit* U, const uint32_t* rt, int ng, int mh,
-                                             int lane, const f32x4 (&acc)[4][K::NTW], int ntw) {
-    constexpr int RO = L + 2, SO = dg_so(L), SSO = SO * SO;
-    constexpr bool SKIP = L == 1 || L == 3;
-    constexpr int RS = L == 1 ? 1 : 3, SK = 2 * RS + 1, SSK = SK * SK;
-    float* hpart = (float*)(lds + K::HP);
-    const int q = lane >> 4, li = lane & 15;
-    const float* cst = (const float*)(lds + K::CST);  // staged at kernel start
-    f32x4 es[4];
-#pragma unroll
-    for (int n = 0; n < 4; n++) es[n] = *(const f32x4*)(cst + L * 128 + (4 * ng + n) * 16 + 4 * q);
-    f32x4 z[ST][4];
-    H4x2 dk[ST][4];
-    uint32_t ent[ST];
-    auto loads = [&](int j, int st) {
-        uint32_t e = rt[(2 * j + mh) * 16 + li];
-#ifdef GZ_DG_CHK
-        if ((e & 15) >= (uint32_t)K::C) {
-            atomicAdd(&gz_dg_chk[6], 1ull);
-            e = 0;
-        }
-#endif
-        ent[st] = e;
-        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
-        const DgUnit& u = U[gi];
-        const int cell = u.cell, cr = cell / BN, cc = cell - (cell / BN) * BN;
-        const bool v = (e >> 21) & 1u;
-        const int pos = v ? (cr + dy) * BN + (cc + dx) : 0;
-        const bool near = SKIP && v && iabs(dy) <= RS && iabs(dx) <= RS;
-        const int sidx = near ? (dy + RS) * SK + (dx + RS) : 0;
-#pragma unroll
-        for (int n = 0; n < 4; n++) {
-            const int ch0 = (4 * ng + n) * 16 + 4 * q;
-            z[st][n] = gld<f32x4>(u.pre + L * PV_PRE_FLOATS + pos * CH + ch0);
-            if (SKIP) {
-                const _Float16* p = u.own + PATCH_OFF[L - 1] + ((ch0 >> 3) * SSK + sidx) * 8 + (ch0 & 7);
-                dk[st][n] = H4x2{gld<h4>(p), gld<h4>(p + 16 * SSK * 8)};
-            }
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < ST - 1; j++)
-        if (j < ntw) loads(j, j);
-#pragma unroll
-    for (int j = 0; j < K::NTW; j++) {
-        if (j >= ntw) break;
-        const int st = j % ST;
-        if (j + ST - 1 < ntw) loads(j + ST - 1, (j + ST - 1) % ST);
-        const uint32_t e = ent[st];
-        const bool v = (e >> 21) & 1u;
-        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
-        const bool near = SKIP && iabs(dy) <= RS && iabs(dx) <= RS;
-        const int oidx = (dy + RO) * SO + (dx + RO);
-        float s0 = 0.f, s1 = 0.f, sv = 0.f;
-#pragma unroll
-        for (int n = 0; n < 4; n++) {
-            const int ch0 = (4 * ng + n) * 16 + 4 * q;
-            f32x4 y, d, h0, h1, hv;
-            if (L == 3) {
-                h0 = *(const f32x4*)(cst + 512 + ch0);
-                h1 = *(const f32x4*)(cst + 640 + ch0);
-                hv = *(const f32x4*)(cst + 768 + ch0);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float zr = z[st][n][r];
-                float tc = __builtin_fmaf(acc[n][j][r], es[n][r], zr);
-                if (SKIP) tc += near ? h2f(dk[st][n], r) : 0.f;
-                tc = tc > 0.f ? tc : 0.f;
-                if (L == 3) {
-                    s0 = __builtin_fmaf(h0[r], tc, s0);
-                    s1 = __builtin_fmaf(h1[r], tc, s1);
-                    sv = __builtin_fmaf(hv[r], tc, sv);
-                } else {
-                    y[r] = tc;
-                    d[r] = tc - (zr > 0.f ? zr : 0.f);
-                }
-            }
-            if (L < 3 && v) {
-                const DgUnit& u = U[gi];
-                const int o = PATCH_OFF[L + 1] + ((ch0 >> 3) * SSO + oidx) * 8 + (ch0 & 7);
-                put_hl(u.own + o, 16 * SSO * 8, d);
-                if (u.patch) put_hl(u.patch + o, 16 * SSO * 8, y);
-            }
-        }
-        if (L == 3) {
-            s0 += __shfl_xor(s0, 16);
-            s1 += __shfl_xor(s1, 16);
-            sv += __shfl_xor(sv, 16);
-            s0 += __shfl_xor(s0, 32);
-            s1 += __shfl_xor(s1, 32);
-            sv += __shfl_xor(sv, 32);
-            if (lane < 16 && v) {
-                float* h = hpart + ((gi * 4 + ng) * 3) * 121 + oidx;
-                h[0] = s0;
-                h[121] = s1;
-                h[242] = sv;
             }
         }
     }
@@ -856,7 +590,7 @@ __device__ __forceinline__ void dg_record(const DgUnit& u, int g, const float* b
                 const int idx = (dy + 5) * 11 + (dx + 5);
                 float a = bias[which];
 #pragma unroll
-                for (int w = 0; w < K::HPW; w++) a += hpart[((g * 4 + w) * 3 + which) * 121 + idx];
+                for (int w = 0; w < 4; w++) a += hpart[((g * 4 + w) * 3 + which) * 121 + idx];
                 v = a;
             }
         }
@@ -1022,39 +756,16 @@ __device__ __forceinline__ void dg_pass(const char* lds, const uint32_t* rt, con
         dg_kloop<K::NMAX, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
 }
 
-// the same for the 4-n-tile ownership: the wave's tiles m = 2 j + mh
-template <int L>
-__device__ __forceinline__ void dg_pass4(const char* lds, const uint32_t* rt, const uint32_t* mk,
-                                         const float* __restrict__ W, int ng, int mh, int lane,
-                                         f32x4 (&acc)[4][K::NTW], int nt) {
-    constexpr int RIN = L + 1, RO = L + 2, S = dg_s(L), SS = dg_ss(L);
-    const int li = lane & 15;
-    uint32_t ri[K::NTW];
-#pragma unroll
-    for (int j = 0; j < K::NTW; j++) {
-        const uint32_t e = rt[(2 * j + mh) * 16 + li];
-        const int gi = e & 15, dy = (int)((e >> 4) & 15) - RO, dx = (int)((e >> 8) & 15) - RO;
-        const int base = gi * SS + (dy + RIN) * S + (dx + RIN) + 32;
-        ri[j] = (e >> 21) & 1u ? ((uint32_t)base & 0xffffu) | (((e >> 12) & 0x1ffu) << 16) : 0u;
-    }
-#pragma unroll
-    for (int n = 0; n < 4; n++)
-#pragma unroll
-        for (int j = 0; j < K::NTW; j++) acc[n][j] = zero4();
-    const _Float16* Wf = (const _Float16*)(W + F16_RES0 + L * F16_STRIDE);
-    // tiles per wave rounded up to even (both waves of an n-half run the same instantiation)
-    if (nt <= 4)
-        dg_kloop4<2, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
-    else if (nt <= 8)
-        dg_kloop4<4, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
-    else
-        dg_kloop4<K::NTW, L, GZ_DG_RING>(lds, ri, mk, Wf, 4 * ng, mh, lane, acc);
-}
-
 // pass p of a chunk of ng nodes: its layer L, first node u0 and node count g (0: empty)
 __device__ __forceinline__ void dg_pass_of(int p, int ng, int& L, int& u0, int& g) {
-    L = p >= K::pb(3) ? 3 : (p >= K::pb(2) ? 2 : (p >= K::pb(1) ? 1 : 0));
-    u0 = (p - K::pb(L)) * K::g(L);
+    if (p < 3) {  // (K::pass_of inverted)
+        L = p == 0 ? 0 : 1;
+        u0 = p == 0 ? 0 : (p - 1) * 3;
+    } else {
+        const int k = (p - 3) / 3, r = p - 3 - 3 * k;
+        L = r == 0 ? 2 : 3;
+        u0 = 2 * k + (r == 2 ? 1 : 0);
+    }
     g = ng - u0 < K::g(L) ? ng - u0 : K::g(L);
     if (L == 0) u0 = 0, g = ng;
 }
@@ -1131,6 +842,20 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             dg_conv0(lds, (const _Float16*)(lds + K::COL), U, ng, Wp, np, t & 63);
             dg_rows_all(lds, U, ng, t);
             __syncthreads();  // the y1 image, the row tables and tap masks
+#ifdef GZ_DG_CHK
+            // every table entry below its pass's row count names a node of that pass
+            for (int e = tid; e < K::NPASS * K::ROWS; e += NTD) {
+                const int pp = e / K::ROWS;
+                int L_, u0_, g_;
+                dg_pass_of(pp, ng, L_, u0_, g_);
+                const uint32_t tot = ((const uint32_t*)(lds + K::MASK))[pp * 16 + 9];
+                const uint32_t en = ((const uint32_t*)(lds + K::ROWT))[e];
+                if ((uint32_t)(e % K::ROWS) < tot && (!((en >> 21) & 1u) || (int)(en & 15) >= g_))
+                    atomicAdd(&gz_dg_chk[8], 1ull);
+                if ((uint32_t)(e % K::ROWS) >= tot && en != 0u) atomicAdd(&gz_dg_chk[9], 1ull);
+            }
+            if (tid < K::C && (U[tid].cell < 0 || U[tid].cell >= 225) && tid < ng) atomicAdd(&gz_dg_chk[10], 1ull);
+#endif
         }
         st(0);
 #ifdef GZ_PVDG_STAMPS
@@ -1147,20 +872,18 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             const float* Wp = W;
             int t = tid;
             asm volatile("" : "+s"(Wp), "+v"(t));
-#if GZ_DG_N4
-            const int ng = wave & 1, mh = wave >> 1, ntw = (nt - mh + 1) >> 1;
-            f32x4 acc[4][K::NTW];
-            if (L == 0) dg_pass4<0>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
-            else if (L == 1) dg_pass4<1>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
-            else if (L == 2) dg_pass4<2>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
-            else dg_pass4<3>(lds, rt, mk, Wp, ng, mh, t & 63, acc, nt);
-#else
+#ifdef GZ_DG_CHK
+            for (int e = tid; e < K::ROWS; e += NTD) {
+                const uint32_t en = rt[e];
+                if ((uint32_t)e < (uint32_t)nrows && (!((en >> 21) & 1u) || (int)(en & 15) >= g))
+                    atomicAdd(&gz_dg_chk[11 + (L > 1 ? 1 : 0)], 1ull);
+            }
+#endif
             f32x4 acc[2][K::NMAX];
             if (L == 0) dg_pass<0>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else if (L == 1) dg_pass<1>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else if (L == 2) dg_pass<2>(lds, rt, mk, Wp, np, t & 63, acc, nt);
             else dg_pass<3>(lds, rt, mk, Wp, np, t & 63, acc, nt);
-#endif
             st(2 + L);
             __syncthreads();  // every wave is past the k-loop: the image is free
             st(6);
@@ -1172,17 +895,24 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
                 if (g2 > 0) break;
             }
             const bool more = q < K::NPASS;
-#if GZ_DG_N4
-            if (L == 0) dg_epilogue4<0, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
-            else if (L == 1) dg_epilogue4<1, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
-            else if (L == 2) dg_epilogue4<2, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
-            else dg_epilogue4<3, GZ_DG_EST>(lds, U + u0, rt, ng, mh, t & 63, acc, ntw);
-#else
-            if (L == 0) dg_epilogue<0>(lds, U + u0, rt, np, t & 63, acc, nt);
-            else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, np, t & 63, acc, nt);
-            else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, np, t & 63, acc, nt);
-            else dg_epilogue<3>(lds, U + u0, rt, np, t & 63, acc, nt);
-#endif
+            // When the next pass is the next layer of this pass's first nodes (y1 -> x1(0..2),
+            // y2(2k, 2k+1) -> x2(2k)), those nodes' D squares go straight into the next
+            // pass's LDS image (dg_fill's layout) instead of the scratch: no store, no fill,
+            // no drain; the pass's other nodes go through the scratch as before.  (The
+            // epilogue's scattered 8-B stores of the D squares are 15 % of the kernel.)
+            const int ldsg = more && L2 == L + 1 && v0 == u0 && (L == 0 || L == 2) ? g2 : 0;
+            const bool to_lds = ldsg > 0;
+            if (L == 0) dg_epilogue<0>(lds, U + u0, rt, np, t & 63, acc, nt, ldsg);
+            else if (L == 1) dg_epilogue<1>(lds, U + u0, rt, np, t & 63, acc, nt, 0);
+            else if (L == 2) dg_epilogue<2>(lds, U + u0, rt, np, t & 63, acc, nt, ldsg);
+            else dg_epilogue<3>(lds, U + u0, rt, np, t & 63, acc, nt, 0);
+            if (to_lds) {  // the image's zero slots past the nodes' squares (dg_fill writes them)
+                const int NPN = L == 0 ? K::npos(1) : K::npos(3), z0 = ldsg * (L == 0 ? dg_ss(1) : dg_ss(3));
+                for (int e = t; e < 32 * (NPN - z0); e += NTD) {
+                    const int pc = e / (NPN - z0), idx = z0 + e % (NPN - z0);
+                    *(uint4*)(lds + K::IN + (pc * NPN + idx) * 16) = make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
             st(7 + L);
             // vmcnt counts loads, stores and LDS-DMA together in issue order, so each wait
             // below also waits for every older store.  The next pass's fill reads, by
@@ -1190,13 +920,13 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             // the next layer over some of the same nodes (y1 -> the first x1 pass): then
             // every wave's stores complete before a barrier first.  x2: the barrier
             // publishes hpart for the record.
-            const bool reads_mine = more && L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2;
+            const bool reads_mine = more && !to_lds && L2 == L + 1 && v0 < u0 + g && u0 < v0 + g2;
             if (reads_mine) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (reads_mine || L == 3) __syncthreads();
             st(11);
             // the fill goes out first; an x2 pass's record (the root's record loaded, the
             // node's written) follows, its loads in flight with the fill's
-            if (more) {
+            if (more && !to_lds) {
                 if (L2 == 1) dg_fill<1>(lds, U + v0, g2, t);
                 else if (L2 == 2) dg_fill<2>(lds, U + v0, g2, t);
                 else if (L2 == 3) dg_fill<3>(lds, U + v0, g2, t);
@@ -1274,6 +1004,6 @@ extern "C" int gz_pvdg_stamps_read(unsigned long long* out, int reset) {
 // out-of-workspace global accesses per code (loads, stores, fills, record reads, record writes)
 extern "C" int gz_pvdg_chk_read(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_dg_chk), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gz_dg_chk), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
 #endif

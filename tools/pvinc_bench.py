@@ -86,10 +86,12 @@ def main():
     if hasattr(lib, "gz_pvdg_chk_read"):  # -DGZ_DG_CHK build: global accesses outside the workspace
         import ctypes
         lib.gz_pvdg_chk_read.argtypes = [ctypes.c_void_p]
-        chk = np.zeros(8, np.uint64)
+        chk = np.zeros(16, np.uint64)
         tree()
         lib.gz_pvdg_chk_read(chk.ctypes.data)
-        print("pv_dg_kernel out-of-workspace accesses (load, store, fill, record r/w):", chk[:5].tolist(), flush=True)
+        print("pv_dg_kernel checks (loads / stores / fills / record r / record w outside the workspace, LDS "
+              "fragment reads, row node index, x2 partial index, tables bad at chunk start, stale past the count, bad "
+              "cells, tables bad before y1/x1 passes, before y2/x2 passes):", chk.tolist(), flush=True)
     timed(run, "tree")
     torch.cuda.synchronize()
     out = [t[: n * k].clone() for t, k in ((eng.d_logits, 225), (eng.d_value, 1), (eng.d_probs, 225),
