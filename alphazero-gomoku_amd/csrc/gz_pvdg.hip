@@ -113,13 +113,27 @@ static_assert(dgk_g(0) * dg_so(0) * dg_so(0) <= K::ROWS && dgk_g(1) * dg_so(1) *
 static_assert(K::C % 6 == 0 && dgk_g(3) == 1, "passes; one x2 node per pass (the record prefetch)");
 static_assert(K::C == 6 && dgk_g(1) == 3 && dgk_g(2) == 2, "pass order (K::pass_of, dg_pass_of): 2 x1 triples, 3 y2 pairs");
 
+// The workgroup's scratch: the D squares that cross passes, each map's squares in a
+// region of their own ([2 planes][16 cg][square][8] halves per node), sized by what is
+// live at once in the pass order -- x0 r1 of the 6 nodes (to the x1 passes' skip), x1 r3
+// of the 6 (to the y2 passes and the x2 skip), and one region shared by y1 r2 of nodes
+// 3..5 (the first x1 pass takes nodes 0..2's from LDS; dead after the second x1 pass) and
+// y2 r4 of node 2k + 1 (node 2k's goes through LDS; dead after x2(2k + 1), before the next
+// pair's y2 writes).  429 positions x 512 B = 215 KiB per workgroup instead of 6 patch
+// layouts (504 KiB): less to evict from L2 per chunk.
+__host__ __device__ constexpr int scr_sq(int map, int node) {
+    return (map == 0 ? 9 * node : (map == 2 ? 54 + 49 * node : (map == 1 ? 348 + (node >= 3 ? 25 * (node - 3) : 0) : 348))) * 256;
+}
+constexpr int SCR_HALVES = (348 + 81) * 256;
+static_assert(348 + 3 * 25 <= 348 + 81 && 54 + 49 * 6 == 348, "scratch regions");
+
 struct DgUnit {
     const _Float16* gm;  // the root's maps x0, y1, x1, y2 (hi / lo)
     const float* pre;    // the root's pre-ReLU values of y1, x1, y2, x2
-    _Float16* own;       // this node's D squares (patch layout), workgroup scratch
+    _Float16* own;       // the workgroup's scratch: this node's D square of map k at own + sq[k]
     _Float16* patch;     // its patch slot (child values for its grandchildren), or nullptr
     int leaf, base, cell, pad0;
-    int pad[4];
+    int sq[4];           // halves offsets of its D squares x0 r1, y1 r2, x1 r3, y2 r4 (scr_sq)
     uint32_t board[16];  // the node's bit-plane board (conv0's input)
 };
 static_assert(sizeof(DgUnit) == 128, "unit size");
@@ -478,7 +492,7 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
                 const int ch0 = (2 * np + n) * 16 + 4 * q;
                 z[st][j][n] = gld<f32x4>(u.pre + L * PV_PRE_FLOATS + pos * CH + ch0);
                 if (SKIP) {
-                    const _Float16* p = u.own + PATCH_OFF[L - 1] + ((ch0 >> 3) * SSK + sidx) * 8 + (ch0 & 7);
+                    const _Float16* p = u.own + u.sq[L - 1] + ((ch0 >> 3) * SSK + sidx) * 8 + (ch0 & 7);
                     dk[st][j][n] = H4x2{gld<h4>(p), gld<h4>(p + 16 * SSK * 8)};
                 }
             }
@@ -529,7 +543,7 @@ __device__ __forceinline__ void dg_epilogue(char* lds, const DgUnit* U, const ui
                         put_hl_lds((_Float16*)(lds + K::IN) + ((ch0 >> 3) * NPN + gi * SSN + oidx) * 8 + (ch0 & 7),
                                    16 * NPN * 8, d);
                     } else {
-                        put_hl(u.own + o, 16 * SSO * 8, d);
+                        put_hl(u.own + u.sq[L + 1] + ((ch0 >> 3) * SSO + oidx) * 8 + (ch0 & 7), 16 * SSO * 8, d);
                     }
                     if (u.patch) put_hl(u.patch + o, 16 * SSO * 8, y);
                 }
@@ -614,7 +628,7 @@ __device__ __forceinline__ void dg_fill(char* lds, const DgUnit* U, int g, int t
         int stride = 0;
         if (idx < g * SS) {
             const int gi = idx / SS, j = idx - gi * SS;
-            src = U[gi].own + PATCH_OFF[L] + j * 8;
+            src = U[gi].own + U[gi].sq[L] + j * 8;
             stride = SS * 8;
         }
         char* dst = lds + K::IN + blk * 64 * 16;
@@ -718,7 +732,7 @@ __device__ __forceinline__ void dg_conv0(char* lds, const _Float16* col, const D
                 }
                 put_hl_lds(in + ((ch0 >> 3) * NPOS + g * 9 + idx) * 8 + (ch0 & 7), 16 * NPOS * 8, d);
                 const int o = PATCH_OFF[0] + ((ch0 >> 3) * 9 + idx) * 8 + (ch0 & 7);
-                put_hl(u.own + o, 16 * 9 * 8, d);
+                put_hl(u.own + u.sq[0] + o, 16 * 9 * 8, d);
                 if (u.patch) put_hl(u.patch + o, 16 * 9 * 8, y);
             }
         }
@@ -784,7 +798,7 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
     const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
-    _Float16* myscr = scratch + (size_t)blockIdx.x * K::C * PATCH_HALVES;
+    _Float16* myscr = scratch + (size_t)blockIdx.x * SCR_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave;
     const float* W = A.W;
@@ -811,15 +825,17 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
             const int o = (ci >> 8) & 0x3fffff;
             u.gm = A.maps + (size_t)o * 4 * PV_MAP_HALVES;
             u.pre = A.pres + (size_t)o * 4 * PV_PRE_FLOATS;
-            u.own = myscr + (size_t)lane * PATCH_HALVES;
+            u.own = myscr;
+            u.sq[0] = scr_sq(0, lane);
+            u.sq[1] = scr_sq(1, lane);
+            u.sq[2] = scr_sq(2, lane);
+            u.sq[3] = scr_sq(3, lane);
             const int ps = A.pslot[b];
             u.patch = ps >= 0 ? A.patches + (size_t)ps * PATCH_HALVES : nullptr;
             u.leaf = b;
             u.base = A.meta[b];
             u.cell = ci & 0xff;
             u.pad0 = 0;
-#pragma unroll
-            for (int w = 0; w < 4; w++) u.pad[w] = 0;
 #pragma unroll
             for (int w = 0; w < 16; w++) u.board[w] = A.boards[(size_t)b * 16 + w];
             U[lane] = u;
@@ -961,7 +977,7 @@ extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_
                                       int grid, void* stream) {
     DgArgs A{d_cinfo, d_weights, d_boards, d_meta, d_pslot, d_maps, d_pres, d_patches, d_hbuf, d_tiles};
     // K::WPS workgroups per grid entry (CU), K::C patch-sized scratch areas each
-    static_assert(K::C * K::WPS <= PV_SCRATCH_PATCHES, "scratch");
+    static_assert(K::WPS * SCR_HALVES <= PV_SCRATCH_PATCHES * PATCH_HALVES, "scratch");
 #ifdef GZ_PVDG_STAMPS
     // stamp builds: GZ_PVDG_WPS=1 runs one workgroup per CU (the k-loop without a co-resident one)
     static const int wps = std::getenv("GZ_PVDG_WPS") && std::getenv("GZ_PVDG_WPS")[0] == '1' ? 1 : K::WPS;
