@@ -90,7 +90,7 @@ def load_traffic(boards, mode):
 def load_clock(kernel):
     """Measured shader clock and MFMA-busy share of `kernel` under load (newest
     profiles/rNN/clock.json that has it), or None."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(REPO, "profiles", rnd, "clock.json")
         if os.path.exists(p):
             with open(p) as f:
