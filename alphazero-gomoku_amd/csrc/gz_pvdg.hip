@@ -325,9 +325,6 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
     const int wo = (nt0 * 64 + lane) * 16;
     auto wload = [&](int ks, int n, int lo) -> h8 {
-#ifdef GZ_DG_PROBE_W
-        ks = 0;  // (probe, wrong results: every weight load hits the L1-resident k-step 0)
-#endif
         return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wo, ks * KS_BYTES + n * 1024 + lo * LO_BYTES, 0));
     };
     auto addr = [&](int tap, uint32_t r) -> int {
