@@ -57,6 +57,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ uint4 gz_dg_zero16[1];  // zero source of the LDS-DMA fills
 
 constexpr int NTD = 256;  // 4 waves
+#ifndef GZ_DG_NTE
+#define GZ_DG_NTE 1
+#endif
 constexpr int PATCH_HALVES = PV_PATCH_HALVES;
 constexpr int PATCH_OFF[4] = {0, 9 * 256, 34 * 256, 83 * 256};  // x0 r1, y1 r2, x1 r3, y2 r4 (halves)
 __host__ __device__ constexpr int dg_s(int L) { return 2 * L + 3; }  // D-square width (radius L+1)
@@ -378,9 +381,9 @@ __device__ __forceinline__ void dg_kloop(const char* lds, const uint32_t (&ri)[K
             }
 #pragma unroll
             for (int m = 0; m < NT; m++) {
-                // fragment parity of tile m in unit h: the units of a tap hold 2 NT fragments
-                // (even), so it does not depend on the tap
-                const int pm = (h * NT + m) & 1, pn = (h * NT + m + 1) & 1;
+                // (NT is even: a unit reads an even number of fragment pairs, so tile m's
+                // parity is m & 1 on every tap)
+                const int pm = m & 1, pn = (m + 1) & 1;
                 // the next tile's pair: tile m + 1, else tile 0 of the next unit (the second
                 // half of this tap, or the next tap's first, whose address ad[0] holds)
                 int na;
@@ -762,12 +765,32 @@ __device__ __forceinline__ void dg_pass(const char* lds, const uint32_t* rt, con
     const _Float16* Wf = (const _Float16*)(W + F16_RES0 + L * F16_STRIDE);
     // the tile count rounded up to a multiple of 4: the padding tiles (no rows, no taps)
     // still cost their fragment reads
+#if GZ_DG_NTE
+    // instantiated per even tile count up to the layer's most: a padding tile costs
+    // its fragment reads and their wait
+    constexpr int MT = (dgk_g(L) * dg_so(L) * dg_so(L) + 15) / 16, MTE = (MT + 1) & ~1;
+    static_assert(MTE <= K::NMAX, "tiles");
+    const int nte = (nt + 1) & ~1;
+    if (nte <= 2)
+        dg_kloop<2, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+    else if (nte == 4)
+        dg_kloop<4, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+    else if (nte == 6 || MTE <= 6)
+        dg_kloop<6 < MTE ? 6 : MTE, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+    else if (nte == 8 || MTE <= 8)
+        dg_kloop<8 < MTE ? 8 : MTE, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+    else if (nte == 10 || MTE <= 10)
+        dg_kloop<10 < MTE ? 10 : MTE, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+    else
+        dg_kloop<MTE, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+#else
     if (nt <= 4)
         dg_kloop<4, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
     else if (nt <= 8)
         dg_kloop<8, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
     else
         dg_kloop<K::NMAX, L>(lds, ri, mk, Wf, 2 * np, lane, acc);
+#endif
 }
 
 // pass p of a chunk of ng nodes: its layer L, first node u0 and node count g (0: empty)
