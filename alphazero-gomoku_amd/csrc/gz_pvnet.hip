@@ -812,77 +812,85 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
 // multiple of 8), restated here term for term so the sum rounds exactly like the
 // reference's (oracle.np_pairwise_sum).  Output: dense [n][225] float64, the prior at
 // empty cells and 0 at stones (the reference's compact vector = dense[empty cells]).
-// One workgroup per 64 boards; lane b of wave 0 sums board b.
+// One workgroup per 64 boards, a wave per board (16 in turn): the empty cells'
+// terms compacted in row-major order by ballot prefix counts, then the pairwise sum
+// with numpy's association -- lane j < 8 of block k runs the j-th of its 8 interleaved
+// accumulators (<= 16 terms in order), one lane combines them and adds the remainder.
 constexpr int PR_B = 64;
+constexpr int PR_PER_WAVE = PR_B / 4;
 
-__device__ double np_pairwise_block(const float* a, int m) {
-    if (m < 8) {
-        double res = 0.0;
-        for (int i = 0; i < m; i++) res += (double)a[i];
-        return res;
+// one block of np_pairwise_block (n terms at a[0..n)) with lanes l0 .. l0 + 7 of the
+// wave; every lane returns the block's sum
+__device__ __forceinline__ double np_pairwise_block_wave(const float* a, int n, int l0, int lane) {
+    const int j = lane - l0;
+    const int nfull = n - n % 8;
+    double r = 0.0;
+    if (n >= 8 && j >= 0 && j < 8) {
+        r = (double)a[j];
+        for (int i = 8 + j; i < nfull; i += 8) r += (double)a[i];
     }
-    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-    int i = 8;
-    for (; i < m - (m % 8); i += 8) {
-        r0 += (double)a[i];
-        r1 += (double)a[i + 1];
-        r2 += (double)a[i + 2];
-        r3 += (double)a[i + 3];
-        r4 += (double)a[i + 4];
-        r5 += (double)a[i + 5];
-        r6 += (double)a[i + 6];
-        r7 += (double)a[i + 7];
+    double rr[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) rr[t] = __shfl(r, l0 + t);
+    double res;
+    if (n < 8) {
+        res = 0.0;
+        for (int i = 0; i < n; i++) res += (double)a[i];
+    } else {
+        res = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+        for (int i = nfull; i < n; i++) res += (double)a[i];
     }
-    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < m; i++) res += (double)a[i];
     return res;
 }
 
 __global__ __launch_bounds__(256) void pv_prior_kernel(const uint32_t* __restrict__ boards, int n, const int32_t* d_count,
                                                        const float* __restrict__ probs, double* __restrict__ prior) {
-    __shared__ float p[PR_B * POS];          // probs, then each board's empty-cell terms compacted in place
-    __shared__ uint32_t occ[PR_B * 8];       // stones (black | white) per board
-    __shared__ double psum[PR_B];
+    __shared__ float terms[4][256];  // a wave's board: the empty cells' terms, compacted
     const int count = board_count(n, d_count);
-    const int b0 = blockIdx.x * PR_B;
-    if (b0 >= count) return;
-    const int nb = count - b0 < PR_B ? count - b0 : PR_B;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < nb * POS; i += 256) p[i] = probs[(size_t)b0 * POS + i];
-    for (int i = tid; i < nb * 8; i += 256) {
-        const uint32_t* bd = boards + (size_t)(b0 + (i >> 3)) * 16;
-        occ[i] = bd[i & 7] | bd[8 + (i & 7)];
-    }
-    __syncthreads();
-    if (tid < nb) {
-        float* a = p + tid * POS;
-        const uint32_t* o = occ + tid * 8;
-        int k = 0;
-        for (int cell = 0; cell < POS; cell++) {  // row-major empty cells (k <= cell: in place is safe)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float* a = terms[wave];
+    for (int i = 0; i < PR_PER_WAVE; i++) {
+        const int b = blockIdx.x * PR_B + wave * PR_PER_WAVE + i;
+        if (b >= count) break;
+        const uint32_t* bd = boards + (size_t)b * 16;
+        float pv[4];
+        bool empty[4];
+        int m = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int cell = 64 * u + lane;
             const int bit = (cell / 15) * 16 + cell % 15;
-            if (!((o[bit >> 5] >> (bit & 31)) & 1u)) a[k++] = a[cell];
+            const int w = cell < POS ? bit >> 5 : 0;
+            const bool occ = ((bd[w] | bd[8 + w]) >> (bit & 31)) & 1u;
+            empty[u] = cell < POS && !occ;
+            pv[u] = cell < POS ? probs[(size_t)b * POS + cell] : 0.f;
+            const uint64_t mk = __ballot(empty[u]);
+            if (empty[u]) a[m + __popcll(mk & ((1ull << lane) - 1ull))] = pv[u];
+            m += __popcll(mk);
         }
+        asm volatile("" ::: "memory");  // (a wave's LDS accesses execute in order)
         double s;
-        if (k <= 128) {
-            s = np_pairwise_block(a, k);
+        if (m <= 128) {
+            s = np_pairwise_block_wave(a, m, 0, lane);
         } else {
-            int k2 = k / 2;
+            int k2 = m / 2;
             k2 -= k2 % 8;
-            s = np_pairwise_block(a, k2) + np_pairwise_block(a + k2, k - k2);
+            const double s0 = np_pairwise_block_wave(a, k2, 0, lane);
+            const double s1 = np_pairwise_block_wave(a + k2, m - k2, 8, lane);
+            s = s0 + s1;
         }
-        psum[tid] = s;
-    }
-    __syncthreads();
-    for (int i = tid; i < nb * POS; i += 256) {
-        const int bb = i / POS, cell = i % POS;
-        const int bit = (cell / 15) * 16 + cell % 15;
-        double v = 0.0;
-        if (!((occ[bb * 8 + (bit >> 5)] >> (bit & 31)) & 1u)) {
-            const double x = (double)probs[(size_t)(b0 + bb) * POS + cell];
-            const double s = psum[bb];
-            v = s > 0.0 ? x / s : x;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int cell = 64 * u + lane;
+            if (cell >= POS) continue;
+            double v = 0.0;
+            if (empty[u]) {
+                const double x = (double)pv[u];
+                v = s > 0.0 ? x / s : x;
+            }
+            prior[(size_t)b * POS + cell] = v;
         }
-        prior[(size_t)(b0 + bb) * POS + cell] = v;
+        asm volatile("" ::: "memory");  // the terms are read before the next board's compaction
     }
 }
 
