@@ -531,7 +531,10 @@ __global__ void selfplay_init_kernel(char* slots, int n_slots, int64_t base, int
 
 // training.play_one_game (training.py:141-218) for one slot, n_plies plies,
 // restarting finished games.
-__global__ __launch_bounds__(WAVE, 4) void selfplay_kernel(char* slots, int n_slots, gz_search_params p, int n_plies,
+#ifndef GZ_SP_WPE
+#define GZ_SP_WPE 3  // selfplay_kernel: waves per SIMD the register allocation targets (4: 96 spilled VGPRs, 7 % slower)
+#endif
+__global__ __launch_bounds__(WAVE, GZ_SP_WPE) void selfplay_kernel(char* slots, int n_slots, gz_search_params p, int n_plies,
                                                            gz_record* records, int rec_cap, LeafSink sink, int gather,
                                                            gz_selfplay_counters* ctr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
