@@ -105,7 +105,8 @@ struct K {
     static constexpr int U = HIST + 2 * NPASS * NKEY * 4;  // units
     static constexpr int CST = U + C * 128;        // BN scales of the 4 residual layers [4][128], the 1x1 head
     static constexpr int CST_FLOATS = 4 * 128 + 3 * 128 + 4;  // weights [3][128], the 3 head biases
-    static constexpr int LDS = CST + CST_FLOATS * 4;
+    static constexpr int POS = CST + CST_FLOATS * 4;  // the chunk's first list entry (int)
+    static constexpr int LDS = POS + 16;
 };
 static_assert(dgk_npos(0) <= K::MAXNPOS && dgk_npos(1) <= K::MAXNPOS && dgk_npos(2) == K::MAXNPOS &&
                   dgk_npos(3) <= K::MAXNPOS, "image");
@@ -152,6 +153,7 @@ struct DgArgs {
     _Float16* patches;
     float* hbuf;
     int32_t* tiles;  // += executed tile-taps (one 16-row tile x one tap x 128 x 128)
+    int32_t* queue;  // [8] per-XCD chunk heads, zero at the launch
 };
 
 __device__ inline int iabs(int x) { return x < 0 ? -x : x; }
@@ -821,6 +823,12 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
     const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+    // the XCD's chunks are taken from its queue head in turn (a workgroup that finishes
+    // early takes more: no static share, no tail); lane 0 of wave 0 holds the next
+    // chunk's claim, made one chunk ahead so that the atomic's latency is hidden
+    int* const head = A.queue + xcd;
+    int claim = 0;
+    if (threadIdx.x == 0) claim = atomicAdd(head, K::C);
     _Float16* myscr = scratch + (size_t)blockIdx.x * SCR_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave;
@@ -838,8 +846,15 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
         }
     }
     DgStamp st;
-    for (int pos = xb + k * K::C; pos < xe; pos += per * K::C) {
-        __syncthreads();  // the previous chunk's readers of U, hpart and the tables are done
+    for (;;) {
+        __syncthreads();  // the previous chunk's readers of U, hpart, the tables and POS are done
+        if (threadIdx.x == 0) {
+            *(int*)(lds + K::POS) = xb + claim;
+            if (xb + claim < xe) claim = atomicAdd(head, K::C);
+        }
+        __syncthreads();
+        const int pos = *(const int*)(lds + K::POS);
+        if (pos >= xe) break;
         const int ng = xe - pos < K::C ? xe - pos : K::C;
         if (wave == 0 && lane < ng) {
             const int b = list[pos + lane];
@@ -996,9 +1011,9 @@ extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                       const int32_t* d_pslot, const int32_t* d_cinfo, const _Float16* d_maps,
                                       const float* d_pres, _Float16* d_patches, float* d_hbuf, _Float16* d_scratch,
-                                      int32_t* d_tiles, const int32_t* d_children, const int32_t* d_nchildren,
-                                      int grid, void* stream) {
-    DgArgs A{d_cinfo, d_weights, d_boards, d_meta, d_pslot, d_maps, d_pres, d_patches, d_hbuf, d_tiles};
+                                      int32_t* d_tiles, int32_t* d_queue, const int32_t* d_children,
+                                      const int32_t* d_nchildren, int grid, void* stream) {
+    DgArgs A{d_cinfo, d_weights, d_boards, d_meta, d_pslot, d_maps, d_pres, d_patches, d_hbuf, d_tiles, d_queue};
     // K::WPS workgroups per grid entry (CU), K::C patch-sized scratch areas each
     static_assert(K::WPS * SCR_HALVES <= PV_SCRATCH_PATCHES * PATCH_HALVES, "scratch");
 #ifdef GZ_PVDG_STAMPS

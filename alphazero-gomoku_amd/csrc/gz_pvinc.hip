@@ -1123,8 +1123,8 @@ extern "C" void gz_internal_set_error(const char* msg);
 extern "C" int gz_internal_tree_delta(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta,
                                       const int32_t* d_pslot, const int32_t* d_cinfo, const _Float16* d_maps,
                                       const float* d_pres, _Float16* d_patches, float* d_hbuf, _Float16* d_scratch,
-                                      int32_t* d_tiles, const int32_t* d_children, const int32_t* d_nchildren,
-                                      int grid, void* stream);
+                                      int32_t* d_tiles, int32_t* d_queue, const int32_t* d_children,
+                                      const int32_t* d_nchildren, int grid, void* stream);
 
 // Launches of the incremental forward's own kernels (called by gz_pv_forward_tree in
 // gz_pvnet.hip, which runs the full kernel on the root and full lists in between).
@@ -1134,7 +1134,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
                                          int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo,
                                          int32_t* d_children, void* stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(d_ctr, 0, 16 * sizeof(int32_t), s) != hipSuccess ||
+    if (hipMemsetAsync(d_ctr, 0, 32 * sizeof(int32_t), s) != hipSuccess ||  // (ctr[16..24): pv_dg_kernel's queue)
         (patch_cap > 0 && hipMemsetAsync(d_ghead, 0xff, (size_t)patch_cap * sizeof(int32_t), s) != hipSuccess)) {
         gz_internal_set_error("gz_pv_forward_tree: memset");
         return GZ_ERR_HIP;
@@ -1164,11 +1164,11 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         const float* d_pres, void* stream) {
+                                         const float* d_pres, int32_t* d_queue, void* stream) {
     TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
     hipStream_t s = (hipStream_t)stream;
     const int rc = gz_internal_tree_delta(d_weights, d_boards, d_meta, d_pslot, d_cinfo, d_maps, d_pres, d_patches,
-                                          d_hbuf, d_scratch, d_tiles, d_children, d_nchildren, grid, stream);
+                                          d_hbuf, d_scratch, d_tiles, d_queue, d_children, d_nchildren, grid, stream);
     if (rc) return rc;
     pv_sib_kernel<<<grid, NTS, 0, s>>>(A, d_scratch, n, d_count, d_grand, d_ngrand);
     hipError_t e = hipGetLastError();

@@ -978,7 +978,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          float* d_hbuf, const int32_t* d_grand, const int32_t* d_ngrand,
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
-                                         const float* d_pres, void* stream);
+                                         const float* d_pres, int32_t* d_queue, void* stream);
 
 namespace {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1052,14 +1052,15 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     const int grid = pv_grid(n);
     // roots (full forward, maps stored), then every board without a stored root or
     // patch (full forward), then the roots' children and their children (incremental);
-    // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed]
+    // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed, .., .,
+    //        executed tile-taps (children, grandchildren) at 8, 9, pv_dg_kernel's XCD queue heads at 16..23]
     pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
                                                      t.ord, t.maps, root_cap, t.pres);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
                                                       nullptr, nullptr, 0);
     rc = gz_internal_tree_children(d_weights, d_boards, d_meta, t.ord, t.pslot, n, d_count, t.maps, t.patches, t.hbuf,
                                    t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, t.children, t.ctr + 2, grid,
-                                   t.pres, stream);
+                                   t.pres, t.ctr + 16, stream);
     if (rc) return rc;
     pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
