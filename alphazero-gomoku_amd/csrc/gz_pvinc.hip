@@ -121,6 +121,7 @@ struct TreeArgs {
     _Float16* patches;
     float* hbuf;
     int32_t* tiles;  // 16-row MFMA tile-taps executed by the residual convs [children, grandchildren]
+    int32_t* queue;  // [8] per-XCD chunk heads of pv_sib_kernel, zero at the launch
 };
 
 // ============================================================ sibling-batched incremental forward
@@ -153,7 +154,8 @@ constexpr int SIB_WIN = SIB_G * wbytes(P_X0);
 static_assert(3 * wbytes(P_Y1) <= SIB_WIN && 2 * wbytes(P_X1) <= SIB_WIN && wbytes(P_Y2) <= SIB_WIN, "windows");
 constexpr int SIB_HP = SIB_WIN;                     // head partials [4 pairs][3][HP_ROWS]
 constexpr int SIB_U = SIB_HP + 4 * 3 * HP_ROWS * 4;  // unit table
-constexpr int LDS_S = SIB_U + SIB_G * 128;  // SibUnit: 128 B
+constexpr int SIB_POS = SIB_U + SIB_G * 128;  // SibUnit: 128 B; then the chunk's first list entry
+constexpr int LDS_S = SIB_POS + 16;
 static_assert(LDS_S <= 160 * 1024, "LDS budget");
 
 // phase stamps of pv_sib_kernel (workgroup 0, thread 0; -DGZ_PVINC_STAMPS builds only)
@@ -801,6 +803,11 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
     const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+    // the XCD's chunks from its queue head in turn (pv_dg_kernel's scheme: no static
+    // share, no tail); thread 0 claims one chunk ahead
+    int* const head = A.queue + xcd;
+    int claim = 0;
+    if (threadIdx.x == 0) claim = atomicAdd(head, SIB_G);
     _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
@@ -827,8 +834,15 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
             Ud[lane] = u;
         }
     };
-    for (int pos = xb + k * SIB_G; pos < xe; pos += per * SIB_G) {
-        __syncthreads();  // the previous chunk's readers of U are done
+    for (;;) {
+        __syncthreads();  // the previous chunk's readers of U and the chunk entry are done
+        if (threadIdx.x == 0) {
+            *(int*)(lds + SIB_POS) = xb + claim;
+            if (xb + claim < xe) claim = atomicAdd(head, SIB_G);
+        }
+        __syncthreads();
+        const int pos = *(const int*)(lds + SIB_POS);
+        if (pos >= xe) break;
         const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
         SibUnit* const U = U0;
         build(U, pos, ng);
@@ -1134,7 +1148,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
                                          int32_t* d_gnext, const uint32_t* d_boards, int32_t* d_cinfo,
                                          int32_t* d_children, void* stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(d_ctr, 0, 32 * sizeof(int32_t), s) != hipSuccess ||  // (ctr[16..24): pv_dg_kernel's queue)
+    if (hipMemsetAsync(d_ctr, 0, 32 * sizeof(int32_t), s) != hipSuccess ||  // (ctr[16..32): the queue heads)
         (patch_cap > 0 && hipMemsetAsync(d_ghead, 0xff, (size_t)patch_cap * sizeof(int32_t), s) != hipSuccess)) {
         gz_internal_set_error("gz_pv_forward_tree: memset");
         return GZ_ERR_HIP;
@@ -1165,7 +1179,7 @@ extern "C" int gz_internal_tree_children(const float* d_weights, const uint32_t*
                                          const int32_t* d_cinfo, _Float16* d_scratch, int32_t* d_tiles,
                                          const int32_t* d_children, const int32_t* d_nchildren, int grid,
                                          const float* d_pres, int32_t* d_queue, void* stream) {
-    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles};
+    TreeArgs A{d_cinfo, d_weights, d_boards, d_meta, d_ord, d_pslot, d_maps, d_patches, d_hbuf, d_tiles, d_queue + 8};
     hipStream_t s = (hipStream_t)stream;
     const int rc = gz_internal_tree_delta(d_weights, d_boards, d_meta, d_pslot, d_cinfo, d_maps, d_pres, d_patches,
                                           d_hbuf, d_scratch, d_tiles, d_queue, d_children, d_nchildren, grid, stream);

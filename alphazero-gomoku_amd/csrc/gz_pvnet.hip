@@ -1053,7 +1053,7 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
     // roots (full forward, maps stored), then every board without a stored root or
     // patch (full forward), then the roots' children and their children (incremental);
     // ctr = [roots seen, #roots, #children, #full, #grandchildren, patch slots claimed, .., .,
-    //        executed tile-taps (children, grandchildren) at 8, 9, pv_dg_kernel's XCD queue heads at 16..23]
+    //        executed tile-taps (children, grandchildren) at 8, 9, pv_dg_kernel's / pv_sib_kernel's XCD queue heads at 16..23 / 24..31]
     pv_kernel_f16x3<true, true><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.roots, t.ctr + 1,
                                                      t.ord, t.maps, root_cap, t.pres);
     pv_kernel_f16x3<true, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, t.hbuf, t.full, t.ctr + 3,
