@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
                                                         const int32_t* __restrict__ list,
                                                         const int32_t* __restrict__ list_count,
                                                         const GnTag* __restrict__ tags, char* __restrict__ slots,
-                                                        float* __restrict__ rec, int per) {
+                                                        float* __restrict__ rec, int per, int* __restrict__ queue) {
     __shared__ __attribute__((aligned(16))) char lds[ILDS];
     GnUnit* U = (GnUnit*)(lds + IU);
     _Float16* col = (_Float16*)(lds + ICOL);
@@ -1234,8 +1234,20 @@ __global__ __launch_bounds__(NTI, IWG) void gn_inc_kernel(const float* __restric
     // chunks of `per` (<= IG) boards: fewer than IG when the launch has too few rows to
     // give every CU a chunk of IG (a workgroup's time is a chain of short phases whose
     // k-loops scale with its tiles)
-    for (int pos0 = blockIdx.x * per; pos0 < count; pos0 += gridDim.x * per) {
-        __syncthreads();  // the previous chunk is done with U
+    // chunks claimed from the queue head in turn (a workgroup whose chunks were cheap takes
+    // more: no static share, no tail); thread 0 claims one chunk ahead and hands the
+    // claim over through pcv[0] (the policy-conv outputs are written at the chunk's end)
+    int claim = 0;
+    if (tid == 0) claim = atomicAdd(queue, per);
+    for (;;) {
+        __syncthreads();  // the previous chunk is done with U and pcv
+        if (tid == 0) {
+            *(int*)pcv = claim;
+            if (claim < count) claim = atomicAdd(queue, per);
+        }
+        __syncthreads();
+        const int pos0 = *(const int*)pcv;
+        if (pos0 >= count) break;
         const int ng = count - pos0 < per ? count - pos0 : per;
         if (tid < ng) {
             const int b = list[pos0 + tid];
@@ -1465,7 +1477,7 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
                                              const int32_t* d_full_count, const int32_t* d_inc_list,
                                              const int32_t* d_inc_count, const void* d_tags, void* d_slots,
                                              float* d_p, float* d_q, float* d_rec, float* d_hscratch,
-                                             void* stream) {
+                                             int32_t* d_queue, void* stream) {
     if (max_rows <= 0) return GZ_OK;
     const int cus = gn_cus();
     hipStream_t s = (hipStream_t)stream;
@@ -1480,7 +1492,8 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
     if (per_env >= 1 && per_env <= IG) per = per_env;
     const int chunks = (max_rows + per - 1) / per;
     gn_inc_kernel<<<chunks < IWG * cus ? chunks : IWG * cus, NTI, 0, s>>>(d_weights, d_rows, d_inc_list, d_inc_count,
-                                                              (const GnTag*)d_tags, (char*)d_slots, d_rec, per);
+                                                              (const GnTag*)d_tags, (char*)d_slots, d_rec, per,
+                                                              d_queue);
     gn_heads_launch(d_weights, d_rec, max_rows, d_count, d_p, d_q, nullptr, cus, s, d_hscratch);
     return gn_launch_check("gn_inc_kernel");
 }
@@ -1513,7 +1526,7 @@ extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boa
     float* hsc = rec + (size_t)n * REC;
     int32_t* lists = (int32_t*)(hsc + (size_t)n * HN_ROW);
     int32_t* counts = lists + 2 * (size_t)n;
-    if (hipMemsetAsync(counts, 0, 8, s) != hipSuccess) {
+    if (hipMemsetAsync(counts, 0, 12, s) != hipSuccess) {  // the two list counts, gn_inc_kernel's queue head
         gz_internal_set_error("gz_gn_forward_chain: memset");
         return GZ_ERR_HIP;
     }
@@ -1521,7 +1534,7 @@ extern "C" int gz_gn_forward_chain(const float* d_weights, const uint32_t* d_boa
     int rc = gn_launch_check("gn_split_kernel");
     if (rc) return rc;
     return gz_internal_gn_forward_tagged(d_weights, d_boards, n, nullptr, lists, counts, lists + n, counts + 1,
-                                         d_tags, d_slots, d_p, d_q, rec, hsc, stream);
+                                         d_tags, d_slots, d_p, d_q, rec, hsc, counts + 2, stream);
 }
 
 extern "C" int gz_gn_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,

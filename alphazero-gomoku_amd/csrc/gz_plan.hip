@@ -77,10 +77,11 @@ static_assert(sizeof(PlanJob) == 128, "job");
 struct Counters {
     int32_t rows;         // GN rows collected this round
     int32_t nfull, ninc;  // this planner step's full-forward / incremental rows
+    int32_t ihead;        // gn_inc_kernel's chunk queue head (cleared with rows, nfull, ninc)
     // games with a job after resume: only w.ctr's is used, cleared by the host right
     // before plan_resume_kernel and never by the per-step resets of (rows, nfull, ninc)
     int32_t pending;
-    int32_t pad[60];
+    int32_t pad[59];
 };
 // never cleared by a search: gz_plan_gn_stats reads (and resets) them
 struct GnStats {
@@ -887,7 +888,7 @@ __global__ __launch_bounds__(PW * WAVE) void plan_step4_kernel(Workspace w, gz_p
     __shared__ PlanShared4 sh;
     // the next planner step's counters (the other set: every kernel of the step that used
     // it is done) -- hipMemsetAsync's work, without a launch
-    if (blockIdx.x == 0 && threadIdx.x < 3) (&next->rows)[threadIdx.x] = 0;  // rows, nfull, ninc (not pending)
+    if (blockIdx.x == 0 && threadIdx.x < 4) (&next->rows)[threadIdx.x] = 0;  // rows, nfull, ninc, ihead (not pending)
     plan_step_row<PW>(w, pp, count_rows, &sh);
 }
 
@@ -1190,7 +1191,7 @@ extern "C" int gz_internal_gn_forward_tagged(const float* d_weights, const uint3
                                              const int32_t* d_full_count, const int32_t* d_inc_list,
                                              const int32_t* d_inc_count, const void* d_tags, void* d_slots,
                                              float* d_p, float* d_q, float* d_rec, float* d_hscratch,
-                                             void* stream);
+                                             int32_t* d_queue, void* stream);
 
 static int plan_fail(int code, const char* msg) {
     gz_internal_set_error(msg);
@@ -1261,8 +1262,8 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         wk.ctr = (step_no & 1) ? w.ctr2 : w.ctr;
         Counters* next = (step_no & 1) ? w.ctr : w.ctr2;
         step_no++;
-        // rows, nfull, ninc (pending is left alone: the resume's own memset clears it)
-        if (!zeroed && hipMemsetAsync(&wk.ctr->rows, 0, 3 * sizeof(int32_t), s) != hipSuccess)
+        // rows, nfull, ninc, ihead (pending is left alone: the resume's own memset clears it)
+        if (!zeroed && hipMemsetAsync(&wk.ctr->rows, 0, 4 * sizeof(int32_t), s) != hipSuccess)
             return plan_fail(GZ_ERR_HIP, "memset");
         // jobs j0 .. j1-1 (round 0's chunk), or (slot_game) the one job per game at g * S
         const int cnt = slot_game ? n : j1 - j0, stride = slot_game ? S : 1;
@@ -1276,7 +1277,8 @@ extern "C" int gz_internal_plan_search(const gz_board_state* d_boards, const int
         } else {
             if ((r = gz_internal_gn_forward_tagged(d_gn_weights, w.gn_in, max_rows, &wk.ctr->rows, w.full_list,
                                                    &wk.ctr->nfull, w.inc_list, &wk.ctr->ninc, w.tags, w.slots, w.gn_p,
-                                                   w.gn_q, w.gn_rec, w.gn_rec + (size_t)max_rows * 928, stream)))
+                                                   w.gn_q, w.gn_rec, w.gn_rec + (size_t)max_rows * 928, &wk.ctr->ihead,
+                                                   stream)))
                 return r;
             if (check) {
                 if ((r = gz_gn_forward(d_gn_weights, w.gn_in, max_rows, &wk.ctr->rows, w.chk_p, w.chk_q, nullptr,
