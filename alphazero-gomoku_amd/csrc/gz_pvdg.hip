@@ -105,7 +105,7 @@ struct K {
     static constexpr int U = HIST + 2 * NPASS * NKEY * 4;  // units
     static constexpr int CST = U + C * 128;        // BN scales of the 4 residual layers [4][128], the 1x1 head
     static constexpr int CST_FLOATS = 4 * 128 + 3 * 128 + 4;  // weights [3][128], the 3 head biases
-    static constexpr int POS = CST + CST_FLOATS * 4;  // the chunk's first list entry (int)
+    static constexpr int POS = CST + CST_FLOATS * 4;  // the chunk's first list entry and its queue's end (int)
     static constexpr int LDS = POS + 16;
 };
 static_assert(dgk_npos(0) <= K::MAXNPOS && dgk_npos(1) <= K::MAXNPOS && dgk_npos(2) == K::MAXNPOS &&
@@ -822,13 +822,13 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
     const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
-    const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
-    // the XCD's chunks are taken from its queue head in turn (a workgroup that finishes
-    // early takes more: no static share, no tail); lane 0 of wave 0 holds the next
-    // chunk's claim, made one chunk ahead so that the atomic's latency is hidden
-    int* const head = A.queue + xcd;
-    int claim = 0;
-    if (threadIdx.x == 0) claim = atomicAdd(head, K::C);
+    // The XCD's chunks are taken from its queue head in turn (a workgroup that finishes
+    // early takes more: no static share, no tail); once the XCD's eighth is exhausted its
+    // workgroups help the other XCDs (q = xcd + 1, ...), so no XCD finishes last alone.
+    // Thread 0 holds the claim (queue q, offset), made one chunk ahead so that the
+    // atomic's latency is hidden, and publishes each chunk's (first entry, end) in LDS.
+    int q = 0, claim = 0;
+    if (threadIdx.x == 0) claim = atomicAdd(A.queue + xcd, K::C);
     _Float16* myscr = scratch + (size_t)blockIdx.x * SCR_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave;
@@ -849,11 +849,22 @@ __global__ __launch_bounds__(NTD, K::WPS) void pv_dg_kernel(DgArgs A, _Float16* 
     for (;;) {
         __syncthreads();  // the previous chunk's readers of U, hpart, the tables and POS are done
         if (threadIdx.x == 0) {
-            *(int*)(lds + K::POS) = xb + claim;
-            if (xb + claim < xe) claim = atomicAdd(head, K::C);
+            int pb = count, pe = count;  // (none left: the loop ends)
+            for (;;) {
+                const int qx = (xcd + q) % nx, xb = qx * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+                if (xb + claim < xe) {
+                    pb = xb + claim, pe = xe;
+                    claim = atomicAdd(A.queue + qx, K::C);
+                    break;
+                }
+                if (++q == nx) break;
+                claim = atomicAdd(A.queue + (xcd + q) % nx, K::C);
+            }
+            ((int*)(lds + K::POS))[0] = pb;
+            ((int*)(lds + K::POS))[1] = pe;
         }
         __syncthreads();
-        const int pos = *(const int*)(lds + K::POS);
+        const int pos = ((const int*)(lds + K::POS))[0], xe = ((const int*)(lds + K::POS))[1];
         if (pos >= xe) break;
         const int ng = xe - pos < K::C ? xe - pos : K::C;
         if (wave == 0 && lane < ng) {

@@ -802,12 +802,10 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     const int xcd = blockIdx.x % nx, per = gridDim.x / nx, k = blockIdx.x / nx;
     if (k >= per) return;
     const int xchunk = (count + nx - 1) / nx;
-    const int xb = xcd * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
-    // the XCD's chunks from its queue head in turn (pv_dg_kernel's scheme: no static
-    // share, no tail); thread 0 claims one chunk ahead
-    int* const head = A.queue + xcd;
-    int claim = 0;
-    if (threadIdx.x == 0) claim = atomicAdd(head, SIB_G);
+    // the XCD's chunks from its queue head in turn, then the other XCDs' (pv_dg_kernel's
+    // scheme: no static share, no tail); thread 0 claims one chunk ahead
+    int q = 0, claim = 0;
+    if (threadIdx.x == 0) claim = atomicAdd(A.queue + xcd, SIB_G);
     _Float16* myscr = scratch + (size_t)blockIdx.x * SIB_G * PATCH_HALVES;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), np = wave & 3, mh = wave >> 2;
@@ -837,11 +835,22 @@ __global__ __launch_bounds__(NTS, 1) void pv_sib_kernel(TreeArgs A, _Float16* __
     for (;;) {
         __syncthreads();  // the previous chunk's readers of U and the chunk entry are done
         if (threadIdx.x == 0) {
-            *(int*)(lds + SIB_POS) = xb + claim;
-            if (xb + claim < xe) claim = atomicAdd(head, SIB_G);
+            int pb = count, pe = count;  // (none left: the loop ends)
+            for (;;) {
+                const int qx = (xcd + q) % nx, xb = qx * xchunk, xe = xb + xchunk < count ? xb + xchunk : count;
+                if (xb + claim < xe) {
+                    pb = xb + claim, pe = xe;
+                    claim = atomicAdd(A.queue + qx, SIB_G);
+                    break;
+                }
+                if (++q == nx) break;
+                claim = atomicAdd(A.queue + (xcd + q) % nx, SIB_G);
+            }
+            ((int*)(lds + SIB_POS))[0] = pb;
+            ((int*)(lds + SIB_POS))[1] = pe;
         }
         __syncthreads();
-        const int pos = *(const int*)(lds + SIB_POS);
+        const int pos = ((const int*)(lds + SIB_POS))[0], xe = ((const int*)(lds + SIB_POS))[1];
         if (pos >= xe) break;
         const int ng = xe - pos < SIB_G ? xe - pos : SIB_G;
         SibUnit* const U = U0;
