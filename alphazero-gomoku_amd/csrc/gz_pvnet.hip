@@ -698,9 +698,97 @@ constexpr int NTH_H = 256;
 constexpr int LG_STRIDE = 228;
 static_assert(HP_K == 16 * PF_KB && HV_K == 16 * V1_KB && HP_K % 16 == 0 && HV_K % 16 == 0 && HV_OFF % 4 == 0 && HSTRIDE % 4 == 0, "16-B A loads");
 
+// The f16x3 tower's heads run the same two GEMMs on v_mfma_f32_16x16x32_f16 with the
+// 3-product split (a_hi w_hi + a_hi w_lo + a_lo w_hi): 32-deep k-blocks, lane group g
+// multiplying k = 32 kb + 8 g + j (j < 8) of its board row (A) and its output column (B).
+// The B fragments -- policy_fc / value_fc1 x 2^8 (exact; it keeps the small weights' lo
+// halves out of fp16's subnormals), split into fp16 hi / lo -- are cut from the fp32
+// fragments once per forward (pv_heads_pack_kernel) into the workspace: [kb][n-tile][lane]
+// [8] hi plane, then the lo plane.  The exact-fp32 path keeps the fp32-MFMA heads.
+constexpr int HF_PKB = 15, HF_VKB = 8;  // k-blocks: policy 480 >= 450 inputs, value 256 >= 225
+constexpr int HF_VAL = HF_PKB * PF_NT * 64 * 8;           // halves: value_fc1's fragments
+constexpr int HF_PLANE = HF_VAL + HF_VKB * V1_NT * 64 * 8;  // halves per plane (hi, lo)
+constexpr size_t HF_BYTES = 2 * (size_t)HF_PLANE * sizeof(_Float16);
+constexpr float HF_SCALE = 256.f, HF_UNSCALE = 1.f / 256.f;
+static_assert(HF_PKB * 32 >= HP_K - 8 && HF_VKB * 32 >= HV_K, "k-blocks");
+
+__global__ __launch_bounds__(256) void pv_heads_pack_kernel(const float* __restrict__ W, _Float16* __restrict__ hf) {
+    constexpr int NPF = HF_PKB * PF_NT * 64, NV = HF_VKB * V1_NT * 64;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= NPF + NV) return;
+    const bool pol = i < NPF;
+    const int f = pol ? i : i - NPF, nts = pol ? PF_NT : V1_NT, kb16max = pol ? PF_KB : V1_KB;
+    const float* Wp = W + (pol ? PF_P : V1_P);
+    const int lane = f & 63, nt = (f >> 6) % nts, kb = (f >> 6) / nts, li = lane & 15, g = lane >> 4;
+    h8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int k = 32 * kb + 8 * g + j, kb16 = k >> 4, r = k & 15;
+        float v = kb16 < kb16max ? Wp[(((size_t)kb16 * nts + nt) * 64 + li + 16 * (r >> 2)) * 4 + (r & 3)] : 0.f;
+        v *= HF_SCALE;
+        hi[j] = (_Float16)v;
+        lo[j] = (_Float16)(v - (float)hi[j]);
+    }
+    _Float16* o = hf + (pol ? 0 : HF_VAL) + (size_t)f * 8;
+    *(h8*)o = hi;
+    *(h8*)(o + HF_PLANE) = lo;
+}
+
+// KB 32-deep k-blocks of the f16x3 heads GEMM over 4 board tiles and the wave's n-tiles
+// nt[0..ntn); A from the boards' rows (k >= klim read as 0), B from the packed fragments
+template <int KB>
+__device__ __forceinline__ void heads_gemm_f16x3(const _Float16* __restrict__ hf, int ntiles, int klim, int lane,
+                                                 const int (&nt)[4], int ntn, f32x4 (&acc)[4][4],
+                                                 const float* __restrict__ arow[4]) {
+    const int g = lane >> 4;
+#pragma unroll 1
+    for (int kb = 0; kb < KB; kb++) {
+        const int k0 = 32 * kb + 8 * g;
+        h8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            f32x4 x0 = zero4(), x1 = zero4();
+            if (k0 < klim) {
+                x0 = *(const f32x4*)(arow[m] + k0);
+                x1 = *(const f32x4*)(arow[m] + k0 + 4);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                ah[m][j] = (_Float16)x0[j];
+                al[m][j] = (_Float16)(x0[j] - (float)ah[m][j]);
+                ah[m][4 + j] = (_Float16)x1[j];
+                al[m][4 + j] = (_Float16)(x1[j] - (float)ah[m][4 + j]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (q >= ntn) continue;
+            const _Float16* b = hf + (((size_t)kb * ntiles + nt[q]) * 64 + lane) * 8;
+            bh[q] = *(const h8*)b;
+            bl[q] = *(const h8*)(b + HF_PLANE);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (q >= ntn) continue;
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh[q], acc[m][q], 0, 0, 0);
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bl[q], acc[m][q], 0, 0, 0);
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh[q], acc[m][q], 0, 0, 0);
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (q < ntn) acc[m][q] = acc[m][q] * HF_UNSCALE;
+}
+
+// hf == nullptr: the fp32-MFMA GEMMs (exact f32 products); else the f16x3 ones
 __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restrict__ W, const float* __restrict__ hbuf,
                                                            int n, const int32_t* d_count, float* __restrict__ logits,
-                                                           float* __restrict__ value, float* __restrict__ probs) {
+                                                           float* __restrict__ value, float* __restrict__ probs,
+                                                           const _Float16* __restrict__ hf) {
     __shared__ float lg[HB * LG_STRIDE];
     __shared__ float h1[HB * 64];
     const int count = board_count(n, d_count);
@@ -729,8 +817,11 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
         for (int m = 0; m < 4; m++)
 #pragma unroll
             for (int q = 0; q < 4; q++) acc[m][q] = zero4();
-        for (int kb = 0; kb < HP_K / 16; kb++)
-            heads_gemm_block(W + PF_P, PF_NT, kb, lane, nt, ntn, acc, arow);
+        if (hf)
+            heads_gemm_f16x3<HF_PKB>(hf, PF_NT, HP_K, lane, nt, ntn, acc, arow);
+        else
+            for (int kb = 0; kb < HP_K / 16; kb++)
+                heads_gemm_block(W + PF_P, PF_NT, kb, lane, nt, ntn, acc, arow);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (q >= ntn) continue;
@@ -751,8 +842,11 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
         f32x4 acc[4][4];
 #pragma unroll
         for (int m = 0; m < 4; m++) acc[m][0] = zero4();
-        for (int kb = 0; kb < HV_K / 16; kb++)
-            heads_gemm_block(W + V1_P, V1_NT, kb, lane, nt, 1, acc, arv);
+        if (hf)
+            heads_gemm_f16x3<HF_VKB>(hf + HF_VAL, V1_NT, HV_K, lane, nt, 1, acc, arv);
+        else
+            for (int kb = 0; kb < HV_K / 16; kb++)
+                heads_gemm_block(W + V1_P, V1_NT, kb, lane, nt, 1, acc, arv);
         const int j = 16 * wave + li;
         const float bias = W[V1_B + j];
 #pragma unroll
@@ -918,11 +1012,23 @@ static int pv_grid(int n) {
     return n < cus ? n : cus;
 }
 
+// f16x3: the tower -> heads records, then the heads' fp16 fragments (HF_BYTES)
+static size_t pv_hf_offset(int32_t n) { return ((size_t)(n < 1 ? 1 : n) * HSTRIDE * sizeof(float) + 255) & ~(size_t)255; }
+
 extern "C" size_t gz_pv_workspace_bytes(int32_t n) {
     const int grid = pv_grid(n < 1 ? 1 : n);
     const size_t slab = (size_t)grid * (NT32 / 64) * SLAB_F * sizeof(float);  // fp32 kernel
-    const size_t heads = (size_t)(n < 1 ? 1 : n) * HSTRIDE * sizeof(float);    // f16x3: tower -> heads
+    const size_t heads = pv_hf_offset(n) + HF_BYTES;
     return slab > heads ? slab : heads;
+}
+
+static void pv_heads_launch(const float* d_weights, const float* hbuf, int32_t n, const int32_t* d_count,
+                            float* d_logits, float* d_value, float* d_probs, _Float16* hf, hipStream_t s) {
+    if (hf) {
+        constexpr int NF = HF_PKB * PF_NT * 64 + HF_VKB * V1_NT * 64;
+        pv_heads_pack_kernel<<<(NF + 255) / 256, 256, 0, s>>>(d_weights, hf);
+    }
+    pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, hbuf, n, d_count, d_logits, d_value, d_probs, hf);
 }
 
 extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, int32_t n, const int32_t* d_count,
@@ -954,8 +1060,8 @@ extern "C" int gz_pv_forward(const float* d_weights, const uint32_t* d_boards, i
     {
         pv_kernel_f16x3<false, false><<<grid, NT16, 0, s>>>(d_weights, d_boards, n, d_count, (float*)d_workspace, nullptr,
                                                      nullptr, nullptr, nullptr, 0);
-        pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, (const float*)d_workspace, n, d_count,
-                                                           d_logits, d_value, d_probs);
+        pv_heads_launch(d_weights, (const float*)d_workspace, n, d_count, d_logits, d_value, d_probs,
+                        (_Float16*)((char*)d_workspace + pv_hf_offset(n)), s);
     }
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
     hipError_t e = hipGetLastError();
@@ -992,6 +1098,7 @@ struct TreeWs {
     float* pres;        // the roots' pre-BN accumulators (pv_dg_kernel)
     _Float16* patches;
     _Float16* scratch;  // pv_sib_kernel / pv_dg_kernel: 12 patch-sized areas per workgroup
+    _Float16* hf;       // the heads' fp16 fragments (HF_BYTES)
 };
 TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     const size_t m = (size_t)(n < 1 ? 1 : n);
@@ -1017,6 +1124,8 @@ TreeWs tree_carve(void* ws, int32_t n, int32_t root_cap) {
     t.patches = (_Float16*)p;
     p += (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16);
     t.scratch = (_Float16*)p;
+    p += (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
+    t.hf = (_Float16*)p;
     return t;
 }
 }  // namespace
@@ -1028,7 +1137,7 @@ extern "C" size_t gz_pv_tree_workspace_bytes(int32_t n, int32_t root_cap) {
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_MAP_HALVES * sizeof(_Float16) +
            (size_t)(root_cap < 0 ? 0 : root_cap) * 4 * PV_PRE_FLOATS * sizeof(float) +
            (size_t)patch_cap_of(root_cap) * PV_PATCH_HALVES * sizeof(_Float16) +
-           (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16);
+           (size_t)pv_grid(1 << 30) * SIB_SCRATCH_HALVES * sizeof(_Float16) + HF_BYTES;
 }
 
 extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boards, const int32_t* d_meta, int32_t n,
@@ -1062,7 +1171,7 @@ extern "C" int gz_pv_forward_tree(const float* d_weights, const uint32_t* d_boar
                                    t.grand, t.ctr + 4, t.cinfo, t.scratch, t.ctr + 8, t.children, t.ctr + 2, grid,
                                    t.pres, t.ctr + 16, stream);
     if (rc) return rc;
-    pv_heads_kernel<<<(n + HB - 1) / HB, NTH_H, 0, s>>>(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs);
+    pv_heads_launch(d_weights, t.hbuf, n, d_count, d_logits, d_value, d_probs, t.hf, s);
     if (d_prior) pv_prior_kernel<<<(n + PR_B - 1) / PR_B, 256, 0, s>>>(d_boards, n, d_count, d_probs, d_prior);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
