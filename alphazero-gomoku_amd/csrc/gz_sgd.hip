@@ -140,6 +140,11 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_conv0_kernel(const float* __re
     __syncthreads();
     const f32x4 bias = *(const f32x4*)(b0 + 4 * q);
     f32x4* yb = (f32x4*)(y + (size_t)b * NPOS * CH) + q;
+    // the thread's channel quad of the 27 weights in registers (read from LDS once: the
+    // loop below was bound by re-reading them per position)
+    f32x4 wr[C0K];
+#pragma unroll
+    for (int kk = 0; kk < C0K; kk++) wr[kk] = *(const f32x4*)(ws + kk * CH + 4 * q);
     f32x4 v[PB_ITEMS], s = zero4(), mx = zero4();
 #pragma unroll
     for (int k = 0; k < PB_ITEMS; k++) {
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_conv0_kernel(const float* __re
             for (int kk = 0; kk < C0K; kk++) {
                 const int ci = kk / 9, tap = kk % 9;
                 const float xv = xs[ci * 289 + (r + tap / 3) * 17 + c + tap % 3];
-                acc += xv * *(const f32x4*)(ws + kk * CH + 4 * q);
+                acc += xv * wr[kk];
             }
             v[k] = acc;
             yb[(size_t)p * 32] = acc;
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_conv0_wgrad_kernel(const float
                                                                     const float* __restrict__ coef,
                                                                     const float* __restrict__ x,
                                                                     float* __restrict__ wpart) {
-    __shared__ f32x4 sh[PB_THREADS];
+    __shared__ f32x4 red7[7][PB_THREADS];
     __shared__ float xs[3 * 17 * 17];
     const int b = blockIdx.x, tid = threadIdx.x, q = tid & 31, h = tid >> 5;
     c0_stage(x, b, xs, tid);
@@ -395,13 +400,26 @@ __global__ __launch_bounds__(PB_THREADS) void sgd_conv0_wgrad_kernel(const float
         }
         acc[C0K] += dy;
     }
+    // the 28 sums over the 8 position strides, 7 at a time through LDS (2 barriers per 7
+    // instead of per sum), stride 0's threads adding the strides in order
     float* o = wpart + (size_t)b * CH * (C0K + 1);
+    constexpr int RB = 7;
+    static_assert((C0K + 1) % RB == 0, "batches");
 #pragma unroll
-    for (int kk = 0; kk <= C0K; kk++) {
-        const f32x4 t = pb_reduce(acc[kk], sh, q, h, false);
+    for (int k0 = 0; k0 <= C0K; k0 += RB) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RB; j++) red7[j][h * 32 + q] = acc[k0 + j];
+        __syncthreads();
         if (h == 0)
 #pragma unroll
-            for (int r = 0; r < 4; r++) o[(4 * q + r) * (C0K + 1) + kk] = t[r];
+            for (int j = 0; j < RB; j++) {
+                f32x4 t = red7[j][q];
+#pragma unroll
+                for (int k = 1; k < PB_STRIDES; k++) t += red7[j][k * 32 + q];
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[(4 * q + r) * (C0K + 1) + k0 + j] = t[r];
+            }
     }
 }
 
