@@ -1061,8 +1061,9 @@ __global__ void tree_lists_kernel(const int32_t* __restrict__ meta, int n, const
 // pv_sib_kernel's work list: the root children in LEAF order (a root's children are
 // adjacent leaves, so neighbouring list entries share a root's maps).  wcount[w] =
 // root children among leaves [64 w, 64 w + 64) (tree_lists_kernel); one workgroup
-// of 1024 threads scans the counts in tiles, then each wave writes its leaves' list
-// entries.  cinfo >= 0 with bit 30 clear marks a root child.
+// of 1024 threads scans the counts in tiles, then (tree_children_scatter_kernel) each
+// group's wave writes its leaves' list entries.  cinfo >= 0 with bit 30 clear marks a
+// root child.
 __global__ __launch_bounds__(1024) void tree_children_kernel(int n, const int32_t* __restrict__ d_count,
                                                             const int32_t* __restrict__ cinfo,
                                                             int32_t* __restrict__ wcount,
@@ -1100,14 +1101,23 @@ __global__ __launch_bounds__(1024) void tree_children_kernel(int n, const int32_
         if (tid == 0) carry += wsum[15];
         __syncthreads();
     }
-    // each wave: its 64-leaf groups, children in lane order at the group's offset
-    for (int w = wv; w < nw; w += 16) {
-        const int i = w * 64 + lane;
-        const int ci = i < count ? cinfo[i] : -1;
-        const bool child = ci >= 0 && !(ci & (1 << 30));
-        const uint64_t m = __ballot(child);
-        if (child) children[wcount[w] + __popcll(m & ((1ull << lane) - 1))] = i;
-    }
+}
+
+// then one wave per 64-leaf group (the loop of 16 waves over the groups was a chain of
+// dependent load latencies, 0.4 ms per forward): the group's children in lane order at its
+// scanned offset
+__global__ __launch_bounds__(1024) void tree_children_scatter_kernel(int n, const int32_t* __restrict__ d_count,
+                                                                    const int32_t* __restrict__ cinfo,
+                                                                    const int32_t* __restrict__ wcount,
+                                                                    int32_t* __restrict__ children) {
+    const int count = d_count ? (*d_count < n ? *d_count : n) : n;
+    const int w = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w * 64 >= count) return;
+    const int i = w * 64 + lane;
+    const int ci = i < count ? cinfo[i] : -1;
+    const bool child = ci >= 0 && !(ci & (1 << 30));
+    const uint64_t m = __ballot(child);
+    if (child) children[wcount[w] + __popcll(m & ((1ull << lane) - 1))] = i;
 }
 
 // the grandchild list in PARENT order: one thread per leaf; a parent with a patch
@@ -1170,6 +1180,7 @@ extern "C" int gz_internal_tree_classify(const int32_t* d_meta, int32_t n, const
     tree_lists_kernel<<<g, 256, 0, s>>>(d_meta, n, d_count, d_ord, d_pslot, d_boards, d_ctr, d_roots, d_full, d_ghead,
                                         d_gnext, d_cinfo, wcount);
     tree_children_kernel<<<1, 1024, 0, s>>>(n, d_count, d_cinfo, wcount, d_children);
+    tree_children_scatter_kernel<<<(n + 1023) / 1024, 1024, 0, s>>>(n, d_count, d_cinfo, wcount, d_children);
     tree_grand_order_kernel<<<g, 256, 0, s>>>(n, d_count, d_pslot, d_ghead, d_gnext, d_ctr, d_grand);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
