@@ -734,32 +734,41 @@ __global__ __launch_bounds__(256) void pv_heads_pack_kernel(const float* __restr
     *(h8*)(o + HF_PLANE) = lo;
 }
 
-// KB 32-deep k-blocks of the f16x3 heads GEMM over 4 board tiles and the wave's n-tiles
-// nt[0..ntn); A from the boards' rows (k >= klim read as 0), B from the packed fragments
+// KB 32-deep k-blocks of the f16x3 heads GEMM over the workgroup's 4 board tiles and the
+// wave's n-tiles nt[0..ntn).  The A operand is split once per workgroup: thread t takes 8
+// k of board t / 4 (its row srow, k >= klim read as 0) into hi / lo fragments in LDS
+// (stage: 2 buffers x [hi, lo] x 256 fragments, 16 KB), so the 4 waves do not each split
+// the same rows; the next k-block is split while this one's MFMAs run (one barrier per block)
 template <int KB>
-__device__ __forceinline__ void heads_gemm_f16x3(const _Float16* __restrict__ hf, int ntiles, int klim, int lane,
-                                                 const int (&nt)[4], int ntn, f32x4 (&acc)[4][4],
-                                                 const float* __restrict__ arow[4]) {
-    const int g = lane >> 4;
+__device__ __forceinline__ void heads_gemm_f16x3(const _Float16* __restrict__ hf, int ntiles, int klim,
+                                                 const float* __restrict__ srow, h8* stage, int tid, int lane,
+                                                 const int (&nt)[4], int ntn, f32x4 (&acc)[4][4]) {
+    const int li = lane & 15, g = lane >> 4, kq = tid & 3;
+    auto split = [&](int kb, int buf) {
+        const int k0 = 32 * kb + 8 * kq;
+        f32x4 x0 = zero4(), x1 = zero4();
+        if (k0 < klim) {
+            x0 = *(const f32x4*)(srow + k0);
+            x1 = *(const f32x4*)(srow + k0 + 4);
+        }
+        h8 vh, vl;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            vh[j] = (_Float16)x0[j];
+            vl[j] = (_Float16)(x0[j] - (float)vh[j]);
+            vh[4 + j] = (_Float16)x1[j];
+            vl[4 + j] = (_Float16)(x1[j] - (float)vh[4 + j]);
+        }
+        stage[buf * 512 + tid] = vh;  // fragment (board, kq) = tid: board 16 m + li, kq = g
+        stage[buf * 512 + 256 + tid] = vl;
+    };
+    split(0, 0);
+    __syncthreads();
 #pragma unroll 1
     for (int kb = 0; kb < KB; kb++) {
-        const int k0 = 32 * kb + 8 * g;
-        h8 ah[4], al[4], bh[4], bl[4];
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            f32x4 x0 = zero4(), x1 = zero4();
-            if (k0 < klim) {
-                x0 = *(const f32x4*)(arow[m] + k0);
-                x1 = *(const f32x4*)(arow[m] + k0 + 4);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                ah[m][j] = (_Float16)x0[j];
-                al[m][j] = (_Float16)(x0[j] - (float)ah[m][j]);
-                ah[m][4 + j] = (_Float16)x1[j];
-                al[m][4 + j] = (_Float16)(x1[j] - (float)ah[m][4 + j]);
-            }
-        }
+        const int buf = kb & 1;
+        if (kb + 1 < KB) split(kb + 1, buf ^ 1);
+        h8 bh[4], bl[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (q >= ntn) continue;
@@ -768,14 +777,17 @@ __device__ __forceinline__ void heads_gemm_f16x3(const _Float16* __restrict__ hf
             bl[q] = *(const h8*)(b + HF_PLANE);
         }
 #pragma unroll
-        for (int m = 0; m < 4; m++)
+        for (int m = 0; m < 4; m++) {
+            const h8 ah = stage[buf * 512 + (16 * m + li) * 4 + g], al = stage[buf * 512 + 256 + (16 * m + li) * 4 + g];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (q >= ntn) continue;
-                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh[q], acc[m][q], 0, 0, 0);
-                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bl[q], acc[m][q], 0, 0, 0);
-                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh[q], acc[m][q], 0, 0, 0);
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[q], acc[m][q], 0, 0, 0);
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[q], acc[m][q], 0, 0, 0);
+                acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[q], acc[m][q], 0, 0, 0);
             }
+        }
+        __syncthreads();  // every wave is done with buffer buf before it is split into again
     }
 #pragma unroll
     for (int m = 0; m < 4; m++)
@@ -789,8 +801,9 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
                                                            int n, const int32_t* d_count, float* __restrict__ logits,
                                                            float* __restrict__ value, float* __restrict__ probs,
                                                            const _Float16* __restrict__ hf) {
-    __shared__ float lg[HB * LG_STRIDE];
-    __shared__ float h1[HB * 64];
+    __shared__ __attribute__((aligned(16))) float lg[HB * LG_STRIDE];  // (the policy GEMM's A stage before)
+    __shared__ __attribute__((aligned(16))) float h1[HB * 64];         // (the value GEMM's A stage before)
+    static_assert(HB == 64 && HB * LG_STRIDE * 4 >= 16384 && HB * 64 * 4 >= 16384, "A stages");
     const int count = board_count(n, d_count);
     const int b0 = blockIdx.x * HB;
     if (b0 >= count) return;
@@ -817,9 +830,11 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
         for (int m = 0; m < 4; m++)
 #pragma unroll
             for (int q = 0; q < 4; q++) acc[m][q] = zero4();
-        if (hf)
-            heads_gemm_f16x3<HF_PKB>(hf, PF_NT, HP_K, lane, nt, ntn, acc, arow);
-        else
+        if (hf) {
+            const int sb = b0 + (tid >> 2);
+            heads_gemm_f16x3<HF_PKB>(hf, PF_NT, HP_K, hbuf + (size_t)(sb < count ? sb : count - 1) * HSTRIDE,
+                                     (h8*)lg, tid, lane, nt, ntn, acc);
+        } else
             for (int kb = 0; kb < HP_K / 16; kb++)
                 heads_gemm_block(W + PF_P, PF_NT, kb, lane, nt, ntn, acc, arow);
 #pragma unroll
@@ -842,9 +857,12 @@ __global__ __launch_bounds__(NTH_H, 2) void pv_heads_kernel(const float* __restr
         f32x4 acc[4][4];
 #pragma unroll
         for (int m = 0; m < 4; m++) acc[m][0] = zero4();
-        if (hf)
-            heads_gemm_f16x3<HF_VKB>(hf + HF_VAL, V1_NT, HV_K, lane, nt, 1, acc, arv);
-        else
+        if (hf) {
+            const int sb = b0 + (tid >> 2);
+            heads_gemm_f16x3<HF_VKB>(hf + HF_VAL, V1_NT, HV_K,
+                                     hbuf + (size_t)(sb < count ? sb : count - 1) * HSTRIDE + HV_OFF, (h8*)h1, tid,
+                                     lane, nt, 1, acc);
+        } else
             for (int kb = 0; kb < HV_K / 16; kb++)
                 heads_gemm_block(W + V1_P, V1_NT, kb, lane, nt, 1, acc, arv);
         const int j = 16 * wave + li;
